@@ -1,0 +1,10 @@
+"""apex.normalization — HIP fused LayerNorm / RMSNorm (NS-03)."""
+from .fused_layer_norm import (FusedLayerNorm, FusedRMSNorm, MixedFusedLayerNorm,
+                               MixedFusedRMSNorm, fused_layer_norm, fused_layer_norm_affine,
+                               fused_rms_norm, fused_rms_norm_affine,
+                               mixed_dtype_fused_layer_norm_affine,
+                               mixed_dtype_fused_rms_norm_affine)
+
+__all__ = ["FusedLayerNorm", "FusedRMSNorm", "MixedFusedLayerNorm", "MixedFusedRMSNorm",
+           "fused_layer_norm", "fused_layer_norm_affine", "fused_rms_norm", "fused_rms_norm_affine",
+           "mixed_dtype_fused_layer_norm_affine", "mixed_dtype_fused_rms_norm_affine"]

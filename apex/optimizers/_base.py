@@ -1,0 +1,78 @@
+"""Shared machinery for the fused optimizers (NS-02).
+
+MI355X-first design points:
+  * one MTPlan per param group, built once and re-validated by pointer in C++;
+  * amp O2 "fused master" mode: the kernel reads the low-precision MODEL grads
+    directly, multiplies by the device-resident inverse loss scale, updates the
+    fp32 MASTER params and writes the low-precision model copy in the same pass
+    (no materialised fp32 master grads, no separate master->model copy kernel);
+  * overflow skip is decided on the device (``noop`` flag), so a training step
+    never synchronises with the host.
+"""
+from __future__ import annotations
+
+import torch
+from torch.optim import Optimizer
+
+from .. import _ext
+from ..multi_tensor_apply import PlanHolder
+
+
+class FusedOptimizerBase(Optimizer):
+    def __init__(self, params, defaults, set_grad_none=True):
+        super().__init__(params, defaults)
+        self.set_grad_none = set_grad_none
+        # amp integration (set by apex.amp when it owns this optimizer)
+        self._amp_model_params = None    # list[list[Tensor]] per group (model copies)
+        self._amp_grad_scale = None      # fp32 [1] device tensor: 1/loss_scale
+        self._amp_noop = None            # int32 [1] device tensor: skip flag
+        self._plans = {}
+
+    # ------------------------------------------------------------------
+    def _plan(self, key, lists):
+        h = self._plans.get(key)
+        if h is None:
+            h = self._plans[key] = PlanHolder()
+        return h.get(lists)
+
+    def _group_tensors(self, gi, group):
+        """Returns (grads, params, model_copies or None) for group gi."""
+        params = [p for p in group["params"]]
+        if self._amp_model_params is not None:
+            models = self._amp_model_params[gi]
+            sel = [(m.grad, p, m) for p, m in zip(params, models) if m.grad is not None]
+            if not sel:
+                return [], [], []
+            g, p, m = zip(*sel)
+            return list(g), list(p), list(m)
+        sel = [(p.grad, p) for p in params if p.grad is not None]
+        if not sel:
+            return [], [], None
+        g, p = zip(*sel)
+        return list(g), list(p), None
+
+    def zero_grad(self, set_to_none: bool | None = None):
+        set_none = self.set_grad_none if set_to_none is None else set_to_none
+        groups = self._amp_model_params if self._amp_model_params is not None else \
+            [g["params"] for g in self.param_groups]
+        for ps in groups:
+            for p in ps:
+                if p.grad is None:
+                    continue
+                if set_none and not getattr(p, "_apex_grad_is_bucket_view", False):
+                    p.grad = None
+                else:
+                    if p.grad.grad_fn is not None:
+                        p.grad.detach_()
+                    else:
+                        p.grad.requires_grad_(False)
+                    p.grad.zero_()
+
+    def _native(self, tensors):
+        return len(tensors) > 0 and _ext.use_native(tensors[0])
+
+    def _grad_scale_args(self):
+        """(scale_tensor_or_None, scale_float)."""
+        if self._amp_grad_scale is not None:
+            return self._amp_grad_scale, 1.0
+        return None, 1.0

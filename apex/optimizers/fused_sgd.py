@@ -1,0 +1,60 @@
+"""FusedSGD (NS-02): momentum / nesterov / weight-decay SGD in one HIP launch per group.
+
+API follows apex.optimizers.FusedSGD:
+``FusedSGD(params, lr, momentum=0., dampening=0., weight_decay=0., nesterov=False,
+wd_after_momentum=False, materialize_master_grads=True, set_grad_none=False)``.
+"""
+from __future__ import annotations
+
+import torch
+
+from ..multi_tensor_apply import ops as mt_ops
+from ._base import FusedOptimizerBase
+
+
+class FusedSGD(FusedOptimizerBase):
+    def __init__(self, params, lr=0.01, momentum=0.0, dampening=0.0, weight_decay=0.0,
+                 nesterov=False, wd_after_momentum=False, materialize_master_grads=True,
+                 set_grad_none=False):
+        if lr < 0.0:
+            raise ValueError(f"Invalid learning rate: {lr}")
+        if momentum < 0.0:
+            raise ValueError(f"Invalid momentum value: {momentum}")
+        if weight_decay < 0.0:
+            raise ValueError(f"Invalid weight_decay value: {weight_decay}")
+        if nesterov and (momentum <= 0 or dampening != 0):
+            raise ValueError("Nesterov momentum requires a momentum and zero dampening")
+        defaults = dict(lr=lr, momentum=momentum, dampening=dampening, weight_decay=weight_decay,
+                        nesterov=nesterov)
+        super().__init__(params, defaults, set_grad_none)
+        self.wd_after_momentum = wd_after_momentum
+        self.materialize_master_grads = materialize_master_grads
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        scale_t, scale_f = self._grad_scale_args()
+        for gi, group in enumerate(self.param_groups):
+            gs, ps, models = self._group_tensors(gi, group)
+            if not gs:
+                continue
+            first_run = False
+            moms = []
+            for p in ps:
+                st = self.state[p]
+                if "momentum_buffer" not in st:
+                    st["momentum_buffer"] = torch.zeros_like(p, dtype=torch.float32)
+                    first_run = True
+                moms.append(st["momentum_buffer"])
+            lists = [gs, ps, moms] + ([models] if models is not None else [])
+            if self._native(gs):
+                self._plan(("sgd", gi), lists).sgd(
+                    float(group["lr"]), float(group["momentum"]), float(group["dampening"]),
+                    float(group["weight_decay"]), bool(group["nesterov"]), first_run,
+                    self.wd_after_momentum, scale_f, scale_t, self._amp_noop)
+            else:
+                mt_ops.multi_tensor_sgd(0, self._amp_noop, lists, group["weight_decay"],
+                                        group["momentum"], group["dampening"], group["lr"],
+                                        group["nesterov"], first_run, self.wd_after_momentum,
+                                        scale_t if scale_t is not None else scale_f)
+        return loss

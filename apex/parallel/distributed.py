@@ -1,0 +1,404 @@
+"""apex.parallel.DistributedDataParallel and Reducer over RCCL (R-15, R-16, R-17, NS-07).
+
+Reference algorithm (apex/parallel/distributed.py:96-351):
+  * params broadcast from rank 0 at construction (:160);
+  * first iteration: record grad-ready order, cut buckets at ``message_size``
+    elements per dtype, all-reduce everything at the end of backward and broadcast
+    rank 0's bucket layout (:176-221);
+  * steady state: a hook per param drops the grad into its bucket; a full bucket that
+    is next in order is all-reduced on a side stream, out-of-order buckets are queued
+    and drained in order (:279-315); the epilogue makes the compute stream wait and
+    checks every bucket fired (:223-233).
+
+MI355X-first redesign (same observable behaviour):
+  * ZERO-COPY buckets: after the first iteration every grad is a VIEW into one
+    persistent flat buffer per dtype laid out in grad-ready order, so a bucket is a
+    contiguous slice (no flatten/unflatten copies, K-04 disappears) and the
+    ``delay_allreduce`` path is ONE all-reduce per dtype;
+  * averaging uses RCCL's native ncclAvg (``ReduceOp.AVG``) when the backend is
+    RCCL ("nccl" on ROCm), so no separate divide kernel;
+  * collectives are issued asynchronously from the backward hooks; RCCL runs them on
+    its own HIP stream, which waits on an event of the compute stream (the
+    reference's ``reduction_stream``) and the end-of-backward callback makes the
+    compute stream wait on every outstanding work handle;
+  * bucket size defaults to the reference's 1e7 elements but is tunable
+    (``message_size`` / ``APEX_DDP_MESSAGE_SIZE``): on 8x MI355X each RCCL channel
+    rides one of 7 xGMI links (~153 GB/s), so buckets of tens of MB keep all
+    channels busy while still starting communication early in backward
+    (``first_bucket_size`` makes the first bucket smaller to start even sooner).
+"""
+from __future__ import annotations
+
+import contextlib
+import os
+from collections import OrderedDict
+
+import torch
+import torch.distributed as dist
+from torch.nn.modules import Module
+
+# ----------------------------------------------------------------------------
+# flat collective helpers (R-17)
+# ----------------------------------------------------------------------------
+
+
+def _is_rccl(group=None) -> bool:
+    try:
+        return dist.get_backend(group) == "nccl"
+    except Exception:
+        return False
+
+
+def _flatten(tensors):
+    return torch.cat([t.contiguous().view(-1) for t in tensors]) if len(tensors) > 1 else \
+        tensors[0].contiguous().view(-1).clone()
+
+
+def _unflatten_copy(flat, tensors):
+    off = 0
+    for t in tensors:
+        n = t.numel()
+        t.copy_(flat[off:off + n].view_as(t))
+        off += n
+
+
+def _all_reduce_avg(flat, group=None, async_op=False, predivide=1.0):
+    world = dist.get_world_size(group)
+    if _is_rccl(group) and predivide == 1.0:
+        return dist.all_reduce(flat, op=dist.ReduceOp.AVG, group=group, async_op=async_op)
+    if predivide != 1.0:
+        flat.mul_(1.0 / predivide)
+    w = dist.all_reduce(flat, group=group, async_op=async_op)
+    post = predivide / world
+    if async_op:
+        return _PostScaleWork(w, flat, post)
+    if post != 1.0:
+        flat.mul_(post)
+    return None
+
+
+class _PostScaleWork:
+    def __init__(self, work, flat, post):
+        self.work, self.flat, self.post = work, flat, post
+
+    def wait(self):
+        self.work.wait()
+        if self.post != 1.0:
+            self.flat.mul_(self.post)
+
+
+def apply_flat_dist_call(bucket, call, extra_args=None, group=None):
+    """Flatten a same-dtype bucket, run ``call`` on it, average after all_reduce,
+    and copy the result back (reference semantics, apex/parallel/distributed.py:11-23)."""
+    coalesced = _flatten(bucket)
+    if call is dist.all_reduce:
+        _all_reduce_avg(coalesced, group)
+    elif extra_args is not None:
+        call(coalesced, *extra_args, group=group) if group is not None else call(coalesced, *extra_args)
+    else:
+        call(coalesced)
+    _unflatten_copy(coalesced, bucket)
+
+
+def flat_dist_call(tensors, call, extra_args=None, group=None):
+    """Group ``tensors`` by dtype/device and apply ``call`` once per group (C1/C2/C4/C7)."""
+    buckets = OrderedDict()
+    for t in tensors:
+        buckets.setdefault((t.dtype, t.device), []).append(t)
+    for bucket in buckets.values():
+        apply_flat_dist_call(bucket, call, extra_args, group)
+
+
+def extract_tensors(maybe_tensor, tensor_list):
+    if torch.is_tensor(maybe_tensor):
+        tensor_list.append(maybe_tensor)
+    else:
+        try:
+            for item in maybe_tensor:
+                extract_tensors(item, tensor_list)
+        except TypeError:
+            return
+
+
+class Reducer:
+    """Manual all-reduce helper (R-16, apex/parallel/distributed.py:52-93).
+
+    ``Reducer(module)`` broadcasts the module's params from rank 0; ``reduce()``
+    averages all present grads across ranks (one collective per dtype). Passing a
+    list of grads instead reduces exactly those tensors.
+    """
+
+    def __init__(self, module_or_grads_list, process_group=None):
+        self.group = process_group
+        if isinstance(module_or_grads_list, Module):
+            self.module = module_or_grads_list
+            flat_dist_call([p.data for p in self.module.parameters()], dist.broadcast, (0,), self.group)
+        else:
+            self.module = None
+            self.grads = []
+            extract_tensors(module_or_grads_list, self.grads)
+
+    def reduce(self):
+        if self.module:
+            grads = [p.grad.data for p in self.module.parameters() if p.grad is not None]
+        else:
+            grads = self.grads
+        if grads:
+            flat_dist_call(grads, dist.all_reduce, group=self.group)
+
+
+# ----------------------------------------------------------------------------
+# DistributedDataParallel
+# ----------------------------------------------------------------------------
+class _Bucket:
+    __slots__ = ("dtype", "flat", "start", "numel", "params", "ready", "work")
+
+    def __init__(self, dtype, flat, start, numel, params):
+        self.dtype, self.flat, self.start, self.numel, self.params = dtype, flat, start, numel, params
+        self.ready = 0
+        self.work = None
+
+    @property
+    def buf(self):
+        return self.flat[self.start:self.start + self.numel]
+
+
+class DistributedDataParallel(Module):
+    """Bucketed, backward-overlapped data parallelism over RCCL.
+
+    Args mirror the reference (apex/parallel/distributed.py:96-124) plus later apex
+    options: ``message_size`` (elements per bucket, default 1e7), ``delay_allreduce``,
+    ``allreduce_always_fp32``, ``gradient_predivide_factor``, ``gradient_average``,
+    ``retain_allreduce_buffers`` (ignored: buffers are always persistent here),
+    ``first_bucket_size``, ``process_group``.
+    """
+
+    def __init__(self, module, message_size=10000000, delay_allreduce=False, shared_param=None,
+                 allreduce_trigger_params=None, retain_allreduce_buffers=False,
+                 allreduce_always_fp32=False, num_allreduce_streams=1,
+                 allreduce_communicators=None, gradient_average=True,
+                 gradient_predivide_factor=1.0, gradient_average_split_factor=None, prof=False,
+                 first_bucket_size=None, process_group=None, broadcast_buffers=True):
+        super().__init__()
+        if shared_param is not None:
+            raise ValueError("shared_param is no longer supported as an option. It was misleadingly "
+                             "named from the start. It turns out overlapping communication with "
+                             "computation should work fine with shared parameters. If you still "
+                             "wish to delay communication to the end of the backward pass, use "
+                             "delay_allreduce=True|False instead.")
+        self.module = module
+        self.group = process_group
+        self.world_size = dist.get_world_size(process_group)
+        self.message_size = int(os.environ.get("APEX_DDP_MESSAGE_SIZE", message_size))
+        self.first_bucket_size = first_bucket_size
+        self.delay_allreduce = delay_allreduce or bool(int(os.environ.get("APEX_DDP_DELAY", "0")))
+        self.allreduce_always_fp32 = allreduce_always_fp32
+        self.gradient_average = gradient_average
+        self.gradient_predivide_factor = gradient_predivide_factor
+        self.broadcast_buffers = broadcast_buffers
+        self.prof = prof
+        backend = dist.get_backend(process_group)
+        self._rccl = backend == "nccl"
+        if self._rccl:
+            for p in module.parameters():
+                if not p.is_cuda:
+                    raise ValueError("RCCL backend requires every parameter on the GPU")
+        self.reduction_stream = torch.cuda.Stream() if (self._rccl and torch.cuda.is_available()) else None
+        self._params = [p for p in module.parameters() if p.requires_grad]
+        self._param_index = {id(p): i for i, p in enumerate(self._params)}
+        self._layout_ready = False
+        self._buckets = []
+        self._flat = {}            # dtype -> flat buffer
+        self._param_bucket = {}    # param idx -> bucket idx
+        self._ready_order = []
+        self._callback_queued = False
+        self._next_bucket = 0
+        self._allreduce_enabled = True
+        self._hooks = []
+        self._sync_params()
+        self._create_hooks()
+
+    # ------------------------------------------------------------ setup
+    def _sync_params(self):
+        if self.world_size == 1:
+            return
+        tensors = [p.data for p in self.module.parameters()]
+        if self.broadcast_buffers:
+            tensors += [b.data for b in self.module.buffers() if b.is_floating_point() or True]
+        if tensors:
+            flat_dist_call(tensors, dist.broadcast, (0,), self.group)
+
+    def _create_hooks(self):
+        for p in self._params:
+            self._hooks.append(p.register_post_accumulate_grad_hook(self._grad_hook))
+
+    def __getstate__(self):
+        attrs = dict(self.__dict__)
+        attrs.pop("reduction_stream", None)  # reference bug fix (distributed.py:168-172)
+        attrs.pop("_hooks", None)
+        return attrs
+
+    def __setstate__(self, state):
+        super().__setstate__(state)
+        self.reduction_stream = torch.cuda.Stream() if self._rccl else None
+        self._hooks = []
+        self._create_hooks()
+
+    # ------------------------------------------------------------ control
+    def enable_allreduce(self):
+        self._allreduce_enabled = True
+
+    def disable_allreduce(self):
+        self._allreduce_enabled = False
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        """Accumulate grads locally (no communication) inside this context."""
+        old = self._allreduce_enabled
+        self._allreduce_enabled = False
+        try:
+            yield
+        finally:
+            self._allreduce_enabled = old
+
+    def forward(self, *inputs, **kwargs):
+        self._callback_queued = False
+        self._next_bucket = 0
+        self._ready_order = []
+        for b in self._buckets:
+            b.ready = 0
+            b.work = None
+        return self.module(*inputs, **kwargs)
+
+    # ------------------------------------------------------------ hooks
+    def _grad_hook(self, p):
+        if not self._allreduce_enabled:
+            return
+        if not self._callback_queued:
+            torch.autograd.Variable._execution_engine.queue_callback(self._end_of_backward)
+            self._callback_queued = True
+        idx = self._param_index[id(p)]
+        if not self._layout_ready or self.delay_allreduce:
+            if not self._layout_ready:
+                self._ready_order.append(idx)
+            else:
+                self._ensure_view(idx, p)
+            return
+        self._ensure_view(idx, p)
+        bi = self._param_bucket[idx]
+        b = self._buckets[bi]
+        b.ready += 1
+        if b.ready > len(b.params):
+            raise RuntimeError("The same param received more than one gradient in one backward "
+                               "pass; shared params must be registered once.")
+        if b.ready == len(b.params) and bi == self._next_bucket:
+            self._launch_ready_in_order()
+
+    def _ensure_view(self, idx, p):
+        v = self._views[idx]
+        g = p.grad
+        if g is None or g.data_ptr() != v.data_ptr():
+            if g is not None:
+                v.copy_(g)
+            else:
+                v.zero_()
+            p.grad = v
+
+    def _launch_ready_in_order(self):
+        while self._next_bucket < len(self._buckets):
+            b = self._buckets[self._next_bucket]
+            if b.ready != len(b.params):
+                break
+            b.work = self._reduce(b.buf, async_op=True)
+            self._next_bucket += 1
+
+    def _reduce(self, buf, async_op):
+        if self.world_size == 1:
+            return None
+        if self.allreduce_always_fp32 and buf.dtype != torch.float32:
+            tmp = buf.float()
+            w = self._reduce_inner(tmp, async_op=False)
+            buf.copy_(tmp)
+            return None
+        return self._reduce_inner(buf, async_op)
+
+    def _reduce_inner(self, buf, async_op):
+        if not self.gradient_average:
+            return dist.all_reduce(buf, group=self.group, async_op=async_op)
+        return _all_reduce_avg(buf, self.group, async_op=async_op,
+                               predivide=self.gradient_predivide_factor)
+
+    def _end_of_backward(self):
+        if not self._layout_ready:
+            self._build_layout()
+            for dt, flat in self._flat.items():
+                self._reduce(flat, async_op=False)
+            self._layout_ready = True
+            return
+        if self.delay_allreduce:
+            for dt, flat in self._flat.items():
+                # any param that produced no grad this step still has a view (zeroed)
+                self._reduce(flat, async_op=False)
+            return
+        # params that did not receive a grad this iteration: treat as ready (zero grads)
+        for b in self._buckets:
+            if b.ready != len(b.params):
+                for idx in b.params:
+                    p = self._params[idx]
+                    if p.grad is None:
+                        self._views[idx].zero_()
+                        p.grad = self._views[idx]
+                b.ready = len(b.params)
+        self._launch_ready_in_order()
+        for b in self._buckets:
+            if b.work is not None:
+                b.work.wait()
+                b.work = None
+        if self._next_bucket != len(self._buckets):
+            raise RuntimeError("In epilogue, next_bucket ({}) != num_buckets ({}). This probably "
+                               "indicates some buckets were not allreduced."
+                               .format(self._next_bucket, len(self._buckets)))
+
+    # ------------------------------------------------------------ layout
+    def _build_layout(self):
+        order = list(self._ready_order)
+        seen = set(order)
+        order += [i for i in range(len(self._params)) if i not in seen]  # never-ready params last
+        if self.world_size > 1:
+            dev = self._params[0].device
+            t = torch.tensor(order, dtype=torch.int64, device=dev if self._rccl else "cpu")
+            dist.broadcast(t, 0, group=self.group)  # C3: rank 0's layout wins
+            order = [int(x) for x in t.tolist()]
+        by_dtype = OrderedDict()
+        for idx in order:
+            p = self._params[idx]
+            by_dtype.setdefault(p.dtype, []).append(idx)
+        self._views = [None] * len(self._params)
+        self._buckets = []
+        self._param_bucket = {}
+        for dt, idxs in by_dtype.items():
+            total = sum(self._params[i].numel() for i in idxs)
+            dev = self._params[idxs[0]].device
+            flat = torch.zeros(total, dtype=dt, device=dev)
+            self._flat[dt] = flat
+            off, start, cur = 0, 0, []
+            limit = self.first_bucket_size or self.message_size
+            for i in idxs:
+                p = self._params[i]
+                n = p.numel()
+                v = flat[off:off + n].view_as(p)
+                if p.grad is not None:
+                    v.copy_(p.grad)
+                p.grad = v
+                p._apex_grad_is_bucket_view = True
+                self._views[i] = v
+                cur.append(i)
+                off += n
+                if off - start >= limit:
+                    self._buckets.append(_Bucket(dt, flat, start, off - start, cur))
+                    start, cur, limit = off, [], self.message_size
+            if cur:
+                self._buckets.append(_Bucket(dt, flat, start, off - start, cur))
+        for bi, b in enumerate(self._buckets):
+            for i in b.params:
+                self._param_bucket[i] = bi
