@@ -91,9 +91,9 @@ struct MTPlan {
     for (int t = 0; t <= ntensors; ++t) q[t] = chunk_off[t];
     q += ntensors + 1;
     for (int c = 0; c < nchunks; ++c) q[c] = chunks[c];
+    // pinned + non_blocking: torch's caching host allocator records the copy's stream
+    // event and will not recycle the staging block before the copy has completed
     meta = host.to(dev, /*non_blocking=*/true);
-    // keep the pinned staging buffer alive until the copy has completed
-    host.record_stream(at::hip::getCurrentHIPStream());
   }
 
   bool matches(const std::vector<std::vector<Tensor>>& lists) const {

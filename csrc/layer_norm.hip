@@ -14,7 +14,7 @@
 namespace apex {
 
 constexpr int kLnBlock = 256;
-constexpr int kRowsPerWaveBwd = 16;
+constexpr int kRowsPerWaveBwd = 4;  // 8192x1024 -> 512 blocks (2/CU)
 
 template <typename T, typename W, int VPT, bool RMS>
 __global__ void __launch_bounds__(kLnBlock) ln_fwd_fast(const T* __restrict__ x,
