@@ -31,7 +31,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("APEX_BENCH_BATCH", 64)),
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("APEX_BENCH_BATCH", 256)),
                     help="per-GPU sequences per step")
     ap.add_argument("--seq", type=int, default=128)
     ap.add_argument("--fp32", action="store_true", help="fp32 (amp O0) reference run")
