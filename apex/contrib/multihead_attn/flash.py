@@ -1,0 +1,85 @@
+"""Autograd wrapper over the MFMA flash-attention kernels (csrc/attention.hip)."""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ... import _ext
+
+
+def _seed_pair(p):
+    if p <= 0.0:
+        return 0, 0
+    # drawn from torch's CPU generator: reproducible under torch.manual_seed, no device sync
+    s = torch.randint(0, 2 ** 62, (2,), dtype=torch.int64)
+    return int(s[0]), int(s[1])
+
+
+class FlashAttnFunc(torch.autograd.Function):
+    """q, k, v: [B, S, H, D] views (D contiguous) -> o [B, Sq, H, D]."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, dropout_p, causal, scale, k_lens):
+        C = _ext.require()
+        seed, offset = _seed_pair(dropout_p)
+        o, lse = C.flash_attn_fwd(q, k, v, bool(causal), float(scale), float(dropout_p), seed, offset,
+                                  k_lens)
+        ctx.save_for_backward(q, k, v, o, lse, k_lens)
+        ctx.cfg = (dropout_p, causal, scale, seed, offset)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        C = _ext.require()
+        q, k, v, o, lse, k_lens = ctx.saved_tensors
+        p, causal, scale, seed, offset = ctx.cfg
+        do = do.contiguous() if do.stride(-1) != 1 else do
+        dq = torch.empty_like(q, memory_format=torch.contiguous_format) if not q.is_contiguous() else torch.empty_like(q)
+        dk = torch.empty_like(k, memory_format=torch.contiguous_format) if not k.is_contiguous() else torch.empty_like(k)
+        dv = torch.empty_like(v, memory_format=torch.contiguous_format) if not v.is_contiguous() else torch.empty_like(v)
+        C.flash_attn_bwd(do, q, k, v, o, lse, dq, dk, dv, bool(causal), float(scale), float(p), seed,
+                         offset, k_lens)
+        return dq, dk, dv, None, None, None, None
+
+
+class FlashAttnPackedFunc(torch.autograd.Function):
+    """qkv: [B, S, 3, H, D] (the fused QKV projection output, consumed in place).
+    The gradient is produced directly in the packed [B, S, 3, H, D] layout (no cat)."""
+
+    @staticmethod
+    def forward(ctx, qkv, dropout_p, causal, scale, k_lens):
+        C = _ext.require()
+        q, k, v = qkv.unbind(2)
+        seed, offset = _seed_pair(dropout_p)
+        o, lse = C.flash_attn_fwd(q, k, v, bool(causal), float(scale), float(dropout_p), seed, offset,
+                                  k_lens)
+        ctx.save_for_backward(qkv, o, lse, k_lens)
+        ctx.cfg = (dropout_p, causal, scale, seed, offset)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        C = _ext.require()
+        qkv, o, lse, k_lens = ctx.saved_tensors
+        p, causal, scale, seed, offset = ctx.cfg
+        if do.stride(-1) != 1 or do.stride(1) % 8 or do.stride(0) % 8 or do.stride(2) % 8:
+            do = do.contiguous()
+        q, k, v = qkv.unbind(2)
+        dqkv = torch.empty(qkv.shape, dtype=qkv.dtype, device=qkv.device)
+        dq, dk, dv = dqkv.unbind(2)
+        C.flash_attn_bwd(do, q, k, v, o, lse, dq, dk, dv, bool(causal), float(scale), float(p), seed,
+                         offset, k_lens)
+        return dqkv, None, None, None, None
+
+
+def flash_attention_packed(qkv, dropout_p=0.0, causal=False, scale=None, k_lens=None):
+    d = qkv.shape[-1]
+    scale = 1.0 / math.sqrt(d) if scale is None else scale
+    return FlashAttnPackedFunc.apply(qkv, float(dropout_p), bool(causal), float(scale), k_lens)
+
+
+def flash_attention(q, k, v, dropout_p=0.0, causal=False, scale=None, k_lens=None):
+    d = q.shape[-1]
+    scale = 1.0 / math.sqrt(d) if scale is None else scale
+    return FlashAttnFunc.apply(q, k, v, float(dropout_p), bool(causal), float(scale), k_lens)

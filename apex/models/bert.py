@@ -87,14 +87,21 @@ class BertSelfAttention(nn.Module):
         self.dense = nn.Linear(c.hidden_size, c.hidden_size)
         self.p_attn = c.attention_probs_dropout_prob
 
-    def forward(self, x, attn_bias):
+    def context(self, x, k_lens):
+        """Attention context [B, S, H] (before the output projection)."""
         B, S, H = x.shape
-        qkv = self.qkv(x).view(B, S, 3, self.h, self.d)
-        ctx = fops.attention_qkv_packed(qkv, attn_bias, self.p_attn if self.training else 0.0)
-        return self.dense(ctx.reshape(B, S, H))
+        qkv = fops.fused_dense(x, self.qkv.weight, self.qkv.bias).view(B, S, 3, self.h, self.d)
+        ctx = fops.attention_qkv_packed(qkv, None, self.p_attn if self.training else 0.0, k_lens=k_lens)
+        return ctx.reshape(B, S, H)
+
+    def forward(self, x, k_lens):
+        return fops.fused_dense(self.context(x, k_lens), self.dense.weight, self.dense.bias)
 
 
 class BertLayer(nn.Module):
+    """Post-LN encoder layer; each sublayer output is ONE fused kernel each way:
+    LN(residual + dropout(x W^T + b)) (csrc/fused_ops.hip bdaln)."""
+
     def __init__(self, c: BertConfig):
         super().__init__()
         self.attention = BertSelfAttention(c)
@@ -103,14 +110,17 @@ class BertLayer(nn.Module):
         self.output = nn.Linear(c.intermediate_size, c.hidden_size)
         self.out_ln = FusedLayerNorm(c.hidden_size, eps=c.layer_norm_eps)
         self.p = c.hidden_dropout_prob
+        self.eps = c.layer_norm_eps
 
-    def forward(self, x, attn_bias):
+    def forward(self, x, k_lens):
         p = self.p if self.training else 0.0
-        a = self.attention(x, attn_bias)
-        x = self.attn_ln(fops.dropout_add(a, x, p))
-        h = fops.linear_gelu(x, self.intermediate.weight, self.intermediate.bias)
-        o = self.output(h)
-        return self.out_ln(fops.dropout_add(o, x, p))
+        ctx = self.attention.context(x, k_lens)
+        d = self.attention.dense
+        x = fops.dense_bias_dropout_add_ln(ctx, d.weight, d.bias, x, self.attn_ln.weight,
+                                           self.attn_ln.bias, p, self.eps)
+        h = fops.dense_gelu(x, self.intermediate.weight, self.intermediate.bias)
+        return fops.dense_bias_dropout_add_ln(h, self.output.weight, self.output.bias, x,
+                                              self.out_ln.weight, self.out_ln.bias, p, self.eps)
 
 
 class BertModel(nn.Module):
@@ -125,11 +135,13 @@ class BertModel(nn.Module):
         if token_type_ids is None:
             token_type_ids = torch.zeros_like(input_ids)
         x = self.embeddings(input_ids, token_type_ids)
-        attn_bias = None
+        # BERT batches are right-padded: the mask is a per-sequence valid length, which the
+        # flash kernel consumes directly (no [B,1,1,S] additive bias tensor)
+        k_lens = None
         if attention_mask is not None:
-            attn_bias = ((1.0 - attention_mask[:, None, None, :].to(x.dtype)) * -10000.0)
+            k_lens = attention_mask.sum(1, dtype=torch.int32)
         for layer in self.layers:
-            x = layer(x, attn_bias)
+            x = layer(x, k_lens)
         pooled = torch.tanh(self.pooler(x[:, 0])) if self.pooler is not None else None
         return x, pooled
 
@@ -165,7 +177,7 @@ class BertForPreTraining(nn.Module):
         sel = seq.reshape(B * S, H).index_select(0, idx)
         t = fops.linear_gelu(sel, self.transform.weight, self.transform.bias)
         t = self.transform_ln(t)
-        logits = F.linear(t, self.bert.embeddings.word_embeddings.weight, self.decoder_bias)
+        logits = fops.fused_dense(t, self.bert.embeddings.word_embeddings.weight, self.decoder_bias)
         labels = masked_lm_labels.reshape(-1)
         mlm = fops.softmax_cross_entropy(logits, labels, ignore_index=-1)
         nsp = fops.softmax_cross_entropy(self.nsp(pooled), next_sentence_labels, ignore_index=-1)

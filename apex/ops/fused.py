@@ -1,8 +1,20 @@
-"""Functional fused ops used by the model zoo.
+"""Functional fused ops used by the model zoo (transformer building blocks).
 
-Each op dispatches to the HIP kernel in apex._C for device tensors (when the kernel
-exists for that shape) and to the PyTorch reference formulation otherwise; the
-reference formulation is what the numerics tests compare against.
+Each op is an autograd Function over the HIP kernels in apex._C for device tensors, and
+the PyTorch reference formulation on CPU (also the numerics reference for the tests):
+
+  fused_dense(x, W, b)                      y = x W^T + b            (bias grad: HIP colsum)
+  dense_gelu(x, W, b)                       y = gelu(x W^T + b)      (bias+GELU fwd/bwd fused,
+                                                                     bias grad folded in)
+  dense_bias_dropout_add_ln(x, W, b, res, gamma, beta, p, eps)
+                                            y = LN(res + dropout(x W^T + b))  (one fused
+                                                                     kernel each way)
+  bias_dropout_add(x, b, res, p)            y = res + dropout(x + b)
+  attention_qkv_packed / softmax_cross_entropy
+
+GEMMs are plain library GEMMs (hipBLASLt through torch); everything around them is ours.
+Dropout masks are regenerated from a Philox seed drawn from torch's CPU generator, so
+results are reproducible under ``torch.manual_seed`` and no mask tensor is stored.
 """
 from __future__ import annotations
 
@@ -11,24 +23,28 @@ import torch.nn.functional as F
 
 from .. import _ext
 
+ACT_GELU, ACT_GELU_TANH, ACT_RELU, ACT_NONE = 0, 1, 2, 3
 
-def attention_qkv_packed(qkv, attn_bias=None, dropout_p=0.0, causal=False, scale=None):
+
+def _seed():
+    s = torch.randint(0, 2 ** 62, (2,), dtype=torch.int64)
+    return int(s[0]), int(s[1])
+
+
+def _native(*ts):
+    return _ext.use_native(*ts)
+
+
+def _2d(x):
+    return x.reshape(-1, x.shape[-1])
+
+
+# ---------------------------------------------------------------------------
+def attention_qkv_packed(qkv, attn_bias=None, dropout_p=0.0, causal=False, scale=None, k_lens=None):
     """qkv: [B, S, 3, h, d] -> context [B, S, h, d]."""
     from ..contrib.multihead_attn import attention as _attn
 
-    return _attn.attention_packed(qkv, attn_bias, dropout_p, causal, scale)
-
-
-def dropout_add(x, residual, p, training=True):
-    """residual + dropout(x)."""
-    if p > 0.0 and training:
-        return residual + F.dropout(x, p, True)
-    return residual + x
-
-
-def linear_gelu(x, weight, bias):
-    """gelu(x @ W^T + b) (erf GELU, as in BERT/GPT-2 exact formulations)."""
-    return F.gelu(F.linear(x, weight, bias))
+    return _attn.attention_packed(qkv, attn_bias, dropout_p, causal, scale, k_lens)
 
 
 def softmax_cross_entropy(logits, labels, ignore_index=-100, smoothing=0.0, reduction="mean"):
@@ -36,3 +52,173 @@ def softmax_cross_entropy(logits, labels, ignore_index=-100, smoothing=0.0, redu
     from ..contrib.xentropy import softmax_xentropy
 
     return softmax_xentropy(logits, labels, smoothing, ignore_index, reduction)
+
+
+# ---------------------------------------------------------------------------
+class _FusedDense(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        x2 = _2d(x)
+        y = torch.addmm(b, x2, w.t()) if b is not None else torch.mm(x2, w.t())
+        ctx.save_for_backward(x2, w)
+        ctx.has_b = b is not None
+        ctx.bdtype = b.dtype if b is not None else None
+        return y.view(*x.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w = ctx.saved_tensors
+        dy2 = _2d(dy).contiguous()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.mm(dy2, w).view(*dy.shape[:-1], w.shape[1])
+        if ctx.needs_input_grad[1]:
+            dw = torch.mm(dy2.t(), x2)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = _ext.require().colsum(dy2, ctx.bdtype)
+        return dx, dw, db
+
+
+def fused_dense(x, weight, bias=None):
+    if _native(x) and x.shape[-1] % 8 == 0 and weight.shape[0] % 8 == 0:
+        return _FusedDense.apply(x, weight, bias)
+    return F.linear(x, weight, bias)
+
+
+class _DenseAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, act):
+        C = _ext.require()
+        x2 = _2d(x)
+        h = torch.mm(x2, w.t())
+        y = C.bias_act_fwd(h, b, act)
+        ctx.save_for_backward(x2, w, h, b)
+        ctx.act = act
+        return y.view(*x.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = _ext.require()
+        x2, w, h, b = ctx.saved_tensors
+        dh, db = C.bias_act_bwd(_2d(dy), h, b, ctx.act)
+        dx = torch.mm(dh, w).view(*dy.shape[:-1], w.shape[1]) if ctx.needs_input_grad[0] else None
+        dw = torch.mm(dh.t(), x2) if ctx.needs_input_grad[1] else None
+        return dx, dw, (db if b is not None else None), None
+
+
+def _act_ref(h, act):
+    if act == ACT_GELU:
+        return F.gelu(h)
+    if act == ACT_GELU_TANH:
+        return F.gelu(h, approximate="tanh")
+    if act == ACT_RELU:
+        return F.relu(h)
+    return h
+
+
+def dense_act(x, weight, bias, act=ACT_GELU):
+    if _native(x) and weight.shape[0] % 8 == 0:
+        return _DenseAct.apply(x, weight, bias, act)
+    return _act_ref(F.linear(x, weight, bias), act)
+
+
+def dense_gelu(x, weight, bias):
+    return dense_act(x, weight, bias, ACT_GELU)
+
+
+def linear_gelu(x, weight, bias):
+    """gelu(x @ W^T + b) (erf GELU, as in BERT)."""
+    return dense_act(x, weight, bias, ACT_GELU)
+
+
+class _BiasAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, b, act):
+        C = _ext.require()
+        h2 = _2d(h).contiguous()
+        y = C.bias_act_fwd(h2, b, act)
+        ctx.save_for_backward(h2, b)
+        ctx.act = act
+        return y.view_as(h)
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = _ext.require()
+        h2, b = ctx.saved_tensors
+        dh, db = C.bias_act_bwd(_2d(dy), h2, b, ctx.act)
+        return dh.view_as(dy), (db if b is not None else None), None
+
+
+def bias_gelu(h, bias):
+    if _native(h) and h.shape[-1] % 8 == 0:
+        return _BiasAct.apply(h, bias, ACT_GELU)
+    return F.gelu(h + bias)
+
+
+# ---------------------------------------------------------------------------
+class _DenseBDALN(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, res, gamma, beta, p, eps):
+        C = _ext.require()
+        x2 = _2d(x)
+        t = torch.mm(x2, w.t())
+        seed, off = _seed() if p > 0 else (0, 0)
+        y, s, mean, rstd = C.bdaln_fwd(t, b, _2d(res).contiguous(), gamma, beta, float(eps), float(p),
+                                       seed, off)
+        ctx.save_for_backward(x2, w, s, gamma, mean, rstd)
+        ctx.cfg = (p, seed, off, b is not None)
+        return y.view(*x.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = _ext.require()
+        x2, w, s, gamma, mean, rstd = ctx.saved_tensors
+        p, seed, off, has_b = ctx.cfg
+        dres, dt, dg, dbeta, db = C.bdaln_bwd(_2d(dy), s, gamma, mean, rstd, float(p), seed, off, has_b)
+        dx = torch.mm(dt, w).view(*dy.shape[:-1], w.shape[1]) if ctx.needs_input_grad[0] else None
+        dw = torch.mm(dt.t(), x2) if ctx.needs_input_grad[1] else None
+        return dx, dw, (db if has_b else None), dres.view_as(dy), dg, dbeta, None, None
+
+
+def dense_bias_dropout_add_ln(x, weight, bias, residual, gamma, beta, p=0.0, eps=1e-5, training=True):
+    """LayerNorm(residual + dropout(x @ W^T + b)) — BERT's post-LN sublayer output."""
+    p = p if training else 0.0
+    if _native(x) and _ext.require().bdaln_supported(weight.shape[0]) and gamma is not None and \
+            beta is not None:
+        return _DenseBDALN.apply(x, weight, bias, residual, gamma, beta, float(p), float(eps))
+    t = F.linear(x, weight, bias)
+    s = residual + F.dropout(t, p, True) if p > 0 else residual + t
+    return F.layer_norm(s, (s.shape[-1],), gamma, beta, eps)
+
+
+class _BiasDropoutAdd(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, b, res, p):
+        C = _ext.require()
+        seed, off = _seed() if p > 0 else (0, 0)
+        y = C.bias_dropout_add_fwd(_2d(x).contiguous(), b, _2d(res).contiguous(), float(p), seed, off)
+        ctx.cfg = (p, seed, off)
+        ctx.has_b = b is not None
+        ctx.b_like = b
+        return y.view_as(x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = _ext.require()
+        p, seed, off = ctx.cfg
+        dx, db = C.bias_dropout_add_bwd(_2d(dy), float(p), seed, off, ctx.b_like if ctx.has_b else None)
+        return dx.view_as(dy), (db if ctx.has_b else None), dy, None
+
+
+def bias_dropout_add(x, bias, residual, p, training=True):
+    """residual + dropout(x + bias) with bias grad folded into the backward kernel."""
+    p = p if training else 0.0
+    if _native(x) and x.shape[-1] % 8 == 0 and x.shape == residual.shape:
+        return _BiasDropoutAdd.apply(x, bias, residual, float(p))
+    t = x + bias if bias is not None else x
+    return residual + (F.dropout(t, p, True) if p > 0 else t)
+
+
+def dropout_add(x, residual, p, training=True):
+    """residual + dropout(x)."""
+    return bias_dropout_add(x, None, residual, p, training)

@@ -1,0 +1,578 @@
+// Flash attention forward + backward on CDNA4 MFMA (NS-05; apex.contrib.multihead_attn core).
+//
+// Layout: q/k/v/o are [B, S, H, D] views with arbitrary batch / seq strides (so the packed
+// QKV projection output [B, S, 3, H, D] is consumed in place, no split/transposes).
+// D in {64, 128}; bf16 / fp16 in, fp32 accumulate; optional causal mask, per-batch key
+// lengths and Philox dropout regenerated identically in backward.
+//
+// Forward (one workgroup = 4 wave64 = 128 query rows, 32 per wave; K/V streamed in 64-key
+// tiles through LDS):
+//   S^T = K . Q^T with v_mfma_f32_32x32x16 — the swapped product puts ONE query per lane
+//   (16 keys in registers, the other 16 in lane^32), so row max / row sum need a single
+//   cross-half exchange and the rescale factor is lane-local;
+//   O^T += V^T . P^T reuses the S^T accumulator registers directly as the B operand
+//   (k-order permuted to match, no LDS round trip for P); the V^T operand comes from the
+//   row-major V tile with ds_read_b64_tr_b16 (hardware transpose read).
+// Backward (one workgroup = 4 waves x 32 keys = 128 keys; loop over 32-query blocks):
+//   S = Q.K^T and dP = dO.V^T with K, V rows held in registers; dV += P^T.dO and
+//   dK += dS^T.Q use the accumulators as A operands with tr-read B operands from the
+//   Q/dO tiles in LDS; dQ = dS.K goes through LDS (dS) and, when several workgroups
+//   share a query block (Sk > 128), fp32 atomics.
+#include "common.h"
+#include "kernels.h"
+
+namespace apex {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+template <typename T> struct MfmaT;
+template <> struct MfmaT<bf16> {
+  using V8 = bf16x8;
+  __device__ static __forceinline__ f32x16 mma(V8 a, V8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct MfmaT<f16> {
+  using V8 = f16x8;
+  __device__ static __forceinline__ f32x16 mma(V8 a, V8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+  }
+};
+
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+// transposed LDS read: 4 rows x 16 cols block, lane i of each 16-lane group gets column i
+__device__ __forceinline__ s16x4 lds_tr16(const void* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)(p));
+}
+
+template <typename V8>
+__device__ __forceinline__ V8 join4(s16x4 lo, s16x4 hi) {
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(V8, r);
+}
+
+template <typename T, typename V8>
+__device__ __forceinline__ V8 pack8(const float* x) {
+  typedef T t8 __attribute__((ext_vector_type(8)));
+  t8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (T)x[j];
+  return __builtin_bit_cast(V8, r);
+}
+
+// dropout keep-test for element (row, col) of head `bh`: 16-bit uniforms, 8 per Philox call
+struct DropGen {
+  uint64_t seed, offset;
+  uint32_t thresh;  // keep if r16 >= thresh
+  __device__ __forceinline__ uint4 block(int64_t bh, int64_t row, int64_t col8, int64_t Sq) const {
+    Philox ph(seed, (uint64_t)(bh * Sq + row), offset + (uint64_t)col8);
+    return ph.next();
+  }
+  __device__ __forceinline__ static uint32_t r16(const uint4& r, int idx) {
+    const uint32_t w = idx < 2 ? r.x : idx < 4 ? r.y : idx < 6 ? r.z : r.w;
+    return (idx & 1) ? (w >> 16) : (w & 0xffffu);
+  }
+};
+
+constexpr int kFwdWaves = 4;
+constexpr int kFwdBQ = 32 * kFwdWaves;  // 128 query rows per workgroup
+constexpr int kFwdKB = 64;              // keys per tile
+
+template <typename T, int D, bool CAUSAL, bool DROPOUT>
+__global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
+  using M = MfmaT<T>;
+  using V8 = typename M::V8;
+  constexpr int LDR = D + 8;  // padded LDS row (elements)
+  __shared__ __attribute__((aligned(16))) T lds_k[kFwdKB * LDR];
+  __shared__ __attribute__((aligned(16))) T lds_v[kFwdKB * LDR];
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r = lane & 31, hl = lane >> 5;
+  const int bh = blockIdx.y;
+  const int b = bh / a.H, h = bh % a.H;
+  const int q0 = blockIdx.x * kFwdBQ;
+  const int qrow = q0 + 32 * wid + r;
+  const int Sk = a.k_lens ? min(a.k_lens[b], a.Sk) : a.Sk;
+
+  const T* qp = (const T*)a.q + b * a.q_bs + h * a.q_hs;
+  const T* kp = (const T*)a.k + b * a.k_bs + h * a.k_hs;
+  const T* vp = (const T*)a.v + b * a.v_bs + h * a.v_hs;
+
+  // Q^T fragments (B operand): lane (q=r, hl) holds Q[q][16s + 8hl .. +7]
+  V8 qf[D / 16];
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) {
+    if (qrow < a.Sq) qf[s] = *(const V8*)(qp + (int64_t)qrow * a.q_ss + 16 * s + 8 * hl);
+    else qf[s] = V8{};
+  }
+
+  f32x16 o[D / 32];
+#pragma unroll
+  for (int i = 0; i < D / 32; ++i) o[i] = f32x16{};
+  float m = -INFINITY, l = 0.f;
+
+  int kend = Sk;
+  if (CAUSAL) kend = min(kend, q0 + kFwdBQ);
+  const int ntiles = (kend + kFwdKB - 1) / kFwdKB;
+
+  // tile loader: 64 x D elements, 16B chunks, CH chunks per thread
+  constexpr int CPR = D / 8;               // chunks per row
+  constexpr int CH = kFwdKB * CPR / 256;   // chunks per thread per tensor
+  uint4 kreg[CH], vreg[CH];
+  auto gload = [&](int kt) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int idx = threadIdx.x + 256 * c;
+      const int row = idx / CPR, col = (idx % CPR) * 8;
+      const int key = kt * kFwdKB + row;
+      if (key < Sk) {
+        kreg[c] = *(const uint4*)(kp + (int64_t)key * a.k_ss + col);
+        vreg[c] = *(const uint4*)(vp + (int64_t)key * a.v_ss + col);
+      } else {
+        kreg[c] = make_uint4(0, 0, 0, 0);
+        vreg[c] = make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+  auto lstore = [&]() {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int idx = threadIdx.x + 256 * c;
+      const int row = idx / CPR, col = (idx % CPR) * 8;
+      *(uint4*)(lds_k + row * LDR + col) = kreg[c];
+      *(uint4*)(lds_v + row * LDR + col) = vreg[c];
+    }
+  };
+
+  DropGen dg{a.seed, a.offset, a.drop_thresh};
+  const float rkeep = a.drop_scale;
+
+  if (ntiles > 0) gload(0);
+  for (int kt = 0; kt < ntiles; ++kt) {
+    __syncthreads();  // previous tile fully consumed
+    lstore();
+    __syncthreads();
+    if (kt + 1 < ntiles) gload(kt + 1);
+    const int kb = kt * kFwdKB;
+
+    // ---- S^T for two 32-key sub-blocks
+    f32x16 st[2];
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb) {
+      st[sb] = f32x16{};
+#pragma unroll
+      for (int s = 0; s < D / 16; ++s) {
+        const V8 kf = *(const V8*)(lds_k + (32 * sb + r) * LDR + 16 * s + 8 * hl);
+        st[sb] = M::mma(kf, qf[s], st[sb]);
+      }
+    }
+    // ---- scale + mask + running max
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int key = kb + 32 * sb + (i & 3) + 8 * (i >> 2) + 4 * hl;
+        float t = st[sb][i] * a.scale_log2;
+        if (key >= Sk || (CAUSAL && key > qrow)) t = -INFINITY;
+        st[sb][i] = t;
+        tmax = fmaxf(tmax, t);
+      }
+    }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float mnew = fmaxf(m, tmax);
+    const float muse = mnew == -INFINITY ? 0.f : mnew;
+    const float alpha = exp2f(m - muse);
+    m = mnew;
+    float psum = 0.f;
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        uint4 rnd;
+        if (DROPOUT) rnd = dg.block(bh, qrow, (kb + 32 * sb + 8 * g) >> 3, a.Sq);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = 4 * g + e;
+          const float p = exp2f(st[sb][i] - muse);
+          psum += p;
+          float pd = p;
+          if (DROPOUT) pd = DropGen::r16(rnd, 4 * hl + e) >= dg.thresh ? p * rkeep : 0.f;
+          st[sb][i] = pd;
+        }
+      }
+    }
+    l = l * alpha + psum;
+#pragma unroll
+    for (int db = 0; db < D / 32; ++db)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) o[db][i] *= alpha;
+    // ---- O^T += V^T . P^T
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb) {
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        float pv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pv[j] = st[sb][8 * s2 + j];
+        const V8 pf = pack8<T, V8>(pv);
+        const int k0 = 32 * sb + 16 * s2 + 4 * hl + ((lane & 15) >> 2);
+#pragma unroll
+        for (int db = 0; db < D / 32; ++db) {
+          const int c0 = 32 * db + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+          const s16x4 lo = lds_tr16(lds_v + k0 * LDR + c0);
+          const s16x4 hi = lds_tr16(lds_v + (k0 + 8) * LDR + c0);
+          o[db] = M::mma(join4<V8>(lo, hi), pf, o[db]);
+        }
+      }
+    }
+  }
+  // ---- epilogue
+  const float ltot = l + __shfl_xor(l, 32, 64);
+  if (qrow < a.Sq) {
+    const float inv = ltot > 0.f ? 1.f / ltot : 0.f;
+    T* op = (T*)a.o + b * a.o_bs + h * a.o_hs + (int64_t)qrow * a.o_ss;
+#pragma unroll
+    for (int db = 0; db < D / 32; ++db) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        typedef T t4 __attribute__((ext_vector_type(4)));
+        t4 w;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[e] = (T)(o[db][4 * g + e] * inv);
+        *(t4*)(op + 32 * db + 8 * g + 4 * hl) = w;
+      }
+    }
+    if (hl == 0 && a.lse)
+      a.lse[(int64_t)bh * a.Sq + qrow] = ltot > 0.f ? (m + log2f(ltot)) * kLn2 : INFINITY;
+  }
+}
+
+// delta[bh, q] = sum_d dO * O   (fp32)
+template <typename T, int D>
+__global__ void __launch_bounds__(256) attn_bwd_delta_kernel(AttnArgs a, const void* dout,
+                                                            float* delta) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // over B*H*Sq
+  if (row >= (int64_t)a.B * a.H * a.Sq) return;
+  const int q = (int)(row % a.Sq);
+  const int64_t bh = row / a.Sq;
+  const int b = (int)(bh / a.H), h = (int)(bh % a.H);
+  const T* op = (const T*)a.o + b * a.o_bs + h * a.o_hs + (int64_t)q * a.o_ss;
+  const T* dp = (const T*)dout + b * a.do_bs + h * a.do_hs + (int64_t)q * a.do_ss;
+  float s = 0.f;
+  for (int d = lane; d < D; d += 64) s += to_f(op[d]) * to_f(dp[d]);
+  s = wave_sum(s);
+  if (lane == 0) delta[row] = s;
+}
+
+// ---------------------------------------------------------------------------
+// Backward
+// ---------------------------------------------------------------------------
+constexpr int kBwdWaves = 4;
+constexpr int kBwdBK = 32 * kBwdWaves;  // 128 keys per workgroup
+constexpr int kBwdBQ = 32;              // queries per inner step
+
+template <typename T, int D, bool CAUSAL, bool DROPOUT>
+__global__ void __launch_bounds__(256, 1) attn_bwd_kernel(AttnArgs a, const void* dout,
+                                                         const float* delta, float* dq_acc,
+                                                         void* dk_out, void* dv_out) {
+  using M = MfmaT<T>;
+  using V8 = typename M::V8;
+  constexpr int LDR = D + 8;
+  constexpr int LDS_S = kBwdBK + 8;  // dS row stride (elements)
+  __shared__ __attribute__((aligned(16))) T lds_q[kBwdBQ * LDR];
+  __shared__ __attribute__((aligned(16))) T lds_do[kBwdBQ * LDR];
+  __shared__ __attribute__((aligned(16))) T lds_k[kBwdBK * LDR];
+  __shared__ __attribute__((aligned(16))) T lds_ds[kBwdBQ * LDS_S];
+  __shared__ float lds_lse[kBwdBQ], lds_delta[kBwdBQ];
+  __shared__ float lds_dqred[(D == 64) ? 2048 : 1];
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r = lane & 31, hl = lane >> 5;
+  const int bh = blockIdx.y;
+  const int b = bh / a.H, h = bh % a.H;
+  const int k0 = blockIdx.x * kBwdBK;
+  const int Sk = a.k_lens ? min(a.k_lens[b], a.Sk) : a.Sk;
+  const int mykey = k0 + 32 * wid + r;  // key row this lane holds as K/V operand
+
+  const T* qp = (const T*)a.q + b * a.q_bs + h * a.q_hs;
+  const T* kp = (const T*)a.k + b * a.k_bs + h * a.k_hs;
+  const T* vp = (const T*)a.v + b * a.v_bs + h * a.v_hs;
+  const T* dop = (const T*)dout + b * a.do_bs + h * a.do_hs;
+  const float* lsep = a.lse + (int64_t)bh * a.Sq;
+  const float* delp = delta + (int64_t)bh * a.Sq;
+
+  // K and V rows for this wave's 32 keys as B operands: lane (key=r, hl) holds X[key][16s+8hl..]
+  V8 kf[D / 16], vf[D / 16];
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) {
+    if (mykey < Sk) {
+      kf[s] = *(const V8*)(kp + (int64_t)mykey * a.k_ss + 16 * s + 8 * hl);
+      vf[s] = *(const V8*)(vp + (int64_t)mykey * a.v_ss + 16 * s + 8 * hl);
+    } else {
+      kf[s] = V8{};
+      vf[s] = V8{};
+    }
+  }
+  // whole K block to LDS (needed as the B operand of dQ = dS.K via tr reads)
+  for (int idx = threadIdx.x; idx < kBwdBK * (D / 8); idx += 256) {
+    const int row = idx / (D / 8), col = (idx % (D / 8)) * 8;
+    const int key = k0 + row;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (key < Sk) v = *(const uint4*)(kp + (int64_t)key * a.k_ss + col);
+    *(uint4*)(lds_k + row * LDR + col) = v;
+  }
+
+  // accumulators: dK, dV  [key x dim]: C rows = keys (regs), cols = dim (lanes)
+  f32x16 dk[D / 32], dv[D / 32];
+#pragma unroll
+  for (int i = 0; i < D / 32; ++i) {
+    dk[i] = f32x16{};
+    dv[i] = f32x16{};
+  }
+
+  int qstart = 0;
+  if (CAUSAL) qstart = (k0 / kBwdBQ) * kBwdBQ;
+  const int nq = a.Sq;
+  DropGen dg{a.seed, a.offset, a.drop_thresh};
+  const float rkeep = a.drop_scale;
+  const bool single_kblock = (a.Sk <= kBwdBK);
+
+  for (int qb = qstart; qb < nq; qb += kBwdBQ) {
+    __syncthreads();
+    // stage Q, dO tiles (32 x D) + lse/delta
+    for (int idx = threadIdx.x; idx < kBwdBQ * (D / 8); idx += 256) {
+      const int row = idx / (D / 8), col = (idx % (D / 8)) * 8;
+      const int q = qb + row;
+      uint4 qv = make_uint4(0, 0, 0, 0), dv4 = make_uint4(0, 0, 0, 0);
+      if (q < nq) {
+        qv = *(const uint4*)(qp + (int64_t)q * a.q_ss + col);
+        dv4 = *(const uint4*)(dop + (int64_t)q * a.do_ss + col);
+      }
+      *(uint4*)(lds_q + row * LDR + col) = qv;
+      *(uint4*)(lds_do + row * LDR + col) = dv4;
+    }
+    if (threadIdx.x < kBwdBQ) {
+      const int q = qb + threadIdx.x;
+      lds_lse[threadIdx.x] = q < nq ? lsep[q] * kLog2e : INFINITY;
+      lds_delta[threadIdx.x] = q < nq ? delp[q] : 0.f;
+    }
+    __syncthreads();
+
+    // S = Q . K^T  [32 q x 32 keys]: A = Q rows (LDS), B = K rows (regs)
+    f32x16 sacc = f32x16{}, dpacc = f32x16{};
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s) {
+      const V8 qa = *(const V8*)(lds_q + r * LDR + 16 * s + 8 * hl);
+      const V8 da = *(const V8*)(lds_do + r * LDR + 16 * s + 8 * hl);
+      sacc = M::mma(qa, kf[s], sacc);
+      dpacc = M::mma(da, vf[s], dpacc);
+    }
+    // element i: q = qb + (i&3) + 8(i>>2) + 4hl, key = mykey
+    float pd[16], ds[16];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      uint4 rnd;
+      const int qr0 = (g * 8) + 4 * hl;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int i = 4 * g + e;
+        const int qi = qr0 + e;
+        const int q = qb + qi;
+        float t = sacc[i] * a.scale_log2 - lds_lse[qi];
+        bool valid = (mykey < Sk) && (q < nq) && !(CAUSAL && mykey > q);
+        const float p = valid ? exp2f(t) : 0.f;
+        float keep = 1.f;
+        if (DROPOUT) {
+          rnd = dg.block(bh, q, mykey >> 3, a.Sq);
+          keep = DropGen::r16(rnd, mykey & 7) >= dg.thresh ? rkeep : 0.f;
+        }
+        pd[i] = p * keep;                                   // dropped P (for dV)
+        const float dpv = dpacc[i] * keep;                  // dP through dropout
+        ds[i] = p * (dpv - lds_delta[qi]) * a.scale;        // dS (includes softmax scale)
+      }
+    }
+    // dV += P^T . dO : accumulator-as-A (contraction over q = rows), B = dO via tr reads
+    // dK += dS^T . Q : same with Q
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const V8 pa = pack8<T, V8>(pd + 8 * s2);
+      const V8 sa = pack8<T, V8>(ds + 8 * s2);
+      const int kq = 16 * s2 + 4 * hl + ((lane & 15) >> 2);
+#pragma unroll
+      for (int db = 0; db < D / 32; ++db) {
+        const int c0 = 32 * db + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+        const V8 dob = join4<V8>(lds_tr16(lds_do + kq * LDR + c0), lds_tr16(lds_do + (kq + 8) * LDR + c0));
+        const V8 qbf = join4<V8>(lds_tr16(lds_q + kq * LDR + c0), lds_tr16(lds_q + (kq + 8) * LDR + c0));
+        dv[db] = M::mma(pa, dob, dv[db]);
+        dk[db] = M::mma(sa, qbf, dk[db]);
+      }
+    }
+    // dS to LDS as [q][key] (bf16) for dQ = dS . K
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int qi = (i & 3) + 8 * (i >> 2) + 4 * hl;
+      lds_ds[qi * LDS_S + 32 * wid + r] = (T)ds[i];
+    }
+    __syncthreads();
+    // dQ [32 q x D]: waves split the D/32 column blocks and the 128-key contraction:
+    // wave w: column block (w % (D/32)), key range half/quarter when D/32 < 4
+    {
+      constexpr int NCB = D / 32;            // column blocks
+      constexpr int KSPLIT = 4 / NCB;        // waves per column block
+      const int cb = wid % NCB;
+      const int ks = wid / NCB;
+      constexpr int KPER = kBwdBK / KSPLIT;  // keys per wave
+      f32x16 dq = f32x16{};
+#pragma unroll
+      for (int s = 0; s < KPER / 16; ++s) {
+        const int kk = ks * KPER + 16 * s;
+        // A = dS[q=r][keys kk + 8hl .. +7] (row read)
+        const V8 aa = *(const V8*)(lds_ds + r * LDS_S + kk + 8 * hl);
+        // B = K[key][dim]: element j -> key kk + 8hl + j, column dim = 32cb + r  (tr reads,
+        // natural k order: rows kk+8hl+0..3 and +4..7)
+        const int krow = kk + 8 * hl + ((lane & 15) >> 2);
+        const int c0 = 32 * cb + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+        const V8 bb = join4<V8>(lds_tr16(lds_k + krow * LDR + c0), lds_tr16(lds_k + (krow + 4) * LDR + c0));
+        dq = M::mma(aa, bb, dq);
+      }
+      // combine the KSPLIT partial tiles of a column block through LDS (no atomics)
+      if (KSPLIT > 1) {
+        if (ks > 0) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) lds_dqred[((ks - 1) * NCB + cb) * 1024 + i * 64 + lane] = dq[i];
+        }
+        __syncthreads();
+        if (ks == 0) {
+#pragma unroll
+          for (int k2 = 1; k2 < KSPLIT; ++k2)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) dq[i] += lds_dqred[((k2 - 1) * NCB + cb) * 1024 + i * 64 + lane];
+        }
+      }
+      // dq element i: row q = (i&3)+8(i>>2)+4hl, col dim = 32cb + r
+      if (ks == 0) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int q = qb + (i & 3) + 8 * (i >> 2) + 4 * hl;
+          if (q < nq) {
+            float* dst = dq_acc + ((int64_t)bh * a.Sq + q) * D + 32 * cb + r;
+            if (single_kblock) *dst = dq[i];  // sole writer of this (b, h) query block
+            else atomicAdd(dst, dq[i]);
+          }
+        }
+      }
+    }
+  }
+  // write dK, dV: element i of block db -> key = k0 + 32wid + (i&3)+8(i>>2)+4hl, dim = 32db + r
+  T* dkp = (T*)dk_out + b * a.dk_bs + h * a.dk_hs;
+  T* dvp = (T*)dv_out + b * a.dv_bs + h * a.dv_hs;
+#pragma unroll
+  for (int db = 0; db < D / 32; ++db) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int key = k0 + 32 * wid + (i & 3) + 8 * (i >> 2) + 4 * hl;
+      if (key < a.Sk) {
+        dkp[(int64_t)key * a.dk_ss + 32 * db + r] = (T)dk[db][i];
+        dvp[(int64_t)key * a.dv_ss + 32 * db + r] = (T)dv[db][i];
+      }
+    }
+  }
+}
+
+// dQ fp32 accumulator [B*H, Sq, D] -> output dtype with strides
+template <typename T, int D>
+__global__ void __launch_bounds__(256) attn_dq_convert(AttnArgs a, const float* dq_acc) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;  // one thread per 8 elements
+  const int64_t total = (int64_t)a.B * a.H * a.Sq * (D / 8);
+  if (idx >= total) return;
+  const int c8 = (int)(idx % (D / 8));
+  const int64_t row = idx / (D / 8);
+  const int q = (int)(row % a.Sq);
+  const int64_t bh = row / a.Sq;
+  const int b = (int)(bh / a.H), h = (int)(bh % a.H);
+  float v[8];
+  load_f<float, 8>(dq_acc + row * D + c8 * 8, v);
+  T* dst = (T*)a.dq + b * a.dq_bs + h * a.dq_hs + (int64_t)q * a.dq_ss + c8 * 8;
+  store_f<T, 8>(dst, v);
+}
+
+// debug / test: materialise the keep-mask the kernels use (uint8 [B*H, Sq, Sk])
+__global__ void attn_dropout_mask_kernel(uint8_t* out, int64_t BH, int Sq, int Sk, uint64_t seed,
+                                         uint64_t offset, uint32_t thresh) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;  // one thread per 8 keys
+  const int64_t n8 = (Sk + 7) / 8;
+  if (idx >= BH * Sq * n8) return;
+  const int64_t c8 = idx % n8, row = idx / n8;
+  const int q = (int)(row % Sq);
+  const int64_t bh = row / Sq;
+  DropGen dg{seed, offset, thresh};
+  const uint4 rnd = dg.block(bh, q, c8, Sq);
+  for (int e = 0; e < 8; ++e) {
+    const int64_t key = c8 * 8 + e;
+    if (key < Sk) out[row * Sk + key] = DropGen::r16(rnd, e) >= thresh ? 1 : 0;
+  }
+}
+
+int attn_dropout_mask(uint8_t* out, int64_t BH, int Sq, int Sk, uint64_t seed, uint64_t offset,
+                      uint32_t thresh, hipStream_t s) {
+  const int64_t n = BH * Sq * ((Sk + 7) / 8);
+  hipLaunchKernelGGL(attn_dropout_mask_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                     out, BH, Sq, Sk, seed, offset, thresh);
+  return (int)hipGetLastError();
+}
+
+#define ATTN_DISPATCH(DT, T, ...)                         \
+  switch (DT) {                                             \
+    case kF16: { using T = f16; __VA_ARGS__; } break;       \
+    case kBF16: { using T = bf16; __VA_ARGS__; } break;     \
+    default: return -1;                                     \
+  }
+#define ATTN_DISPATCH_D(DD, D, ...)                         \
+  switch (DD) {                                             \
+    case 64: { constexpr int D = 64; __VA_ARGS__; } break;  \
+    case 128: { constexpr int D = 128; __VA_ARGS__; } break;\
+    default: return -1;                                     \
+  }
+#define ATTN_DISPATCH_B(X, NAME, ...)                       \
+  if (X) { constexpr bool NAME = true; __VA_ARGS__; }       \
+  else { constexpr bool NAME = false; __VA_ARGS__; }
+
+int attn_fwd(const AttnArgs& a, int dt, hipStream_t s) {
+  if (a.B * a.H == 0 || a.Sq == 0) return 0;
+  dim3 grid((a.Sq + kFwdBQ - 1) / kFwdBQ, a.B * a.H);
+  const bool drop = a.drop_thresh > 0;
+  ATTN_DISPATCH(dt, T, ATTN_DISPATCH_D(a.D, D, ATTN_DISPATCH_B(a.causal, C, ATTN_DISPATCH_B(drop, DR,
+      hipLaunchKernelGGL((attn_fwd_kernel<T, D, C, DR>), grid, dim3(256), 0, s, a)))));
+  return (int)hipGetLastError();
+}
+
+int attn_bwd(const AttnArgs& a, const void* dout, float* delta, float* dq_acc, void* dk, void* dv,
+             int dt, hipStream_t s) {
+  if (a.B * a.H == 0 || a.Sq == 0) return 0;
+  const bool drop = a.drop_thresh > 0;
+  const int64_t rows = (int64_t)a.B * a.H * a.Sq;
+  hipMemsetAsync(dq_acc, 0, rows * a.D * sizeof(float), s);
+  ATTN_DISPATCH(dt, T, ATTN_DISPATCH_D(a.D, D, {
+    hipLaunchKernelGGL((attn_bwd_delta_kernel<T, D>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0,
+                       s, a, dout, delta);
+    dim3 grid((a.Sk + kBwdBK - 1) / kBwdBK, a.B * a.H);
+    ATTN_DISPATCH_B(a.causal, C, ATTN_DISPATCH_B(drop, DR,
+        hipLaunchKernelGGL((attn_bwd_kernel<T, D, C, DR>), grid, dim3(256), 0, s, a, dout, delta,
+                           dq_acc, dk, dv)));
+    const int64_t tot = rows * (D / 8);
+    hipLaunchKernelGGL((attn_dq_convert<T, D>), dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s,
+                       a, dq_acc);
+  }));
+  return (int)hipGetLastError();
+}
+
+}  // namespace apex

@@ -275,6 +275,216 @@ Tensor xent_bwd(Tensor dloss, Tensor logits, Tensor lse, Tensor labels, double s
   return dx;
 }
 
+// --------------------------------------------------------------------------
+// flash attention: q, k, v, o are [B, S, H, D] (any batch/seq/head strides, D contiguous)
+// --------------------------------------------------------------------------
+void attn_set(apex::AttnArgs& a, const Tensor& t, int64_t& bs, int64_t& ss, int64_t& hs) {
+  TORCH_CHECK(t.dim() == 4 && t.stride(3) == 1, "attention tensors must be [B, S, H, D], D contiguous");
+  TORCH_CHECK(t.stride(1) % 8 == 0 && t.stride(2) % 8 == 0 && t.stride(0) % 8 == 0 &&
+                  ((uintptr_t)t.data_ptr() & 15) == 0,
+              "attention tensors must be 16-byte aligned per row");
+  bs = t.stride(0);
+  ss = t.stride(1);
+  hs = t.stride(2);
+}
+
+apex::AttnArgs attn_common(const Tensor& q, const Tensor& k, const Tensor& v, bool causal,
+                           double scale, double p_drop, int64_t seed, int64_t offset,
+                           const c10::optional<Tensor>& k_lens) {
+  apex::AttnArgs a{};
+  TORCH_CHECK(q.scalar_type() == k.scalar_type() && q.scalar_type() == v.scalar_type(), "dtype mismatch");
+  a.q = q.data_ptr();
+  a.k = k.data_ptr();
+  a.v = v.data_ptr();
+  attn_set(a, q, a.q_bs, a.q_ss, a.q_hs);
+  attn_set(a, k, a.k_bs, a.k_ss, a.k_hs);
+  attn_set(a, v, a.v_bs, a.v_ss, a.v_hs);
+  a.B = (int)q.size(0);
+  a.Sq = (int)q.size(1);
+  a.H = (int)q.size(2);
+  a.D = (int)q.size(3);
+  a.Sk = (int)k.size(1);
+  TORCH_CHECK(k.size(0) == a.B && k.size(2) == a.H && k.size(3) == a.D && v.sizes() == k.sizes(),
+              "k/v shape mismatch");
+  TORCH_CHECK(a.D == 64 || a.D == 128, "flash attention supports head dim 64 or 128");
+  a.causal = causal;
+  a.scale = (float)scale;
+  a.scale_log2 = (float)(scale * 1.4426950408889634);
+  TORCH_CHECK(p_drop >= 0.0 && p_drop < 1.0, "dropout p must be in [0, 1)");
+  a.drop_thresh = p_drop > 0.0 ? (uint32_t)std::lround(p_drop * 65536.0) : 0u;
+  if (p_drop > 0.0 && a.drop_thresh == 0) a.drop_thresh = 1;
+  a.drop_scale = p_drop > 0.0 ? (float)(1.0 / (1.0 - a.drop_thresh / 65536.0)) : 1.f;
+  a.seed = (uint64_t)seed;
+  a.offset = (uint64_t)offset;
+  if (k_lens.has_value() && k_lens->defined()) {
+    TORCH_CHECK(k_lens->scalar_type() == at::kInt && k_lens->numel() == a.B, "k_lens must be int32 [B]");
+    a.k_lens = k_lens->data_ptr<int>();
+  }
+  return a;
+}
+
+std::vector<Tensor> flash_attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, double scale,
+                                   double p_drop, int64_t seed, int64_t offset,
+                                   const c10::optional<Tensor>& k_lens) {
+  apex::AttnArgs a = attn_common(q, k, v, causal, scale, p_drop, seed, offset, k_lens);
+  Tensor o = at::empty({a.B, a.Sq, a.H, a.D}, q.options());
+  Tensor lse = at::empty({a.B, a.H, a.Sq}, q.options().dtype(at::kFloat));
+  a.o = o.data_ptr();
+  attn_set(a, o, a.o_bs, a.o_ss, a.o_hs);
+  a.lse = lse.data_ptr<float>();
+  check(apex::attn_fwd(a, dt_code(q.scalar_type()), cur_stream()), "attn_fwd");
+  return {o, lse};
+}
+
+void flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor dq,
+                    Tensor dk, Tensor dv, bool causal, double scale, double p_drop, int64_t seed,
+                    int64_t offset, const c10::optional<Tensor>& k_lens) {
+  apex::AttnArgs a = attn_common(q, k, v, causal, scale, p_drop, seed, offset, k_lens);
+  a.o = o.data_ptr();
+  attn_set(a, o, a.o_bs, a.o_ss, a.o_hs);
+  a.lse = lse.data_ptr<float>();
+  attn_set(a, dout, a.do_bs, a.do_ss, a.do_hs);
+  attn_set(a, dq, a.dq_bs, a.dq_ss, a.dq_hs);
+  attn_set(a, dk, a.dk_bs, a.dk_ss, a.dk_hs);
+  attn_set(a, dv, a.dv_bs, a.dv_ss, a.dv_hs);
+  a.dq = dq.data_ptr();
+  const int64_t rows = (int64_t)a.B * a.H * a.Sq;
+  Tensor delta = at::empty({rows}, q.options().dtype(at::kFloat));
+  Tensor dq_acc = at::empty({rows * a.D}, q.options().dtype(at::kFloat));
+  check(apex::attn_bwd(a, dout.data_ptr(), delta.data_ptr<float>(), dq_acc.data_ptr<float>(),
+                       dk.data_ptr(), dv.data_ptr(), dt_code(q.scalar_type()), cur_stream()),
+        "attn_bwd");
+}
+
+// --------------------------------------------------------------------------
+// fused elementwise (bias / act / dropout / residual / LN)
+// --------------------------------------------------------------------------
+std::pair<uint32_t, float> drop_params(double p) {
+  if (p <= 0.0) return {0u, 1.f};
+  TORCH_CHECK(p < 1.0, "dropout p must be < 1");
+  uint32_t th = (uint32_t)std::lround(p * 65536.0);
+  if (th == 0) th = 1;
+  return {th, (float)(1.0 / (1.0 - th / 65536.0))};
+}
+
+int64_t cols_of(const Tensor& x) { return x.dim() ? x.size(-1) : 1; }
+
+Tensor k_bias_act_fwd(Tensor x, const c10::optional<Tensor>& b, int64_t act) {
+  TORCH_CHECK(x.is_contiguous(), "bias_act: x must be contiguous");
+  const int64_t cols = cols_of(x), rows = x.numel() / std::max<int64_t>(cols, 1);
+  Tensor y = at::empty_like(x);
+  const int bdt = b.has_value() && b->defined() ? dt_code(b->scalar_type()) : dt_code(x.scalar_type());
+  check(apex::bias_act_fwd(x.data_ptr(), opt_vptr(b), y.data_ptr(), rows, (int)cols, (int)act,
+                           dt_code(x.scalar_type()), bdt, cur_stream()),
+        "bias_act_fwd");
+  return y;
+}
+
+std::vector<Tensor> k_bias_act_bwd(Tensor dy, Tensor x, const c10::optional<Tensor>& b, int64_t act) {
+  const int64_t cols = cols_of(x), rows = x.numel() / std::max<int64_t>(cols, 1);
+  Tensor dyc = dy.contiguous();
+  Tensor dx = at::empty_like(x);
+  const bool hb = b.has_value() && b->defined();
+  Tensor db = hb ? at::empty_like(*b) : Tensor();
+  Tensor ws = hb ? at::empty({apex::colsum_parts(rows) * cols}, x.options().dtype(at::kFloat)) : Tensor();
+  const int bdt = hb ? dt_code(b->scalar_type()) : dt_code(x.scalar_type());
+  check(apex::bias_act_bwd(dyc.data_ptr(), x.data_ptr(), opt_vptr(b), dx.data_ptr(),
+                           hb ? db.data_ptr() : nullptr, hb ? ws.data_ptr<float>() : nullptr, rows,
+                           (int)cols, (int)act, dt_code(x.scalar_type()), bdt, cur_stream()),
+        "bias_act_bwd");
+  return {dx, db};
+}
+
+Tensor k_bda_fwd(Tensor x, const c10::optional<Tensor>& b, Tensor res, double p, int64_t seed,
+                 int64_t offset) {
+  TORCH_CHECK(x.is_contiguous() && res.is_contiguous() && x.sizes() == res.sizes(), "bias_dropout_add: shapes");
+  const int64_t cols = cols_of(x), rows = x.numel() / std::max<int64_t>(cols, 1);
+  Tensor y = at::empty_like(x);
+  auto dp = drop_params(p);
+  const int bdt = b.has_value() && b->defined() ? dt_code(b->scalar_type()) : dt_code(x.scalar_type());
+  check(apex::bias_dropout_add_fwd(x.data_ptr(), opt_vptr(b), res.data_ptr(), y.data_ptr(), rows, (int)cols,
+                                   (uint64_t)seed, (uint64_t)offset, dp.first, dp.second,
+                                   dt_code(x.scalar_type()), bdt, cur_stream()),
+        "bias_dropout_add_fwd");
+  return y;
+}
+
+std::vector<Tensor> k_bda_bwd(Tensor dy, double p, int64_t seed, int64_t offset,
+                              const c10::optional<Tensor>& bias_like) {
+  Tensor dyc = dy.contiguous();
+  const int64_t cols = cols_of(dyc), rows = dyc.numel() / std::max<int64_t>(cols, 1);
+  Tensor dx = at::empty_like(dyc);
+  const bool hb = bias_like.has_value() && bias_like->defined();
+  Tensor db = hb ? at::empty_like(*bias_like) : Tensor();
+  Tensor ws = hb ? at::empty({apex::colsum_parts(rows) * cols}, dyc.options().dtype(at::kFloat)) : Tensor();
+  auto dp = drop_params(p);
+  check(apex::bias_dropout_add_bwd(dyc.data_ptr(), dx.data_ptr(), hb ? db.data_ptr() : nullptr,
+                                   hb ? ws.data_ptr<float>() : nullptr, rows, (int)cols, (uint64_t)seed,
+                                   (uint64_t)offset, dp.first, dp.second, dt_code(dyc.scalar_type()),
+                                   hb ? dt_code(bias_like->scalar_type()) : dt_code(dyc.scalar_type()),
+                                   cur_stream()),
+        "bias_dropout_add_bwd");
+  return {dx, db};
+}
+
+Tensor k_colsum(Tensor x, at::ScalarType out_dtype) {
+  Tensor xc = x.contiguous();
+  const int64_t cols = cols_of(xc), rows = xc.numel() / std::max<int64_t>(cols, 1);
+  Tensor out = at::empty({cols}, xc.options().dtype(out_dtype));
+  Tensor ws = at::empty({apex::colsum_parts(rows) * cols}, xc.options().dtype(at::kFloat));
+  check(apex::colsum(xc.data_ptr(), out.data_ptr(), ws.data_ptr<float>(), rows, (int)cols,
+                     dt_code(xc.scalar_type()), dt_code(out_dtype), cur_stream()),
+        "colsum");
+  return out;
+}
+
+bool k_bdaln_supported(int64_t cols) { return apex::bdaln_supported((int)cols) != 0; }
+
+std::vector<Tensor> k_bdaln_fwd(Tensor x, const c10::optional<Tensor>& b, Tensor res, Tensor gamma,
+                                Tensor beta, double eps, double p, int64_t seed, int64_t offset) {
+  TORCH_CHECK(x.is_contiguous() && res.is_contiguous() && x.sizes() == res.sizes(), "bdaln: shapes");
+  const int64_t cols = cols_of(x), rows = x.numel() / std::max<int64_t>(cols, 1);
+  Tensor y = at::empty_like(x), s = at::empty_like(x);
+  auto fo = x.options().dtype(at::kFloat);
+  Tensor mean = at::empty({rows}, fo), rstd = at::empty({rows}, fo);
+  auto dp = drop_params(p);
+  check(apex::bdaln_fwd(x.data_ptr(), opt_vptr(b), res.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+                        y.data_ptr(), s.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(), rows,
+                        (int)cols, (float)eps, (uint64_t)seed, (uint64_t)offset, dp.first, dp.second,
+                        dt_code(x.scalar_type()), dt_code(gamma.scalar_type()), cur_stream()),
+        "bdaln_fwd");
+  return {y, s, mean, rstd};
+}
+
+std::vector<Tensor> k_bdaln_bwd(Tensor dy, Tensor s, Tensor gamma, Tensor mean, Tensor rstd, double p,
+                                int64_t seed, int64_t offset, bool has_bias) {
+  Tensor dyc = dy.contiguous();
+  const int64_t cols = cols_of(s), rows = s.numel() / std::max<int64_t>(cols, 1);
+  Tensor dres = at::empty_like(s), dx = at::empty_like(s);
+  Tensor dgamma = at::empty_like(gamma), dbeta = at::empty_like(gamma);
+  Tensor dbias = has_bias ? at::empty_like(gamma) : Tensor();
+  Tensor ws = at::empty({apex::bdaln_ws_floats(rows, (int)cols)}, s.options().dtype(at::kFloat));
+  auto dp = drop_params(p);
+  check(apex::bdaln_bwd(dyc.data_ptr(), s.data_ptr(), gamma.data_ptr(), mean.data_ptr<float>(),
+                        rstd.data_ptr<float>(), dres.data_ptr(), dx.data_ptr(), dgamma.data_ptr(),
+                        dbeta.data_ptr(), has_bias ? dbias.data_ptr() : nullptr, ws.data_ptr<float>(), rows,
+                        (int)cols, (uint64_t)seed, (uint64_t)offset, dp.first, dp.second,
+                        dt_code(s.scalar_type()), dt_code(gamma.scalar_type()), cur_stream()),
+        "bdaln_bwd");
+  return {dres, dx, dgamma, dbeta, dbias};
+}
+
+Tensor flash_dropout_mask(int64_t B, int64_t H, int64_t Sq, int64_t Sk, double p_drop, int64_t seed,
+                          int64_t offset, at::Device dev) {
+  Tensor out = at::empty({B, H, Sq, Sk}, at::TensorOptions().dtype(at::kByte).device(dev));
+  uint32_t th = p_drop > 0.0 ? (uint32_t)std::lround(p_drop * 65536.0) : 0u;
+  if (p_drop > 0.0 && th == 0) th = 1;
+  check(apex::attn_dropout_mask(out.data_ptr<uint8_t>(), B * H, (int)Sq, (int)Sk, (uint64_t)seed,
+                                (uint64_t)offset, th, cur_stream()),
+        "attn_dropout_mask");
+  return out;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -299,4 +509,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ln_bwd", &ln_bwd);
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd", &xent_bwd);
+  m.def("flash_attn_fwd", &flash_attn_fwd);
+  m.def("flash_attn_bwd", &flash_attn_bwd);
+  m.def("flash_dropout_mask", &flash_dropout_mask);
+  m.def("bias_act_fwd", &k_bias_act_fwd);
+  m.def("bias_act_bwd", &k_bias_act_bwd);
+  m.def("bias_dropout_add_fwd", &k_bda_fwd);
+  m.def("bias_dropout_add_bwd", &k_bda_bwd);
+  m.def("colsum", &k_colsum);
+  m.def("bdaln_supported", &k_bdaln_supported);
+  m.def("bdaln_fwd", &k_bdaln_fwd);
+  m.def("bdaln_bwd", &k_bdaln_bwd);
 }

@@ -84,6 +84,45 @@ __device__ __forceinline__ float block_max(float v, float* red) {
 }
 
 // ---------------------------------------------------------------------------
+// Column sum of fp32 partial rows: out[c] = sum_p part[p*ld + c]  (c < cols).
+// Block = 256 threads = 16 columns x 16 part-groups: every thread issues parts/16
+// loads of 64-byte row segments, the 16 groups combine in LDS. Launch with
+// grid = ceil(cols / 16). Deterministic (fixed summation order).
+// ---------------------------------------------------------------------------
+template <typename W, typename Conv>
+__global__ void __launch_bounds__(256) partial_colsum_kernel(const float* __restrict__ part, int parts,
+                                                            int64_t ld, int cols, W* __restrict__ out,
+                                                            Conv conv) {
+  __shared__ float red[16][17];
+  const int cl = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
+  float a = 0.f;
+  if (c < cols)
+    for (int p = grp; p < parts; p += 16) a += part[(int64_t)p * ld + c];
+  red[grp][cl] = a;
+  __syncthreads();
+  if (grp == 0 && c < cols) {
+    float t = 0.f;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) t += red[g][cl];
+    out[c] = conv(t);
+  }
+}
+
+template <typename W>
+struct ToW {
+  __device__ __forceinline__ W operator()(float v) const { return (W)v; }
+};
+
+template <typename W>
+inline void launch_partial_colsum(const float* part, int parts, int64_t ld, int cols, W* out,
+                                  hipStream_t s) {
+  if (!out || cols <= 0) return;
+  hipLaunchKernelGGL((partial_colsum_kernel<W, ToW<W>>), dim3((cols + 15) / 16), dim3(256), 0, s, part,
+                     parts, ld, cols, out, ToW<W>{});
+}
+
+// ---------------------------------------------------------------------------
 // Philox-4x32-10 counter RNG (stateless: (seed, offset, subsequence) -> 4 u32).
 // Dropout kernels derive the counter from the element index so fwd and bwd
 // regenerate identical masks without storing them when asked to.

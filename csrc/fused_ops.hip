@@ -1,0 +1,546 @@
+// Fused transformer elementwise kernels (bias / activation / dropout / residual / LayerNorm)
+// with the bias gradient folded into the backward pass.
+//
+//   bias_act      y = act(x + b)                         bwd: dx = dy*act'(x+b), db = colsum(dx)
+//   bias_drop_add y = res + dropout(x + b)               bwd: dres = dy, dx = dy*mask/(1-p), db
+//   bdaln         s = res + dropout(x + b); y = LN(s)     bwd: LN bwd -> ds; dres = ds; dx; db,
+//                                                              dgamma, dbeta
+// Dropout masks are never stored: element e keeps iff 16-bit chunk (e & 7) of
+// Philox(seed, 0, offset + e/8) >= thresh, regenerated identically in backward.
+// Column sums (bias / gamma / beta grads) are accumulated per thread in registers over a
+// row block, written as fp32 partial rows and reduced by colsum_reduce (deterministic).
+#include "common.h"
+#include "kernels.h"
+
+namespace apex {
+
+constexpr int kEwBlock = 256;
+
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_erf_grad(float x) {
+  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
+  return 0.5f * x * (1.f + tanhf(u));
+}
+__device__ __forceinline__ float gelu_tanh_grad(float x) {
+  const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
+  const float t = tanhf(u);
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * 0.7978845608028654f * (1.f + 3.f * 0.044715f * x * x);
+}
+
+template <int ACT>
+__device__ __forceinline__ float act_f(float x) {
+  if (ACT == 0) return gelu_erf(x);
+  if (ACT == 1) return gelu_tanh(x);
+  if (ACT == 2) return fmaxf(x, 0.f);
+  return x;  // identity
+}
+template <int ACT>
+__device__ __forceinline__ float act_g(float x) {
+  if (ACT == 0) return gelu_erf_grad(x);
+  if (ACT == 1) return gelu_tanh_grad(x);
+  if (ACT == 2) return x > 0.f ? 1.f : 0.f;
+  return 1.f;
+}
+
+// 8 keep flags for elements [e8*8, e8*8+8)
+__device__ __forceinline__ void drop_mask8(uint64_t seed, uint64_t offset, int64_t e8, uint32_t thresh,
+                                           bool (&keep)[8]) {
+  Philox ph(seed, 0, offset + (uint64_t)e8);
+  const uint4 r = ph.next();
+  const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint32_t v = (k & 1) ? (w[k >> 1] >> 16) : (w[k >> 1] & 0xffffu);
+    keep[k] = v >= thresh;
+  }
+}
+
+// Geometry shared by the column-chunk kernels: block = 256 threads x 8 columns = 2048
+// columns; grid.x = column chunks, grid.y = row blocks of `rpb` rows.
+struct ColGeom {
+  int64_t rows;
+  int cols;
+  int rpb;
+};
+
+// ------------------------------- bias + activation -------------------------
+template <typename T, typename W, int ACT>
+__global__ void __launch_bounds__(kEwBlock) bias_act_fwd_kernel(const T* __restrict__ x,
+                                                               const W* __restrict__ b,
+                                                               T* __restrict__ y, ColGeom g) {
+  const int c = (blockIdx.x * kEwBlock + threadIdx.x) * 8;
+  if (c >= g.cols) return;
+  float bv[8];
+  if (b) load_f<W, 8>(b + c, bv);
+  else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) bv[k] = 0.f;
+  }
+  const int64_t r0 = (int64_t)blockIdx.y * g.rpb;
+  const int64_t r1 = min(r0 + g.rpb, g.rows);
+  for (int64_t r = r0; r < r1; ++r) {
+    float v[8];
+    load_f<T, 8>(x + r * g.cols + c, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = act_f<ACT>(v[k] + bv[k]);
+    store_f<T, 8>(y + r * g.cols + c, v);
+  }
+}
+
+template <typename T, typename W, int ACT>
+__global__ void __launch_bounds__(kEwBlock) bias_act_bwd_kernel(const T* __restrict__ dy,
+                                                               const T* __restrict__ x,
+                                                               const W* __restrict__ b,
+                                                               T* __restrict__ dx,
+                                                               float* __restrict__ part, ColGeom g) {
+  const int c = (blockIdx.x * kEwBlock + threadIdx.x) * 8;
+  if (c >= g.cols) return;
+  float bv[8], acc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  if (b) load_f<W, 8>(b + c, bv);
+  else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) bv[k] = 0.f;
+  }
+  const int64_t r0 = (int64_t)blockIdx.y * g.rpb;
+  const int64_t r1 = min(r0 + g.rpb, g.rows);
+  for (int64_t r = r0; r < r1; ++r) {
+    float v[8], d[8];
+    load_f<T, 8>(x + r * g.cols + c, v);
+    load_f<T, 8>(dy + r * g.cols + c, d);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      d[k] *= act_g<ACT>(v[k] + bv[k]);
+      acc[k] += d[k];
+    }
+    store_f<T, 8>(dx + r * g.cols + c, d);
+  }
+  if (part) store_f<float, 8>(part + (int64_t)blockIdx.y * g.cols + c, acc);
+}
+
+// ----------------------------- bias + dropout + residual ---------------------
+template <typename T, typename W, bool DROP>
+__global__ void __launch_bounds__(kEwBlock) bda_fwd_kernel(const T* __restrict__ x, const W* __restrict__ b,
+                                                          const T* __restrict__ res, T* __restrict__ y,
+                                                          ColGeom g, uint64_t seed, uint64_t offset,
+                                                          uint32_t thresh, float scale) {
+  const int c = (blockIdx.x * kEwBlock + threadIdx.x) * 8;
+  if (c >= g.cols) return;
+  float bv[8];
+  if (b) load_f<W, 8>(b + c, bv);
+  else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) bv[k] = 0.f;
+  }
+  const int64_t r0 = (int64_t)blockIdx.y * g.rpb;
+  const int64_t r1 = min(r0 + g.rpb, g.rows);
+  for (int64_t r = r0; r < r1; ++r) {
+    const int64_t e = r * g.cols + c;
+    float v[8], rv[8];
+    load_f<T, 8>(x + e, v);
+    load_f<T, 8>(res + e, rv);
+    bool keep[8];
+    if (DROP) drop_mask8(seed, offset, e >> 3, thresh, keep);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float t = v[k] + bv[k];
+      if (DROP) t = keep[k] ? t * scale : 0.f;
+      v[k] = rv[k] + t;
+    }
+    store_f<T, 8>(y + e, v);
+  }
+}
+
+template <typename T, bool DROP>
+__global__ void __launch_bounds__(kEwBlock) bda_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx,
+                                                          float* __restrict__ part, ColGeom g,
+                                                          uint64_t seed, uint64_t offset,
+                                                          uint32_t thresh, float scale) {
+  const int c = (blockIdx.x * kEwBlock + threadIdx.x) * 8;
+  if (c >= g.cols) return;
+  float acc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  const int64_t r0 = (int64_t)blockIdx.y * g.rpb;
+  const int64_t r1 = min(r0 + g.rpb, g.rows);
+  for (int64_t r = r0; r < r1; ++r) {
+    const int64_t e = r * g.cols + c;
+    float d[8];
+    load_f<T, 8>(dy + e, d);
+    bool keep[8];
+    if (DROP) drop_mask8(seed, offset, e >> 3, thresh, keep);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (DROP) d[k] = keep[k] ? d[k] * scale : 0.f;
+      acc[k] += d[k];
+    }
+    if (dx) store_f<T, 8>(dx + e, d);
+  }
+  if (part) store_f<float, 8>(part + (int64_t)blockIdx.y * g.cols + c, acc);
+}
+
+// ------------------------- bias + dropout + residual + LayerNorm ------------
+// one wave per row (cols % 8 == 0, cols <= 512*VPT... VPT vectors of 8 per lane)
+template <typename T, typename W, int VPT, bool DROP>
+__global__ void __launch_bounds__(kEwBlock) bdaln_fwd_kernel(const T* __restrict__ x, const W* __restrict__ b,
+                                                            const T* __restrict__ res,
+                                                            const W* __restrict__ gamma,
+                                                            const W* __restrict__ beta, T* __restrict__ y,
+                                                            T* __restrict__ s_out, float* __restrict__ mean,
+                                                            float* __restrict__ rstd, int64_t rows, int cols,
+                                                            float eps, uint64_t seed, uint64_t offset,
+                                                            uint32_t thresh, float scale) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nvec = cols >> 3;
+  float v[VPT][8];
+  float sum = 0.f;
+#pragma unroll
+  for (int j = 0; j < VPT; ++j) {
+    const int vi = j * 64 + lane;
+    if (vi < nvec) {
+      const int64_t e = row * cols + vi * 8;
+      float xv[8], rv[8], bv[8];
+      load_f<T, 8>(x + e, xv);
+      load_f<T, 8>(res + e, rv);
+      if (b) load_f<W, 8>(b + vi * 8, bv);
+      else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) bv[k] = 0.f;
+      }
+      bool keep[8];
+      if (DROP) drop_mask8(seed, offset, e >> 3, thresh, keep);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float t = xv[k] + bv[k];
+        if (DROP) t = keep[k] ? t * scale : 0.f;
+        v[j][k] = rv[k] + t;
+      }
+      // the LN input is stored at the activation precision and normalised from that value,
+      // so backward (which reads s_out) sees exactly what forward normalised
+      store_f<T, 8>(s_out + e, v[j]);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        v[j][k] = to_f(from_f<T>(v[j][k]));
+        sum += v[j][k];
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[j][k] = 0.f;
+    }
+  }
+  const float inv_n = 1.f / (float)cols;
+  const float mu = wave_sum(sum) * inv_n;
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < VPT; ++j) {
+    if (j * 64 + lane < nvec) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float d = v[j][k] - mu;
+        ss += d * d;
+      }
+    }
+  }
+  const float rs = rsqrtf(wave_sum(ss) * inv_n + eps);
+  if (lane == 0) {
+    mean[row] = mu;
+    rstd[row] = rs;
+  }
+#pragma unroll
+  for (int j = 0; j < VPT; ++j) {
+    const int vi = j * 64 + lane;
+    if (vi < nvec) {
+      float gv[8], bb[8], o[8];
+      load_f<W, 8>(gamma + vi * 8, gv);
+      load_f<W, 8>(beta + vi * 8, bb);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = (v[j][k] - mu) * rs * gv[k] + bb[k];
+      store_f<T, 8>(y + row * cols + vi * 8, o);
+    }
+  }
+}
+
+// part rows: [dgamma | dbeta | dbias] (3*cols floats) per block
+template <typename T, typename W, int VPT, bool DROP>
+__global__ void __launch_bounds__(kEwBlock) bdaln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ s,
+                                                            const W* __restrict__ gamma,
+                                                            const float* __restrict__ mean,
+                                                            const float* __restrict__ rstd,
+                                                            T* __restrict__ dres, T* __restrict__ dx,
+                                                            float* __restrict__ part, int64_t rows, int cols,
+                                                            int rows_per_wave, uint64_t seed,
+                                                            uint64_t offset, uint32_t thresh, float scale) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // [4][3*cols]
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nvec = cols >> 3;
+  const float inv_n = 1.f / (float)cols;
+  float dg[VPT][8], dbt[VPT][8], dbi[VPT][8], g[VPT][8];
+#pragma unroll
+  for (int j = 0; j < VPT; ++j) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      dg[j][k] = dbt[j][k] = dbi[j][k] = 0.f;
+      g[j][k] = 1.f;
+    }
+    if (j * 64 + lane < nvec) load_f<W, 8>(gamma + (j * 64 + lane) * 8, g[j]);
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_wave * 4;
+  for (int rr = 0; rr < rows_per_wave; ++rr) {
+    const int64_t row = r0 + (int64_t)rr * 4 + wid;
+    if (row >= rows) break;
+    const float mu = mean[row], rs = rstd[row];
+    float xh[VPT][8], dv[VPT][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int vi = j * 64 + lane;
+      if (vi < nvec) {
+        load_f<T, 8>(s + row * cols + vi * 8, xh[j]);
+        load_f<T, 8>(dy + row * cols + vi * 8, dv[j]);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          xh[j][k] = (xh[j][k] - mu) * rs;
+          const float dyg = dv[j][k] * g[j][k];
+          s1 += dyg;
+          s2 += dyg * xh[j][k];
+          dg[j][k] += dv[j][k] * xh[j][k];
+          dbt[j][k] += dv[j][k];
+        }
+      }
+    }
+    s1 = wave_sum(s1) * inv_n;
+    s2 = wave_sum(s2) * inv_n;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int vi = j * 64 + lane;
+      if (vi < nvec) {
+        const int64_t e = row * cols + vi * 8;
+        float ds[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) ds[k] = rs * (dv[j][k] * g[j][k] - s1 - xh[j][k] * s2);
+        store_f<T, 8>(dres + e, ds);
+        bool keep[8];
+        if (DROP) drop_mask8(seed, offset, e >> 3, thresh, keep);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          if (DROP) ds[k] = keep[k] ? ds[k] * scale : 0.f;
+          dbi[j][k] += ds[k];
+        }
+        store_f<T, 8>(dx + e, ds);
+      }
+    }
+  }
+  float* mine = lds + wid * 3 * cols;
+#pragma unroll
+  for (int j = 0; j < VPT; ++j) {
+    const int vi = j * 64 + lane;
+    if (vi < nvec) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        mine[vi * 8 + k] = dg[j][k];
+        mine[cols + vi * 8 + k] = dbt[j][k];
+        mine[2 * cols + vi * 8 + k] = dbi[j][k];
+      }
+    }
+  }
+  __syncthreads();
+  float* out = part + (int64_t)blockIdx.x * 3 * cols;
+  for (int c = threadIdx.x; c < 3 * cols; c += kEwBlock)
+    out[c] = lds[c] + lds[3 * cols + c] + lds[6 * cols + c] + lds[9 * cols + c];
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+#define EW_DISPATCH(DT, T, ...)                             \
+  switch (DT) {                                             \
+    case kF32: { using T = float; __VA_ARGS__; } break;     \
+    case kF16: { using T = f16; __VA_ARGS__; } break;       \
+    case kBF16: { using T = bf16; __VA_ARGS__; } break;     \
+    default: return -1;                                     \
+  }
+#define EW_ACT(A, ACT, ...)                                 \
+  switch (A) {                                              \
+    case 0: { constexpr int ACT = 0; __VA_ARGS__; } break;  \
+    case 1: { constexpr int ACT = 1; __VA_ARGS__; } break;  \
+    case 2: { constexpr int ACT = 2; __VA_ARGS__; } break;  \
+    case 3: { constexpr int ACT = 3; __VA_ARGS__; } break;  \
+    default: return -1;                                     \
+  }
+
+static inline ColGeom col_geom(int64_t rows, int cols, int target_parts) {
+  ColGeom g;
+  g.rows = rows;
+  g.cols = cols;
+  const int chunks = (cols + 2047) / 2048;
+  // aim for ~target_parts * chunks blocks, >= 16 rows per block
+  int64_t rpb = (rows + target_parts - 1) / target_parts;
+  if (rpb < 16) rpb = 16;
+  g.rpb = (int)rpb;
+  (void)chunks;
+  return g;
+}
+
+int64_t colsum_parts(int64_t rows) {
+  int64_t p = (rows + 15) / 16;
+  return p < 512 ? p : 512;
+}
+
+int bias_act_fwd(const void* x, const void* b, void* y, int64_t rows, int cols, int act, int xdt,
+                 int bdt, hipStream_t s) {
+  if (rows == 0) return 0;
+  if (cols % 8) return -2;
+  ColGeom g = col_geom(rows, cols, 512);
+  dim3 grid((cols / 8 + kEwBlock - 1) / kEwBlock, (unsigned)((rows + g.rpb - 1) / g.rpb));
+  if (!b) bdt = xdt;
+  EW_DISPATCH(xdt, T, EW_DISPATCH(bdt, W, EW_ACT(act, ACT,
+      hipLaunchKernelGGL((bias_act_fwd_kernel<T, W, ACT>), grid, dim3(kEwBlock), 0, s, (const T*)x,
+                         (const W*)b, (T*)y, g))));
+  return (int)hipGetLastError();
+}
+
+int bias_act_bwd(const void* dy, const void* x, const void* b, void* dx, void* db, float* ws,
+                 int64_t rows, int cols, int act, int xdt, int bdt, hipStream_t s) {
+  if (rows == 0) return 0;
+  if (cols % 8) return -2;
+  ColGeom g = col_geom(rows, cols, 512);
+  const int parts = (int)((rows + g.rpb - 1) / g.rpb);
+  dim3 grid((cols / 8 + kEwBlock - 1) / kEwBlock, parts);
+  if (!b) bdt = xdt;
+  EW_DISPATCH(xdt, T, EW_DISPATCH(bdt, W, EW_ACT(act, ACT, {
+    hipLaunchKernelGGL((bias_act_bwd_kernel<T, W, ACT>), grid, dim3(kEwBlock), 0, s, (const T*)dy,
+                       (const T*)x, (const W*)b, (T*)dx, db ? ws : nullptr, g);
+    if (db)
+      launch_partial_colsum<W>(ws, parts, (int64_t)cols, cols, (W*)db, s);
+  })));
+  return (int)hipGetLastError();
+}
+
+int bias_dropout_add_fwd(const void* x, const void* b, const void* res, void* y, int64_t rows, int cols,
+                         uint64_t seed, uint64_t offset, uint32_t thresh, float scale, int xdt, int bdt,
+                         hipStream_t s) {
+  if (rows == 0) return 0;
+  if (cols % 8) return -2;
+  ColGeom g = col_geom(rows, cols, 512);
+  dim3 grid((cols / 8 + kEwBlock - 1) / kEwBlock, (unsigned)((rows + g.rpb - 1) / g.rpb));
+  if (!b) bdt = xdt;
+  EW_DISPATCH(xdt, T, EW_DISPATCH(bdt, W, {
+    if (thresh)
+      hipLaunchKernelGGL((bda_fwd_kernel<T, W, true>), grid, dim3(kEwBlock), 0, s, (const T*)x,
+                         (const W*)b, (const T*)res, (T*)y, g, seed, offset, thresh, scale);
+    else
+      hipLaunchKernelGGL((bda_fwd_kernel<T, W, false>), grid, dim3(kEwBlock), 0, s, (const T*)x,
+                         (const W*)b, (const T*)res, (T*)y, g, seed, offset, thresh, scale);
+  }));
+  return (int)hipGetLastError();
+}
+
+int bias_dropout_add_bwd(const void* dy, void* dx, void* db, float* ws, int64_t rows, int cols,
+                         uint64_t seed, uint64_t offset, uint32_t thresh, float scale, int xdt, int bdt,
+                         hipStream_t s) {
+  if (rows == 0) return 0;
+  if (cols % 8) return -2;
+  ColGeom g = col_geom(rows, cols, 512);
+  const int parts = (int)((rows + g.rpb - 1) / g.rpb);
+  dim3 grid((cols / 8 + kEwBlock - 1) / kEwBlock, parts);
+  EW_DISPATCH(xdt, T, EW_DISPATCH(bdt, W, {
+    if (thresh)
+      hipLaunchKernelGGL((bda_bwd_kernel<T, true>), grid, dim3(kEwBlock), 0, s, (const T*)dy, (T*)dx,
+                         db ? ws : nullptr, g, seed, offset, thresh, scale);
+    else
+      hipLaunchKernelGGL((bda_bwd_kernel<T, false>), grid, dim3(kEwBlock), 0, s, (const T*)dy, (T*)dx,
+                         db ? ws : nullptr, g, seed, offset, thresh, scale);
+    if (db)
+      launch_partial_colsum<W>(ws, parts, (int64_t)cols, cols, (W*)db, s);
+  }));
+  return (int)hipGetLastError();
+}
+
+int colsum(const void* x, void* out, float* ws, int64_t rows, int cols, int xdt, int odt, hipStream_t s) {
+  return bias_dropout_add_bwd(x, nullptr, out, ws, rows, cols, 0, 0, 0, 1.f, xdt, odt, s);
+}
+
+static inline int bdaln_vpt(int cols) {
+  if (cols % 8) return 0;
+  const int nvec = cols / 8;
+  if (nvec <= 64) return 1;
+  if (nvec <= 128) return 2;
+  if (nvec <= 256) return 4;
+  return 0;
+}
+
+int bdaln_supported(int cols) { return bdaln_vpt(cols) > 0; }
+
+#define EW_VPT(V, VPT, ...)                                 \
+  switch (V) {                                              \
+    case 1: { constexpr int VPT = 1; __VA_ARGS__; } break;  \
+    case 2: { constexpr int VPT = 2; __VA_ARGS__; } break;  \
+    case 4: { constexpr int VPT = 4; __VA_ARGS__; } break;  \
+    default: return -2;                                     \
+  }
+
+int bdaln_fwd(const void* x, const void* b, const void* res, const void* gamma, const void* beta, void* y,
+              void* s_out, float* mean, float* rstd, int64_t rows, int cols, float eps, uint64_t seed,
+              uint64_t offset, uint32_t thresh, float scale, int xdt, int wdt, hipStream_t s) {
+  if (rows == 0) return 0;
+  const int vpt = bdaln_vpt(cols);
+  const dim3 grid((unsigned)((rows + 3) / 4));
+  EW_DISPATCH(xdt, T, EW_DISPATCH(wdt, W, EW_VPT(vpt, VPT, {
+    if (thresh)
+      hipLaunchKernelGGL((bdaln_fwd_kernel<T, W, VPT, true>), grid, dim3(kEwBlock), 0, s, (const T*)x,
+                         (const W*)b, (const T*)res, (const W*)gamma, (const W*)beta, (T*)y, (T*)s_out,
+                         mean, rstd, rows, cols, eps, seed, offset, thresh, scale);
+    else
+      hipLaunchKernelGGL((bdaln_fwd_kernel<T, W, VPT, false>), grid, dim3(kEwBlock), 0, s, (const T*)x,
+                         (const W*)b, (const T*)res, (const W*)gamma, (const W*)beta, (T*)y, (T*)s_out,
+                         mean, rstd, rows, cols, eps, seed, offset, thresh, scale);
+  })));
+  return (int)hipGetLastError();
+}
+
+constexpr int kBdalnMaxParts = 512;
+static inline int bdaln_rpw(int64_t rows) {
+  const int64_t r = (rows + 4 * kBdalnMaxParts - 1) / (4 * kBdalnMaxParts);
+  return r < 1 ? 1 : (int)r;
+}
+
+int64_t bdaln_ws_floats(int64_t rows, int cols) {
+  (void)rows;
+  return (int64_t)kBdalnMaxParts * 3 * (int64_t)cols;
+}
+
+int bdaln_bwd(const void* dy, const void* s_in, const void* gamma, const float* mean, const float* rstd,
+              void* dres, void* dx, void* dgamma, void* dbeta, void* dbias, float* ws, int64_t rows,
+              int cols, uint64_t seed, uint64_t offset, uint32_t thresh, float scale, int xdt, int wdt,
+              hipStream_t s) {
+  if (rows == 0) return 0;
+  const int vpt = bdaln_vpt(cols);
+  const int rpw = bdaln_rpw(rows);
+  const int parts = (int)((rows + 4 * rpw - 1) / (4 * rpw));
+  const size_t lds = (size_t)4 * 3 * cols * sizeof(float);
+  EW_DISPATCH(xdt, T, EW_DISPATCH(wdt, W, EW_VPT(vpt, VPT, {
+    if (thresh)
+      hipLaunchKernelGGL((bdaln_bwd_kernel<T, W, VPT, true>), dim3(parts), dim3(kEwBlock), lds, s,
+                         (const T*)dy, (const T*)s_in, (const W*)gamma, mean, rstd, (T*)dres, (T*)dx, ws,
+                         rows, cols, rpw, seed, offset, thresh, scale);
+    else
+      hipLaunchKernelGGL((bdaln_bwd_kernel<T, W, VPT, false>), dim3(parts), dim3(kEwBlock), lds, s,
+                         (const T*)dy, (const T*)s_in, (const W*)gamma, mean, rstd, (T*)dres, (T*)dx, ws,
+                         rows, cols, rpw, seed, offset, thresh, scale);
+    const int64_t ld = 3 * (int64_t)cols;
+    launch_partial_colsum<W>(ws, parts, ld, cols, (W*)dgamma, s);
+    launch_partial_colsum<W>(ws + cols, parts, ld, cols, (W*)dbeta, s);
+    launch_partial_colsum<W>(ws + 2 * cols, parts, ld, cols, (W*)dbias, s);
+  })));
+  return (int)hipGetLastError();
+}
+
+}  // namespace apex

@@ -70,6 +70,57 @@ int layer_norm_bwd(const void* dy, const void* x, const void* gamma, const float
                    int64_t rows, int cols, int xdt, int wdt, int rms, hipStream_t s);
 int64_t layer_norm_bwd_ws_floats(int64_t rows, int cols);
 
+// ----------------------------- flash attention ------------------------------
+// Tensors are [B, S, H, D] views; *_bs / *_ss / *_hs are batch / seq / head strides in
+// elements (the D dimension must be contiguous and 16-byte aligned).
+struct AttnArgs {
+  const void* q;
+  const void* k;
+  const void* v;
+  void* o;
+  float* lse;  // [B*H, Sq] natural-log sum-exp
+  void* dq;
+  int64_t q_bs, q_ss, q_hs, k_bs, k_ss, k_hs, v_bs, v_ss, v_hs, o_bs, o_ss, o_hs;
+  int64_t do_bs, do_ss, do_hs, dq_bs, dq_ss, dq_hs, dk_bs, dk_ss, dk_hs, dv_bs, dv_ss, dv_hs;
+  int B, H, Sq, Sk, D;
+  int causal;
+  float scale, scale_log2;
+  uint32_t drop_thresh;  // keep iff 16-bit uniform >= drop_thresh (0 = no dropout)
+  float drop_scale;      // 1 / (1 - p)
+  uint64_t seed, offset;
+  const int* k_lens;     // optional per-batch valid key length
+};
+int attn_fwd(const AttnArgs& a, int dt, hipStream_t s);
+int attn_bwd(const AttnArgs& a, const void* dout, float* delta, float* dq_acc, void* dk, void* dv,
+             int dt, hipStream_t s);
+int attn_dropout_mask(uint8_t* out, int64_t BH, int Sq, int Sk, uint64_t seed, uint64_t offset,
+                      uint32_t thresh, hipStream_t s);
+
+// ----------------------------- fused elementwise ---------------------------
+// act: 0 gelu(erf), 1 gelu(tanh), 2 relu, 3 identity. cols % 8 == 0.
+int bias_act_fwd(const void* x, const void* b, void* y, int64_t rows, int cols, int act, int xdt,
+                 int bdt, hipStream_t s);
+// ws: >= colsum_parts(rows) * cols floats
+int bias_act_bwd(const void* dy, const void* x, const void* b, void* dx, void* db, float* ws,
+                 int64_t rows, int cols, int act, int xdt, int bdt, hipStream_t s);
+int bias_dropout_add_fwd(const void* x, const void* b, const void* res, void* y, int64_t rows, int cols,
+                         uint64_t seed, uint64_t offset, uint32_t thresh, float scale, int xdt, int bdt,
+                         hipStream_t s);
+int bias_dropout_add_bwd(const void* dy, void* dx, void* db, float* ws, int64_t rows, int cols,
+                         uint64_t seed, uint64_t offset, uint32_t thresh, float scale, int xdt, int bdt,
+                         hipStream_t s);
+int colsum(const void* x, void* out, float* ws, int64_t rows, int cols, int xdt, int odt, hipStream_t s);
+int64_t colsum_parts(int64_t rows);
+int bdaln_supported(int cols);
+int bdaln_fwd(const void* x, const void* b, const void* res, const void* gamma, const void* beta, void* y,
+              void* s_out, float* mean, float* rstd, int64_t rows, int cols, float eps, uint64_t seed,
+              uint64_t offset, uint32_t thresh, float scale, int xdt, int wdt, hipStream_t s);
+int64_t bdaln_ws_floats(int64_t rows, int cols);
+int bdaln_bwd(const void* dy, const void* s_in, const void* gamma, const float* mean, const float* rstd,
+              void* dres, void* dx, void* dgamma, void* dbeta, void* dbias, float* ws, int64_t rows,
+              int cols, uint64_t seed, uint64_t offset, uint32_t thresh, float scale, int xdt, int wdt,
+              hipStream_t s);
+
 // ----------------------------- softmax cross-entropy -----------------------
 int xentropy_fwd(const void* logits, const int64_t* labels, float* losses, float* lse, int64_t rows,
                  int V, float smoothing, int64_t ignore_index, int dt, hipStream_t s);

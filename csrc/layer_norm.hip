@@ -14,7 +14,7 @@
 namespace apex {
 
 constexpr int kLnBlock = 256;
-constexpr int kRowsPerWaveBwd = 4;  // 8192x1024 -> 512 blocks (2/CU)
+constexpr int kMaxBwdParts = 512;  // ~2 blocks per CU; rows per wave adapts to reach it
 
 template <typename T, typename W, int VPT, bool RMS>
 __global__ void __launch_bounds__(kLnBlock) ln_fwd_fast(const T* __restrict__ x,
@@ -93,7 +93,7 @@ __global__ void __launch_bounds__(kLnBlock) ln_bwd_fast(const T* __restrict__ dy
                                                        const float* __restrict__ mean,
                                                        const float* __restrict__ rstd,
                                                        T* __restrict__ dx, float* __restrict__ ws,
-                                                       int64_t rows, int cols) {
+                                                       int64_t rows, int cols, int rpw) {
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [4 waves][2*cols]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int nvec = cols >> 3;
@@ -110,9 +110,9 @@ __global__ void __launch_bounds__(kLnBlock) ln_bwd_fast(const T* __restrict__ dy
     }
     if (gamma && vi < nvec) load_f<W, 8>(gamma + vi * 8, g[j]);
   }
-  const int64_t rows_per_block = (int64_t)kRowsPerWaveBwd * (kLnBlock / 64);
+  const int64_t rows_per_block = (int64_t)rpw * (kLnBlock / 64);
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
-  for (int rr = 0; rr < kRowsPerWaveBwd; ++rr) {
+  for (int rr = 0; rr < rpw; ++rr) {
     const int64_t row = r0 + (int64_t)rr * (kLnBlock / 64) + wid;
     if (row >= rows) break;
     const float mu = RMS ? 0.f : mean[row];
@@ -265,33 +265,6 @@ __global__ void __launch_bounds__(kLnBlock) ln_bwd_gb_slow(const T* __restrict__
   out[cols + c] = db;
 }
 
-// sum ws[parts][2*cols] over parts -> dgamma, dbeta (dtype W)
-template <typename W>
-__global__ void __launch_bounds__(kLnBlock) ln_gb_reduce(const float* __restrict__ ws, int parts,
-                                                        int cols, W* __restrict__ dgamma,
-                                                        W* __restrict__ dbeta) {
-  // block = 64 columns x 4 part-groups
-  __shared__ float red[4][2][64];
-  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
-  float a = 0.f, b = 0.f;
-  if (c < cols) {
-    for (int p = grp; p < parts; p += 4) {
-      a += ws[(int64_t)p * 2 * cols + c];
-      b += ws[(int64_t)p * 2 * cols + cols + c];
-    }
-  }
-  red[grp][0][lane] = a;
-  red[grp][1][lane] = b;
-  __syncthreads();
-  if (grp == 0 && c < cols) {
-    a = red[0][0][lane] + red[1][0][lane] + red[2][0][lane] + red[3][0][lane];
-    b = red[0][1][lane] + red[1][1][lane] + red[2][1][lane] + red[3][1][lane];
-    if (dgamma) dgamma[c] = from_f<W>(a);
-    if (dbeta) dbeta[c] = from_f<W>(b);
-  }
-}
-
 static inline int ln_vpt(int cols) {
   if (cols % 8 != 0) return 0;
   const int nvec = cols / 8;
@@ -307,12 +280,14 @@ static inline bool ln_fast_ok(const void* a, const void* b, const void* c, const
   return ln_vpt(cols) > 0 && al(a) && al(b) && al(c) && al(d);
 }
 
+static inline int ln_bwd_rpw(int64_t rows) {
+  const int64_t r = (rows + 4 * kMaxBwdParts - 1) / (4 * kMaxBwdParts);
+  return r < 1 ? 1 : (int)r;
+}
+
 int64_t layer_norm_bwd_ws_floats(int64_t rows, int cols) {
-  const int64_t rpb = (int64_t)kRowsPerWaveBwd * (kLnBlock / 64);
-  int64_t parts_fast = (rows + rpb - 1) / rpb;
-  int64_t parts_slow = 256;
-  int64_t parts = parts_fast > parts_slow ? parts_fast : parts_slow;
-  return parts * 2 * (int64_t)cols;
+  (void)rows;
+  return (int64_t)kMaxBwdParts * 2 * (int64_t)cols;
 }
 
 #define LN_DISPATCH_T(DT, T, ...)                           \
@@ -363,19 +338,20 @@ int layer_norm_bwd(const void* dy, const void* x, const void* gamma, const float
                    int cols, int xdt, int wdt, int rms, hipStream_t s) {
   if (rows == 0) return 0;
   if (!gamma) wdt = xdt;
-  const bool fast = ln_fast_ok(x, dy, dx, gamma, cols) && (2 * cols * 4 * 4) <= 64 * 1024 * 2;
+  const bool fast = ln_fast_ok(x, dy, dx, gamma, cols) && ln_vpt(cols) <= 4;
   const bool need_gb = dgamma || dbeta;
   LN_DISPATCH_T(xdt, T, LN_DISPATCH_T(wdt, W, LN_DISPATCH_RMS(rms, RMS, {
     int parts;
     if (fast) {
       const int vpt = ln_vpt(cols);
-      const int64_t rpb = (int64_t)kRowsPerWaveBwd * (kLnBlock / 64);
+      const int rpw = ln_bwd_rpw(rows);
+      const int64_t rpb = (int64_t)rpw * (kLnBlock / 64);
       parts = (int)((rows + rpb - 1) / rpb);
       const size_t lds = (size_t)4 * 2 * cols * sizeof(float);
       LN_DISPATCH_VPT(vpt, VPT,
           hipLaunchKernelGGL((ln_bwd_fast<T, W, VPT, RMS>), dim3(parts), dim3(kLnBlock), lds, s,
                              (const T*)dy, (const T*)x, (const W*)gamma, mean, rstd, (T*)dx, ws,
-                             rows, cols));
+                             rows, cols, rpw));
     } else {
       hipLaunchKernelGGL((ln_bwd_dx_slow<T, W, RMS>), dim3((unsigned)rows), dim3(kLnBlock), 0, s,
                          (const T*)dy, (const T*)x, (const W*)gamma, mean, rstd, (T*)dx, cols);
@@ -388,8 +364,8 @@ int layer_norm_bwd(const void* dy, const void* x, const void* gamma, const float
       }
     }
     if (need_gb) {
-      hipLaunchKernelGGL((ln_gb_reduce<W>), dim3((cols + 63) / 64), dim3(kLnBlock), 0, s, ws, parts,
-                         cols, (W*)dgamma, (W*)dbeta);
+      launch_partial_colsum<W>(ws, parts, 2 * (int64_t)cols, cols, (W*)dgamma, s);
+      launch_partial_colsum<W>(ws + cols, parts, 2 * (int64_t)cols, cols, (W*)dbeta, s);
     }
   })));
   return (int)hipGetLastError();

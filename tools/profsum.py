@@ -1,0 +1,7 @@
+import csv, sys
+rows = list(csv.DictReader(open(sys.argv[1])))
+steps = float(sys.argv[2]) if len(sys.argv) > 2 else 1
+tot = sum(float(r['TotalDurationNs']) for r in rows)
+print(f"total {tot/1e6/steps:.2f} ms/step over {steps} steps")
+for r in rows[:int(sys.argv[3]) if len(sys.argv) > 3 else 25]:
+    print(f"{float(r['TotalDurationNs'])/1e6/steps:8.3f} ms/step {float(r['Percentage']):6.2f}% n/step={int(r['Calls'])/steps:7.1f} avg={float(r['AverageNs'])/1e3:8.1f}us {r['Name'][:90]}")
