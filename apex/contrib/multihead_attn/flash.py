@@ -23,23 +23,23 @@ class FlashAttnFunc(torch.autograd.Function):
     def forward(ctx, q, k, v, dropout_p, causal, scale, k_lens):
         C = _ext.require()
         seed, offset = _seed_pair(dropout_p)
-        o, lse = C.flash_attn_fwd(q, k, v, bool(causal), float(scale), float(dropout_p), seed, offset,
+        o, lse, dmask = C.flash_attn_fwd(q, k, v, bool(causal), float(scale), float(dropout_p), seed, offset,
                                   k_lens)
-        ctx.save_for_backward(q, k, v, o, lse, k_lens)
+        ctx.save_for_backward(q, k, v, o, lse, k_lens, dmask)
         ctx.cfg = (dropout_p, causal, scale, seed, offset)
         return o
 
     @staticmethod
     def backward(ctx, do):
         C = _ext.require()
-        q, k, v, o, lse, k_lens = ctx.saved_tensors
+        q, k, v, o, lse, k_lens, dmask = ctx.saved_tensors
         p, causal, scale, seed, offset = ctx.cfg
         do = do.contiguous() if do.stride(-1) != 1 else do
         dq = torch.empty_like(q, memory_format=torch.contiguous_format) if not q.is_contiguous() else torch.empty_like(q)
         dk = torch.empty_like(k, memory_format=torch.contiguous_format) if not k.is_contiguous() else torch.empty_like(k)
         dv = torch.empty_like(v, memory_format=torch.contiguous_format) if not v.is_contiguous() else torch.empty_like(v)
         C.flash_attn_bwd(do, q, k, v, o, lse, dq, dk, dv, bool(causal), float(scale), float(p), seed,
-                         offset, k_lens)
+                         offset, k_lens, dmask)
         return dq, dk, dv, None, None, None, None
 
 
@@ -52,16 +52,16 @@ class FlashAttnPackedFunc(torch.autograd.Function):
         C = _ext.require()
         q, k, v = qkv.unbind(2)
         seed, offset = _seed_pair(dropout_p)
-        o, lse = C.flash_attn_fwd(q, k, v, bool(causal), float(scale), float(dropout_p), seed, offset,
+        o, lse, dmask = C.flash_attn_fwd(q, k, v, bool(causal), float(scale), float(dropout_p), seed, offset,
                                   k_lens)
-        ctx.save_for_backward(qkv, o, lse, k_lens)
+        ctx.save_for_backward(qkv, o, lse, k_lens, dmask)
         ctx.cfg = (dropout_p, causal, scale, seed, offset)
         return o
 
     @staticmethod
     def backward(ctx, do):
         C = _ext.require()
-        qkv, o, lse, k_lens = ctx.saved_tensors
+        qkv, o, lse, k_lens, dmask = ctx.saved_tensors
         p, causal, scale, seed, offset = ctx.cfg
         if do.stride(-1) != 1 or do.stride(1) % 8 or do.stride(0) % 8 or do.stride(2) % 8:
             do = do.contiguous()
@@ -69,7 +69,7 @@ class FlashAttnPackedFunc(torch.autograd.Function):
         dqkv = torch.empty(qkv.shape, dtype=qkv.dtype, device=qkv.device)
         dq, dk, dv = dqkv.unbind(2)
         C.flash_attn_bwd(do, q, k, v, o, lse, dq, dk, dv, bool(causal), float(scale), float(p), seed,
-                         offset, k_lens)
+                         offset, k_lens, dmask)
         return dqkv, None, None, None, None
 
 

@@ -194,20 +194,45 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
     float psum = 0.f;
 #pragma unroll
     for (int sb = 0; sb < 2; ++sb) {
+      // dropout: this lane's 16 keys are 4 groups g of 4 (keys 8g + 4hl + e). Each 8-key
+      // group is one Philox block shared by the two lane halves, so each half generates
+      // two of the four blocks and swaps the other half's chunks over lane^32.
+      uint32_t wlo[2][2], whi[2][2];
+      if (DROPOUT) {
+#pragma unroll
+        for (int gg = 0; gg < 2; ++gg) {
+          const int gme = hl ? gg + 2 : gg;
+          const uint4 rr = dg.block(bh, qrow, (kb + 32 * sb + 8 * gme) >> 3, a.Sq);
+          const uint32_t m0 = hl ? rr.z : rr.x, m1 = hl ? rr.w : rr.y;
+          const uint32_t s0 = hl ? rr.x : rr.z, s1 = hl ? rr.y : rr.w;
+          const uint32_t r0 = __shfl_xor(s0, 32, 64), r1 = __shfl_xor(s1, 32, 64);
+          wlo[gg][0] = hl ? r0 : m0;
+          wlo[gg][1] = hl ? r1 : m1;
+          whi[gg][0] = hl ? m0 : r0;
+          whi[gg][1] = hl ? m1 : r1;
+        }
+      }
+      uint32_t bits = 0;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        uint4 rnd;
-        if (DROPOUT) rnd = dg.block(bh, qrow, (kb + 32 * sb + 8 * g) >> 3, a.Sq);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int i = 4 * g + e;
           const float p = exp2f(st[sb][i] - muse);
           psum += p;
           float pd = p;
-          if (DROPOUT) pd = DropGen::r16(rnd, 4 * hl + e) >= dg.thresh ? p * rkeep : 0.f;
+          if (DROPOUT) {
+            const uint32_t w = g < 2 ? wlo[g & 1][e >> 1] : whi[g & 1][e >> 1];
+            const uint32_t r16 = (e & 1) ? (w >> 16) : (w & 0xffffu);
+            const bool keep = r16 >= dg.thresh;
+            bits |= (uint32_t)keep << i;
+            pd = keep ? p * rkeep : 0.f;
+          }
           st[sb][i] = pd;
         }
       }
+      if (DROPOUT && a.dmask && qrow < a.Sq && kb + 32 * sb < a.Sk)
+        a.dmask[((int64_t)bh * a.Sq + qrow) * a.mask_words + ((kb >> 5) + sb) * 2 + hl] = (uint16_t)bits;
     }
     l = l * alpha + psum;
 #pragma unroll
@@ -255,24 +280,6 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
   }
 }
 
-// delta[bh, q] = sum_d dO * O   (fp32)
-template <typename T, int D>
-__global__ void __launch_bounds__(256) attn_bwd_delta_kernel(AttnArgs a, const void* dout,
-                                                            float* delta) {
-  const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // over B*H*Sq
-  if (row >= (int64_t)a.B * a.H * a.Sq) return;
-  const int q = (int)(row % a.Sq);
-  const int64_t bh = row / a.Sq;
-  const int b = (int)(bh / a.H), h = (int)(bh % a.H);
-  const T* op = (const T*)a.o + b * a.o_bs + h * a.o_hs + (int64_t)q * a.o_ss;
-  const T* dp = (const T*)dout + b * a.do_bs + h * a.do_hs + (int64_t)q * a.do_ss;
-  float s = 0.f;
-  for (int d = lane; d < D; d += 64) s += to_f(op[d]) * to_f(dp[d]);
-  s = wave_sum(s);
-  if (lane == 0) delta[row] = s;
-}
-
 // ---------------------------------------------------------------------------
 // Backward
 // ---------------------------------------------------------------------------
@@ -281,8 +288,7 @@ constexpr int kBwdBK = 32 * kBwdWaves;  // 128 keys per workgroup
 constexpr int kBwdBQ = 32;              // queries per inner step
 
 template <typename T, int D, bool CAUSAL, bool DROPOUT>
-__global__ void __launch_bounds__(256, 1) attn_bwd_kernel(AttnArgs a, const void* dout,
-                                                         const float* delta, float* dq_acc,
+__global__ void __launch_bounds__(256, 1) attn_bwd_kernel(AttnArgs a, const void* dout, float* dq_acc,
                                                          void* dk_out, void* dv_out) {
   using M = MfmaT<T>;
   using V8 = typename M::V8;
@@ -294,6 +300,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_kernel(AttnArgs a, const void
   __shared__ __attribute__((aligned(16))) T lds_ds[kBwdBQ * LDS_S];
   __shared__ float lds_lse[kBwdBQ], lds_delta[kBwdBQ];
   __shared__ float lds_dqred[(D == 64) ? 2048 : 1];
+  __shared__ uint16_t lds_mask[kBwdBQ * 8];  // [q][4 key blocks][2 halves]
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int r = lane & 31, hl = lane >> 5;
@@ -307,8 +314,8 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_kernel(AttnArgs a, const void
   const T* kp = (const T*)a.k + b * a.k_bs + h * a.k_hs;
   const T* vp = (const T*)a.v + b * a.v_bs + h * a.v_hs;
   const T* dop = (const T*)dout + b * a.do_bs + h * a.do_hs;
+  const T* op = (const T*)a.o + b * a.o_bs + h * a.o_hs;
   const float* lsep = a.lse + (int64_t)bh * a.Sq;
-  const float* delp = delta + (int64_t)bh * a.Sq;
 
   // K and V rows for this wave's 32 keys as B operands: lane (key=r, hl) holds X[key][16s+8hl..]
   V8 kf[D / 16], vf[D / 16];
@@ -348,22 +355,43 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_kernel(AttnArgs a, const void
 
   for (int qb = qstart; qb < nq; qb += kBwdBQ) {
     __syncthreads();
-    // stage Q, dO tiles (32 x D) + lse/delta
-    for (int idx = threadIdx.x; idx < kBwdBQ * (D / 8); idx += 256) {
-      const int row = idx / (D / 8), col = (idx % (D / 8)) * 8;
+    // stage Q, dO tiles (32 x D) + lse; delta = rowsum(dO * O) computed here from O
+    // (CPR consecutive threads own one row -> xor-shuffle reduce), no separate pass.
+    constexpr int CPR = D / 8;
+#pragma unroll
+    for (int c = 0; c < kBwdBQ * CPR / 256; ++c) {
+      const int idx = threadIdx.x + 256 * c;
+      const int row = idx / CPR, col = (idx % CPR) * 8;
       const int q = qb + row;
       uint4 qv = make_uint4(0, 0, 0, 0), dv4 = make_uint4(0, 0, 0, 0);
+      float part = 0.f;
       if (q < nq) {
         qv = *(const uint4*)(qp + (int64_t)q * a.q_ss + col);
         dv4 = *(const uint4*)(dop + (int64_t)q * a.do_ss + col);
+        float ov[8], dov[8];
+        load_f<T, 8>(op + (int64_t)q * a.o_ss + col, ov);
+        load_f<T, 8>((const T*)&dv4, dov);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) part += ov[e] * dov[e];
       }
+#pragma unroll
+      for (int o = CPR / 2; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+      if ((idx % CPR) == 0) lds_delta[row] = part;
       *(uint4*)(lds_q + row * LDR + col) = qv;
       *(uint4*)(lds_do + row * LDR + col) = dv4;
     }
     if (threadIdx.x < kBwdBQ) {
       const int q = qb + threadIdx.x;
       lds_lse[threadIdx.x] = q < nq ? lsep[q] * kLog2e : INFINITY;
-      lds_delta[threadIdx.x] = q < nq ? delp[q] : 0.f;
+    }
+    if (DROPOUT) {
+      // dropout bits written by the forward pass: [q][32-key block][half] uint16 words
+      const int qi = threadIdx.x >> 3, w = threadIdx.x & 7;
+      const int q = qb + qi, blk = (k0 >> 5) + (w >> 1);
+      uint16_t word = 0;
+      if (q < nq && blk * 32 < a.Sk)
+        word = a.dmask[((int64_t)bh * a.Sq + q) * a.mask_words + blk * 2 + (w & 1)];
+      lds_mask[threadIdx.x] = word;
     }
     __syncthreads();
 
@@ -378,9 +406,10 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_kernel(AttnArgs a, const void
     }
     // element i: q = qb + (i&3) + 8(i>>2) + 4hl, key = mykey
     float pd[16], ds[16];
+    // this lane's key within its 32-key block: forward stored it as bit kbit of half khalf
+    const int khalf = (r >> 2) & 1, kbit = (r & 3) + 4 * (r >> 3);
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      uint4 rnd;
       const int qr0 = (g * 8) + 4 * hl;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -391,10 +420,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_kernel(AttnArgs a, const void
         bool valid = (mykey < Sk) && (q < nq) && !(CAUSAL && mykey > q);
         const float p = valid ? exp2f(t) : 0.f;
         float keep = 1.f;
-        if (DROPOUT) {
-          rnd = dg.block(bh, q, mykey >> 3, a.Sq);
-          keep = DropGen::r16(rnd, mykey & 7) >= dg.thresh ? rkeep : 0.f;
-        }
+        if (DROPOUT) keep = ((lds_mask[qi * 8 + wid * 2 + khalf] >> kbit) & 1) ? rkeep : 0.f;
         pd[i] = p * keep;                                   // dropped P (for dV)
         const float dpv = dpacc[i] * keep;                  // dP through dropout
         ds[i] = p * (dpv - lds_delta[qi]) * a.scale;        // dS (includes softmax scale)
@@ -464,9 +490,11 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_kernel(AttnArgs a, const void
         for (int i = 0; i < 16; ++i) {
           const int q = qb + (i & 3) + 8 * (i >> 2) + 4 * hl;
           if (q < nq) {
-            float* dst = dq_acc + ((int64_t)bh * a.Sq + q) * D + 32 * cb + r;
-            if (single_kblock) *dst = dq[i];  // sole writer of this (b, h) query block
-            else atomicAdd(dst, dq[i]);
+            if (single_kblock) {  // sole writer of this (b, h) query block: final dtype, strided
+              ((T*)a.dq)[b * a.dq_bs + h * a.dq_hs + (int64_t)q * a.dq_ss + 32 * cb + r] = (T)dq[i];
+            } else {
+              atomicAdd(dq_acc + ((int64_t)bh * a.Sq + q) * D + 32 * cb + r, dq[i]);
+            }
           }
         }
       }
@@ -555,22 +583,26 @@ int attn_fwd(const AttnArgs& a, int dt, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-int attn_bwd(const AttnArgs& a, const void* dout, float* delta, float* dq_acc, void* dk, void* dv,
-             int dt, hipStream_t s) {
+bool attn_bwd_needs_dq_acc(const AttnArgs& a) { return a.Sk > kBwdBK; }
+
+int attn_bwd(const AttnArgs& a, const void* dout, float* dq_acc, void* dk, void* dv, int dt,
+             hipStream_t s) {
   if (a.B * a.H == 0 || a.Sq == 0) return 0;
   const bool drop = a.drop_thresh > 0;
+  if (drop && !a.dmask) return -3;  // backward needs the forward's dropout bits
   const int64_t rows = (int64_t)a.B * a.H * a.Sq;
-  hipMemsetAsync(dq_acc, 0, rows * a.D * sizeof(float), s);
+  const bool multi = attn_bwd_needs_dq_acc(a);
+  if (multi) hipMemsetAsync(dq_acc, 0, rows * a.D * sizeof(float), s);
   ATTN_DISPATCH(dt, T, ATTN_DISPATCH_D(a.D, D, {
-    hipLaunchKernelGGL((attn_bwd_delta_kernel<T, D>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0,
-                       s, a, dout, delta);
     dim3 grid((a.Sk + kBwdBK - 1) / kBwdBK, a.B * a.H);
     ATTN_DISPATCH_B(a.causal, C, ATTN_DISPATCH_B(drop, DR,
-        hipLaunchKernelGGL((attn_bwd_kernel<T, D, C, DR>), grid, dim3(256), 0, s, a, dout, delta,
-                           dq_acc, dk, dv)));
-    const int64_t tot = rows * (D / 8);
-    hipLaunchKernelGGL((attn_dq_convert<T, D>), dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s,
-                       a, dq_acc);
+        hipLaunchKernelGGL((attn_bwd_kernel<T, D, C, DR>), grid, dim3(256), 0, s, a, dout, dq_acc, dk,
+                           dv)));
+    if (multi) {
+      const int64_t tot = rows * (D / 8);
+      hipLaunchKernelGGL((attn_dq_convert<T, D>), dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s,
+                         a, dq_acc);
+    }
   }));
   return (int)hipGetLastError();
 }

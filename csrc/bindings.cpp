@@ -332,13 +332,22 @@ std::vector<Tensor> flash_attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, do
   a.o = o.data_ptr();
   attn_set(a, o, a.o_bs, a.o_ss, a.o_hs);
   a.lse = lse.data_ptr<float>();
+  a.mask_words = 2 * (((int64_t)a.Sk + 31) / 32);
+  Tensor dmask;  // dropout keep bits, consumed by the backward pass
+  if (a.drop_thresh) {
+    dmask = at::empty({(int64_t)a.B * a.H * a.Sq * a.mask_words}, q.options().dtype(at::kShort));
+    a.dmask = (uint16_t*)dmask.data_ptr();
+  } else {
+    dmask = at::empty({0}, q.options().dtype(at::kShort));
+  }
   check(apex::attn_fwd(a, dt_code(q.scalar_type()), cur_stream()), "attn_fwd");
-  return {o, lse};
+  return {o, lse, dmask};
 }
 
 void flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor dq,
                     Tensor dk, Tensor dv, bool causal, double scale, double p_drop, int64_t seed,
-                    int64_t offset, const c10::optional<Tensor>& k_lens) {
+                    int64_t offset, const c10::optional<Tensor>& k_lens,
+                    const c10::optional<Tensor>& dmask) {
   apex::AttnArgs a = attn_common(q, k, v, causal, scale, p_drop, seed, offset, k_lens);
   a.o = o.data_ptr();
   attn_set(a, o, a.o_bs, a.o_ss, a.o_hs);
@@ -348,10 +357,16 @@ void flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor 
   attn_set(a, dk, a.dk_bs, a.dk_ss, a.dk_hs);
   attn_set(a, dv, a.dv_bs, a.dv_ss, a.dv_hs);
   a.dq = dq.data_ptr();
+  a.mask_words = 2 * (((int64_t)a.Sk + 31) / 32);
+  if (a.drop_thresh) {
+    TORCH_CHECK(dmask.has_value() && dmask->numel() == (int64_t)a.B * a.H * a.Sq * a.mask_words,
+                "flash_attn_bwd: dropout mask from the forward pass is required");
+    a.dmask = (uint16_t*)dmask->data_ptr();
+  }
   const int64_t rows = (int64_t)a.B * a.H * a.Sq;
-  Tensor delta = at::empty({rows}, q.options().dtype(at::kFloat));
-  Tensor dq_acc = at::empty({rows * a.D}, q.options().dtype(at::kFloat));
-  check(apex::attn_bwd(a, dout.data_ptr(), delta.data_ptr<float>(), dq_acc.data_ptr<float>(),
+  Tensor dq_acc;
+  if (apex::attn_bwd_needs_dq_acc(a)) dq_acc = at::empty({rows * a.D}, q.options().dtype(at::kFloat));
+  check(apex::attn_bwd(a, dout.data_ptr(), dq_acc.defined() ? dq_acc.data_ptr<float>() : nullptr,
                        dk.data_ptr(), dv.data_ptr(), dt_code(q.scalar_type()), cur_stream()),
         "attn_bwd");
 }

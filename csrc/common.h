@@ -89,37 +89,52 @@ __device__ __forceinline__ float block_max(float v, float* red) {
 // loads of 64-byte row segments, the 16 groups combine in LDS. Launch with
 // grid = ceil(cols / 16). Deterministic (fixed summation order).
 // ---------------------------------------------------------------------------
-template <typename W, typename Conv>
+// Up to 3 column sets of `cols` each, laid out consecutively in a partial row
+// (e.g. [dgamma | dbeta | dbias]); set k is written to outs[k] (null -> skipped).
+template <typename W>
+struct ColsumOuts {
+  W* o[3];
+};
+
+template <typename W>
 __global__ void __launch_bounds__(256) partial_colsum_kernel(const float* __restrict__ part, int parts,
-                                                            int64_t ld, int cols, W* __restrict__ out,
-                                                            Conv conv) {
+                                                            int64_t ld, int cols, int nsets,
+                                                            ColsumOuts<W> outs) {
   __shared__ float red[16][17];
   const int cl = threadIdx.x & 15, grp = threadIdx.x >> 4;
-  const int c = blockIdx.x * 16 + cl;
+  const int c = blockIdx.x * 16 + cl;  // over nsets * cols
+  const int set = c / cols;
+  const bool live = c < nsets * cols && outs.o[set < 3 ? set : 0] != nullptr;
   float a = 0.f;
-  if (c < cols)
+  if (live) {
+#pragma unroll 4
     for (int p = grp; p < parts; p += 16) a += part[(int64_t)p * ld + c];
+  }
   red[grp][cl] = a;
   __syncthreads();
-  if (grp == 0 && c < cols) {
+  if (grp == 0 && live) {
     float t = 0.f;
 #pragma unroll
     for (int g = 0; g < 16; ++g) t += red[g][cl];
-    out[c] = conv(t);
+    outs.o[set][c - set * cols] = (W)t;
   }
 }
 
 template <typename W>
-struct ToW {
-  __device__ __forceinline__ W operator()(float v) const { return (W)v; }
-};
+inline void launch_partial_colsum3(const float* part, int parts, int64_t ld, int cols, W* o0, W* o1,
+                                   W* o2, hipStream_t s) {
+  const int nsets = o2 ? 3 : (o1 ? 2 : 1);
+  if (cols <= 0) return;
+  ColsumOuts<W> outs{{o0, o1, o2}};
+  hipLaunchKernelGGL((partial_colsum_kernel<W>), dim3((nsets * cols + 15) / 16), dim3(256), 0, s, part,
+                     parts, ld, cols, nsets, outs);
+}
 
 template <typename W>
 inline void launch_partial_colsum(const float* part, int parts, int64_t ld, int cols, W* out,
                                   hipStream_t s) {
-  if (!out || cols <= 0) return;
-  hipLaunchKernelGGL((partial_colsum_kernel<W, ToW<W>>), dim3((cols + 15) / 16), dim3(256), 0, s, part,
-                     parts, ld, cols, out, ToW<W>{});
+  if (!out) return;
+  launch_partial_colsum3<W>(part, parts, ld, cols, out, nullptr, nullptr, s);
 }
 
 // ---------------------------------------------------------------------------

@@ -536,9 +536,7 @@ int bdaln_bwd(const void* dy, const void* s_in, const void* gamma, const float* 
                          (const T*)dy, (const T*)s_in, (const W*)gamma, mean, rstd, (T*)dres, (T*)dx, ws,
                          rows, cols, rpw, seed, offset, thresh, scale);
     const int64_t ld = 3 * (int64_t)cols;
-    launch_partial_colsum<W>(ws, parts, ld, cols, (W*)dgamma, s);
-    launch_partial_colsum<W>(ws + cols, parts, ld, cols, (W*)dbeta, s);
-    launch_partial_colsum<W>(ws + 2 * cols, parts, ld, cols, (W*)dbias, s);
+    launch_partial_colsum3<W>(ws, parts, ld, cols, (W*)dgamma, (W*)dbeta, (W*)dbias, s);
   })));
   return (int)hipGetLastError();
 }

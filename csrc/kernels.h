@@ -89,10 +89,13 @@ struct AttnArgs {
   float drop_scale;      // 1 / (1 - p)
   uint64_t seed, offset;
   const int* k_lens;     // optional per-batch valid key length
+  uint16_t* dmask;       // dropout keep bits [B*H, Sq, mask_words] (fwd writes, bwd reads)
+  int64_t mask_words;    // 2 * ceil(Sk / 32)
 };
 int attn_fwd(const AttnArgs& a, int dt, hipStream_t s);
-int attn_bwd(const AttnArgs& a, const void* dout, float* delta, float* dq_acc, void* dk, void* dv,
-             int dt, hipStream_t s);
+bool attn_bwd_needs_dq_acc(const AttnArgs& a);
+int attn_bwd(const AttnArgs& a, const void* dout, float* dq_acc, void* dk, void* dv, int dt,
+             hipStream_t s);
 int attn_dropout_mask(uint8_t* out, int64_t BH, int Sq, int Sk, uint64_t seed, uint64_t offset,
                       uint32_t thresh, hipStream_t s);
 

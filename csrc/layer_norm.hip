@@ -364,8 +364,7 @@ int layer_norm_bwd(const void* dy, const void* x, const void* gamma, const float
       }
     }
     if (need_gb) {
-      launch_partial_colsum<W>(ws, parts, 2 * (int64_t)cols, cols, (W*)dgamma, s);
-      launch_partial_colsum<W>(ws + cols, parts, 2 * (int64_t)cols, cols, (W*)dbeta, s);
+      launch_partial_colsum3<W>(ws, parts, 2 * (int64_t)cols, cols, (W*)dgamma, (W*)dbeta, (W*)nullptr, s);
     }
   })));
   return (int)hipGetLastError();

@@ -51,11 +51,14 @@ def test_bias_dropout_add(p):
     x = torch.randn(rows, cols, device=DEV).bfloat16().requires_grad_(True)
     b = torch.randn(cols, device=DEV).bfloat16().requires_grad_(True)
     r = torch.randn(rows, cols, device=DEV).bfloat16().requires_grad_(True)
+    torch.manual_seed(7)
     y = fused.bias_dropout_add(x, b, r, p)
-    # recover the mask: with res=0 the kept entries are (x+b)*scale
+    # recover the mask: same seed, res = 0, x + b = 1 -> kept entries are exactly `scale`
+    torch.manual_seed(7)
+    ones = fused.bias_dropout_add(torch.ones_like(x), torch.zeros_like(b), torch.zeros_like(r), p)
+    keep = ones.detach().float() != 0
     t = (x + b).detach().float()
     delta = (y - r).detach().float()
-    keep = delta != 0
     if p > 0:
         frac = keep.float().mean().item()
         assert abs(frac - (1 - p)) < 0.02
