@@ -489,6 +489,171 @@ std::vector<Tensor> k_bdaln_bwd(Tensor dy, Tensor s, Tensor gamma, Tensor mean, 
   return {dres, dx, dgamma, dbeta, dbias};
 }
 
+// --------------------------------------------------------------------------
+// weight norm: v viewed as [R, C]; row_mode: one norm per row (dim=0), else per column
+// --------------------------------------------------------------------------
+std::vector<Tensor> k_wn_fwd(Tensor v, Tensor g, bool row_mode) {
+  Tensor vc = v.contiguous();
+  const int64_t R = row_mode ? vc.size(0) : vc.numel() / vc.size(-1);
+  const int64_t C = vc.numel() / std::max<int64_t>(R, 1);
+  Tensor w = at::empty_like(vc);
+  Tensor norms = at::empty({row_mode ? R : C}, vc.options().dtype(at::kFloat));
+  Tensor gc = g.contiguous();
+  check(apex::weight_norm_fwd(vc.data_ptr(), gc.data_ptr(), w.data_ptr(), norms.data_ptr<float>(), R, C,
+                              row_mode, dt_code(vc.scalar_type()), dt_code(gc.scalar_type()), cur_stream()),
+        "weight_norm_fwd");
+  return {w, norms};
+}
+
+std::vector<Tensor> k_wn_bwd(Tensor dw, Tensor v, Tensor g, Tensor norms, bool row_mode) {
+  Tensor vc = v.contiguous(), dwc = dw.contiguous(), gc = g.contiguous();
+  const int64_t R = row_mode ? vc.size(0) : vc.numel() / vc.size(-1);
+  const int64_t C = vc.numel() / std::max<int64_t>(R, 1);
+  Tensor dv = at::empty_like(vc), dg = at::empty_like(gc);
+  check(apex::weight_norm_bwd(dwc.data_ptr(), vc.data_ptr(), gc.data_ptr(), norms.data_ptr<float>(),
+                              dv.data_ptr(), dg.data_ptr(), R, C, row_mode, dt_code(vc.scalar_type()),
+                              dt_code(gc.scalar_type()), cur_stream()),
+        "weight_norm_bwd");
+  return {dv, dg};
+}
+
+// --------------------------------------------------------------------------
+// RNN cells (gates precomputed by GEMMs): PyTorch gate order
+// --------------------------------------------------------------------------
+std::vector<Tensor> k_lstm_fwd(Tensor ig, const c10::optional<Tensor>& hg, const c10::optional<Tensor>& bih,
+                               const c10::optional<Tensor>& bhh, Tensor cx) {
+  Tensor igc = ig.contiguous(), cxc = cx.contiguous();
+  const int64_t B = cxc.size(0), H = cxc.size(1);
+  Tensor hy = at::empty_like(cxc), cy = at::empty_like(cxc);
+  Tensor ws = at::empty({B * 5 * H}, cxc.options().dtype(at::kFloat));
+  c10::optional<Tensor> hgc = hg.has_value() && hg->defined() ? c10::optional<Tensor>(hg->contiguous()) : c10::nullopt;
+  check(apex::lstm_cell_fwd(igc.data_ptr(), opt_vptr(hgc), opt_vptr(bih), opt_vptr(bhh), cxc.data_ptr(),
+                            hy.data_ptr(), cy.data_ptr(), ws.data_ptr<float>(), B, H,
+                            dt_code(cxc.scalar_type()), cur_stream()),
+        "lstm_cell_fwd");
+  return {hy, cy, ws};
+}
+
+std::vector<Tensor> k_lstm_bwd(const c10::optional<Tensor>& dhy, const c10::optional<Tensor>& dcy, Tensor cx,
+                               Tensor ws) {
+  Tensor cxc = cx.contiguous();
+  const int64_t B = cxc.size(0), H = cxc.size(1);
+  Tensor dg = at::empty({B, 4 * H}, cxc.options()), dcx = at::empty_like(cxc);
+  c10::optional<Tensor> a = dhy.has_value() && dhy->defined() ? c10::optional<Tensor>(dhy->contiguous()) : c10::nullopt;
+  c10::optional<Tensor> c = dcy.has_value() && dcy->defined() ? c10::optional<Tensor>(dcy->contiguous()) : c10::nullopt;
+  check(apex::lstm_cell_bwd(opt_vptr(a), opt_vptr(c), cxc.data_ptr(), ws.data_ptr<float>(), dg.data_ptr(),
+                            dcx.data_ptr(), B, H, dt_code(cxc.scalar_type()), cur_stream()),
+        "lstm_cell_bwd");
+  return {dg, dcx};
+}
+
+std::vector<Tensor> k_gru_fwd(Tensor ig, Tensor hg, const c10::optional<Tensor>& bih,
+                              const c10::optional<Tensor>& bhh, Tensor hx) {
+  Tensor igc = ig.contiguous(), hgc = hg.contiguous(), hxc = hx.contiguous();
+  const int64_t B = hxc.size(0), H = hxc.size(1);
+  Tensor hy = at::empty_like(hxc);
+  Tensor ws = at::empty({B * 4 * H}, hxc.options().dtype(at::kFloat));
+  check(apex::gru_cell_fwd(igc.data_ptr(), hgc.data_ptr(), opt_vptr(bih), opt_vptr(bhh), hxc.data_ptr(),
+                           hy.data_ptr(), ws.data_ptr<float>(), B, H, dt_code(hxc.scalar_type()), cur_stream()),
+        "gru_cell_fwd");
+  return {hy, ws};
+}
+
+std::vector<Tensor> k_gru_bwd(Tensor dhy, Tensor hx, Tensor ws) {
+  Tensor hxc = hx.contiguous(), d = dhy.contiguous();
+  const int64_t B = hxc.size(0), H = hxc.size(1);
+  Tensor dig = at::empty({B, 3 * H}, hxc.options()), dhg = at::empty({B, 3 * H}, hxc.options());
+  Tensor dhx = at::empty_like(hxc);
+  check(apex::gru_cell_bwd(d.data_ptr(), hxc.data_ptr(), ws.data_ptr<float>(), dig.data_ptr(), dhg.data_ptr(),
+                           dhx.data_ptr(), B, H, dt_code(hxc.scalar_type()), cur_stream()),
+        "gru_cell_bwd");
+  return {dig, dhg, dhx};
+}
+
+// --------------------------------------------------------------------------
+// SyncBatchNorm: x viewed as [N, C, S] (NCHW) or [N, S, C] (nhwc)
+// --------------------------------------------------------------------------
+std::vector<int64_t> bn_dims(const Tensor& x, bool nhwc) {
+  const int64_t N = x.size(0);
+  const int64_t C = nhwc ? x.size(-1) : x.size(1);
+  const int64_t S = x.numel() / std::max<int64_t>(N * C, 1);
+  return {N, C, S};
+}
+
+// local per-channel (mean, m2, count) triples [C, 3]
+Tensor k_bn_local_stats(Tensor x, bool nhwc) {
+  TORCH_CHECK(x.is_contiguous(), "syncbn: input must be contiguous in its layout");
+  auto d = bn_dims(x, nhwc);
+  const int sp = apex::bn_splits_for(d[0], d[1], d[2]);
+  auto fo = x.options().dtype(at::kFloat);
+  Tensor part = at::empty({d[1] * sp * 3}, fo);
+  int spo = 0;
+  check(apex::bn_stats(x.data_ptr(), part.data_ptr<float>(), d[0], d[1], d[2], nhwc, dt_code(x.scalar_type()),
+                       &spo, cur_stream()),
+        "bn_stats");
+  Tensor out = at::empty({d[1], 3}, fo);
+  Tensor mean = at::empty({d[1]}, fo), var = at::empty({d[1]}, fo), cnt = at::empty({d[1]}, fo);
+  check(apex::bn_combine(part.data_ptr<float>(), spo, d[1], 0, mean.data_ptr<float>(), var.data_ptr<float>(),
+                         cnt.data_ptr<float>(), cur_stream()),
+        "bn_combine");
+  // triple = (mean, m2 = var*count, count)
+  return at::stack({mean, var * cnt, cnt}, 1).contiguous();
+}
+
+// gathered [G, C, 3] -> (mean, biased var, count)
+std::vector<Tensor> k_bn_combine(Tensor gathered) {
+  Tensor g = gathered.contiguous();
+  const int groups = (int)g.size(0);
+  const int64_t C = g.size(1);
+  auto fo = g.options().dtype(at::kFloat);
+  Tensor mean = at::empty({C}, fo), var = at::empty({C}, fo), cnt = at::empty({C}, fo);
+  check(apex::bn_combine(g.data_ptr<float>(), groups, C, 1, mean.data_ptr<float>(), var.data_ptr<float>(),
+                         cnt.data_ptr<float>(), cur_stream()),
+        "bn_combine");
+  return {mean, var, cnt};
+}
+
+Tensor k_bn_elemt(Tensor x, Tensor mean, Tensor invstd, const c10::optional<Tensor>& w,
+                  const c10::optional<Tensor>& b, bool nhwc, bool relu) {
+  auto d = bn_dims(x, nhwc);
+  Tensor y = at::empty_like(x);
+  const int wdt = w.has_value() && w->defined() ? dt_code(w->scalar_type()) : apex::kF32Code;
+  check(apex::bn_elemt(x.data_ptr(), mean.data_ptr<float>(), invstd.data_ptr<float>(), opt_vptr(w), opt_vptr(b),
+                       y.data_ptr(), d[0], d[1], d[2], nhwc, relu, dt_code(x.scalar_type()), wdt, cur_stream()),
+        "bn_elemt");
+  return y;
+}
+
+// local (sum_dy, sum_dy_xmu) -> [2, C]
+Tensor k_bn_bwd_reduce(Tensor dy, Tensor x, Tensor mean, bool nhwc) {
+  auto d = bn_dims(x, nhwc);
+  Tensor dyc = dy.contiguous();
+  const int sp = apex::bn_splits_for(d[0], d[1], d[2]);
+  auto fo = x.options().dtype(at::kFloat);
+  Tensor part = at::empty({d[1] * sp * 2}, fo);
+  Tensor out = at::empty({2, d[1]}, fo);
+  check(apex::bn_bwd_reduce(dyc.data_ptr(), x.data_ptr(), mean.data_ptr<float>(), part.data_ptr<float>(),
+                            out.data_ptr<float>(), out.data_ptr<float>() + d[1], d[0], d[1], d[2], nhwc,
+                            dt_code(x.scalar_type()), cur_stream()),
+        "bn_bwd_reduce");
+  return out;
+}
+
+Tensor k_bn_bwd_elemt(Tensor dy, Tensor x, Tensor mean, Tensor invstd, const c10::optional<Tensor>& w,
+                      Tensor sums, double total_count, bool nhwc) {
+  auto d = bn_dims(x, nhwc);
+  Tensor dyc = dy.contiguous();
+  Tensor dx = at::empty_like(x);
+  Tensor sc = sums.contiguous();
+  const int wdt = w.has_value() && w->defined() ? dt_code(w->scalar_type()) : apex::kF32Code;
+  check(apex::bn_bwd_elemt(dyc.data_ptr(), x.data_ptr(), mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                           opt_vptr(w), sc.data_ptr<float>(), sc.data_ptr<float>() + d[1],
+                           (float)(1.0 / total_count), dx.data_ptr(), d[0], d[1], d[2], nhwc,
+                           dt_code(x.scalar_type()), wdt, cur_stream()),
+        "bn_bwd_elemt");
+  return dx;
+}
+
 Tensor flash_dropout_mask(int64_t B, int64_t H, int64_t Sq, int64_t Sk, double p_drop, int64_t seed,
                           int64_t offset, at::Device dev) {
   Tensor out = at::empty({B, H, Sq, Sk}, at::TensorOptions().dtype(at::kByte).device(dev));
@@ -527,6 +692,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("flash_attn_fwd", &flash_attn_fwd);
   m.def("flash_attn_bwd", &flash_attn_bwd);
   m.def("flash_dropout_mask", &flash_dropout_mask);
+  m.def("weight_norm_fwd", &k_wn_fwd);
+  m.def("weight_norm_bwd", &k_wn_bwd);
+  m.def("lstm_cell_fwd", &k_lstm_fwd);
+  m.def("lstm_cell_bwd", &k_lstm_bwd);
+  m.def("gru_cell_fwd", &k_gru_fwd);
+  m.def("gru_cell_bwd", &k_gru_bwd);
+  m.def("bn_local_stats", &k_bn_local_stats);
+  m.def("bn_combine", &k_bn_combine);
+  m.def("bn_elemt", &k_bn_elemt);
+  m.def("bn_bwd_reduce", &k_bn_bwd_reduce);
+  m.def("bn_bwd_elemt", &k_bn_bwd_elemt);
   m.def("bias_act_fwd", &k_bias_act_fwd);
   m.def("bias_act_bwd", &k_bias_act_bwd);
   m.def("bias_dropout_add_fwd", &k_bda_fwd);

@@ -124,6 +124,32 @@ int bdaln_bwd(const void* dy, const void* s_in, const void* gamma, const float* 
               int cols, uint64_t seed, uint64_t offset, uint32_t thresh, float scale, int xdt, int wdt,
               hipStream_t s);
 
+// ----------------------------- weight norm / RNN cells / SyncBN ------------
+int weight_norm_fwd(const void* v, const void* g, void* w, float* norms, int64_t R, int64_t C, int row_mode,
+                    int vdt, int gdt, hipStream_t s);
+int weight_norm_bwd(const void* dw, const void* v, const void* g, const float* norms, void* dv, void* dg,
+                    int64_t R, int64_t C, int row_mode, int vdt, int gdt, hipStream_t s);
+int lstm_cell_fwd(const void* ig, const void* hg, const void* bih, const void* bhh, const void* cx, void* hy,
+                  void* cy, float* ws, int64_t B, int64_t H, int dt, hipStream_t s);
+int lstm_cell_bwd(const void* dhy, const void* dcy, const void* cx, const float* ws, void* dgates, void* dcx,
+                  int64_t B, int64_t H, int dt, hipStream_t s);
+int gru_cell_fwd(const void* ig, const void* hg, const void* bih, const void* bhh, const void* hx, void* hy,
+                 float* ws, int64_t B, int64_t H, int dt, hipStream_t s);
+int gru_cell_bwd(const void* dhy, const void* hx, const float* ws, void* dig, void* dhg, void* dhx, int64_t B,
+                 int64_t H, int dt, hipStream_t s);
+int bn_splits_for(int64_t N, int64_t C, int64_t S);
+int bn_stats(const void* x, float* part, int64_t N, int64_t C, int64_t S, int nhwc, int dt, int* splits_out,
+             hipStream_t s);
+int bn_combine(const float* in, int groups, int64_t C, int gmajor, float* mean, float* var, float* count,
+               hipStream_t s);
+int bn_elemt(const void* x, const float* mean, const float* invstd, const void* w, const void* b, void* y,
+             int64_t N, int64_t C, int64_t S, int nhwc, int relu, int dt, int wdt, hipStream_t s);
+int bn_bwd_reduce(const void* dy, const void* x, const float* mean, float* part, float* sum_dy,
+                  float* sum_dy_xmu, int64_t N, int64_t C, int64_t S, int nhwc, int dt, hipStream_t s);
+int bn_bwd_elemt(const void* dy, const void* x, const float* mean, const float* invstd, const void* w,
+                 const float* sum_dy, const float* sum_dy_xmu, float inv_count, void* dx, int64_t N, int64_t C,
+                 int64_t S, int nhwc, int dt, int wdt, hipStream_t s);
+
 // ----------------------------- softmax cross-entropy -----------------------
 int xentropy_fwd(const void* logits, const int64_t* labels, float* losses, float* lse, int64_t rows,
                  int V, float smoothing, int64_t ignore_index, int dt, hipStream_t s);

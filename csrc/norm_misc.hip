@@ -1,0 +1,494 @@
+// Weight norm (K-03), LSTM/GRU cell pointwise (K-06) and SyncBatchNorm (NS-04) kernels.
+//
+// Weight norm  w = g * v / ||v||, norm over every dim except `dim`:
+//   dim == 0   -> "row" layout [R, C] (one norm per row): one 256-thread block per row,
+//                 two passes over the row (the second from L2);
+//   dim == last-> "col" layout [R, C] (one norm per column): each thread owns one column and
+//                 walks the rows (coalesced across threads), fp32 accumulation.
+// LSTM / GRU cells: everything after the two GEMMs of a step in ONE kernel each way
+// (gate bias adds, sigmoid/tanh, cell update), fp32 math, gate grads written once so the
+// caller's GEMMs produce dx/dh/dW; bias grads come from colsum of the gate grads.
+// SyncBN: per-channel Welford partials (NCHW or NHWC), combine to global mean/invstd after
+// the caller's all-reduce/all-gather, fused normalise(+ReLU), backward reductions
+// (sum dy, sum dy*(x-mean)) and the elementwise dx.
+#include "common.h"
+#include "kernels.h"
+
+namespace apex {
+
+#define NM_DISPATCH(DT, T, ...)                             \
+  switch (DT) {                                             \
+    case kF32: { using T = float; __VA_ARGS__; } break;     \
+    case kF16: { using T = f16; __VA_ARGS__; } break;       \
+    case kBF16: { using T = bf16; __VA_ARGS__; } break;     \
+    default: return -1;                                     \
+  }
+
+// ============================ weight norm ===================================
+template <typename T, typename G>
+__global__ void __launch_bounds__(256) wn_row_fwd(const T* __restrict__ v, const G* __restrict__ g,
+                                                 T* __restrict__ w, float* __restrict__ norms, int64_t C) {
+  __shared__ float red[4];
+  const int64_t r = blockIdx.x;
+  const T* vr = v + r * C;
+  float s = 0.f;
+  for (int64_t c = threadIdx.x; c < C; c += 256) {
+    const float x = to_f(vr[c]);
+    s += x * x;
+  }
+  const float n = sqrtf(block_sum(s, red));
+  if (threadIdx.x == 0) norms[r] = n;
+  const float sc = to_f(g[r]) / n;
+  T* wr = w + r * C;
+  for (int64_t c = threadIdx.x; c < C; c += 256) wr[c] = from_f<T>(to_f(vr[c]) * sc);
+}
+
+template <typename T, typename G>
+__global__ void __launch_bounds__(256) wn_row_bwd(const T* __restrict__ dw, const T* __restrict__ v,
+                                                 const G* __restrict__ g, const float* __restrict__ norms,
+                                                 T* __restrict__ dv, G* __restrict__ dg, int64_t C) {
+  __shared__ float red[4];
+  const int64_t r = blockIdx.x;
+  const T* vr = v + r * C;
+  const T* dwr = dw + r * C;
+  float s = 0.f;
+  for (int64_t c = threadIdx.x; c < C; c += 256) s += to_f(dwr[c]) * to_f(vr[c]);
+  const float dot = block_sum(s, red);
+  const float n = norms[r], gv = to_f(g[r]);
+  if (threadIdx.x == 0) dg[r] = from_f<G>(dot / n);
+  const float a = gv / n, b = gv * dot / (n * n * n);
+  T* dvr = dv + r * C;
+  for (int64_t c = threadIdx.x; c < C; c += 256) dvr[c] = from_f<T>(a * to_f(dwr[c]) - b * to_f(vr[c]));
+}
+
+template <typename T, typename G>
+__global__ void __launch_bounds__(256) wn_col_fwd(const T* __restrict__ v, const G* __restrict__ g,
+                                                 T* __restrict__ w, float* __restrict__ norms, int64_t R,
+                                                 int64_t C) {
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int64_t r = 0; r < R; ++r) {
+    const float x = to_f(v[r * C + c]);
+    s += x * x;
+  }
+  const float n = sqrtf(s);
+  norms[c] = n;
+  const float sc = to_f(g[c]) / n;
+  for (int64_t r = 0; r < R; ++r) w[r * C + c] = from_f<T>(to_f(v[r * C + c]) * sc);
+}
+
+template <typename T, typename G>
+__global__ void __launch_bounds__(256) wn_col_bwd(const T* __restrict__ dw, const T* __restrict__ v,
+                                                 const G* __restrict__ g, const float* __restrict__ norms,
+                                                 T* __restrict__ dv, G* __restrict__ dg, int64_t R,
+                                                 int64_t C) {
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int64_t r = 0; r < R; ++r) s += to_f(dw[r * C + c]) * to_f(v[r * C + c]);
+  const float n = norms[c], gv = to_f(g[c]);
+  dg[c] = from_f<G>(s / n);
+  const float a = gv / n, b = gv * s / (n * n * n);
+  for (int64_t r = 0; r < R; ++r) dv[r * C + c] = from_f<T>(a * to_f(dw[r * C + c]) - b * to_f(v[r * C + c]));
+}
+
+int weight_norm_fwd(const void* v, const void* g, void* w, float* norms, int64_t R, int64_t C, int row_mode,
+                    int vdt, int gdt, hipStream_t s) {
+  if (R == 0 || C == 0) return 0;
+  NM_DISPATCH(vdt, T, NM_DISPATCH(gdt, G, {
+    if (row_mode)
+      hipLaunchKernelGGL((wn_row_fwd<T, G>), dim3((unsigned)R), dim3(256), 0, s, (const T*)v, (const G*)g,
+                         (T*)w, norms, C);
+    else
+      hipLaunchKernelGGL((wn_col_fwd<T, G>), dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, (const T*)v,
+                         (const G*)g, (T*)w, norms, R, C);
+  }));
+  return (int)hipGetLastError();
+}
+
+int weight_norm_bwd(const void* dw, const void* v, const void* g, const float* norms, void* dv, void* dg,
+                    int64_t R, int64_t C, int row_mode, int vdt, int gdt, hipStream_t s) {
+  if (R == 0 || C == 0) return 0;
+  NM_DISPATCH(vdt, T, NM_DISPATCH(gdt, G, {
+    if (row_mode)
+      hipLaunchKernelGGL((wn_row_bwd<T, G>), dim3((unsigned)R), dim3(256), 0, s, (const T*)dw, (const T*)v,
+                         (const G*)g, norms, (T*)dv, (G*)dg, C);
+    else
+      hipLaunchKernelGGL((wn_col_bwd<T, G>), dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s,
+                         (const T*)dw, (const T*)v, (const G*)g, norms, (T*)dv, (G*)dg, R, C);
+  }));
+  return (int)hipGetLastError();
+}
+
+// ============================ RNN cells ======================================
+__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+
+// LSTM: gates [B, 4H] in PyTorch order (i, f, g, o). ws saves activated gates + tanh(cy).
+template <typename T>
+__global__ void __launch_bounds__(256) lstm_fwd_kernel(const T* __restrict__ ig, const T* __restrict__ hg,
+                                                      const T* __restrict__ bih, const T* __restrict__ bhh,
+                                                      const T* __restrict__ cx, T* __restrict__ hy,
+                                                      T* __restrict__ cy, float* __restrict__ ws, int64_t B,
+                                                      int64_t H) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= B * H) return;
+  const int64_t b = idx / H, j = idx % H;
+  float pre[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t o = b * 4 * H + k * H + j;
+    float v = to_f(ig[o]) + (hg ? to_f(hg[o]) : 0.f);
+    if (bih) v += to_f(bih[k * H + j]);
+    if (bhh) v += to_f(bhh[k * H + j]);
+    pre[k] = v;
+  }
+  const float i = sigm(pre[0]), f = sigm(pre[1]), g = tanhf(pre[2]), o = sigm(pre[3]);
+  const float c = f * to_f(cx[idx]) + i * g;
+  const float tc = tanhf(c);
+  cy[idx] = from_f<T>(c);
+  hy[idx] = from_f<T>(o * tc);
+  if (ws) {
+    float* w = ws + b * 5 * H;
+    w[j] = i;
+    w[H + j] = f;
+    w[2 * H + j] = g;
+    w[3 * H + j] = o;
+    w[4 * H + j] = tc;
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) lstm_bwd_kernel(const T* __restrict__ dhy, const T* __restrict__ dcy,
+                                                      const T* __restrict__ cx, const float* __restrict__ ws,
+                                                      T* __restrict__ dgates, T* __restrict__ dcx, int64_t B,
+                                                      int64_t H) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= B * H) return;
+  const int64_t b = idx / H, j = idx % H;
+  const float* w = ws + b * 5 * H;
+  const float i = w[j], f = w[H + j], g = w[2 * H + j], o = w[3 * H + j], tc = w[4 * H + j];
+  const float dh = dhy ? to_f(dhy[idx]) : 0.f;
+  const float dc = (dcy ? to_f(dcy[idx]) : 0.f) + dh * o * (1.f - tc * tc);
+  T* dg = dgates + b * 4 * H;
+  dg[j] = from_f<T>(dc * g * i * (1.f - i));
+  dg[H + j] = from_f<T>(dc * to_f(cx[idx]) * f * (1.f - f));
+  dg[2 * H + j] = from_f<T>(dc * i * (1.f - g * g));
+  dg[3 * H + j] = from_f<T>(dh * tc * o * (1.f - o));
+  dcx[idx] = from_f<T>(dc * f);
+}
+
+// GRU: gates [B, 3H] order (r, z, n). ws saves r, z, n, (hg_n + b_hn).
+template <typename T>
+__global__ void __launch_bounds__(256) gru_fwd_kernel(const T* __restrict__ ig, const T* __restrict__ hg,
+                                                     const T* __restrict__ bih, const T* __restrict__ bhh,
+                                                     const T* __restrict__ hx, T* __restrict__ hy,
+                                                     float* __restrict__ ws, int64_t B, int64_t H) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= B * H) return;
+  const int64_t b = idx / H, j = idx % H;
+  auto IG = [&](int k) { return to_f(ig[b * 3 * H + k * H + j]) + (bih ? to_f(bih[k * H + j]) : 0.f); };
+  auto HG = [&](int k) { return to_f(hg[b * 3 * H + k * H + j]) + (bhh ? to_f(bhh[k * H + j]) : 0.f); };
+  const float r = sigm(IG(0) + HG(0));
+  const float z = sigm(IG(1) + HG(1));
+  const float hn = HG(2);
+  const float n = tanhf(IG(2) + r * hn);
+  const float h = to_f(hx[idx]);
+  hy[idx] = from_f<T>((1.f - z) * n + z * h);
+  if (ws) {
+    float* w = ws + b * 4 * H;
+    w[j] = r;
+    w[H + j] = z;
+    w[2 * H + j] = n;
+    w[3 * H + j] = hn;
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) gru_bwd_kernel(const T* __restrict__ dhy, const T* __restrict__ hx,
+                                                     const float* __restrict__ ws, T* __restrict__ dig,
+                                                     T* __restrict__ dhg, T* __restrict__ dhx, int64_t B,
+                                                     int64_t H) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= B * H) return;
+  const int64_t b = idx / H, j = idx % H;
+  const float* w = ws + b * 4 * H;
+  const float r = w[j], z = w[H + j], n = w[2 * H + j], hn = w[3 * H + j];
+  const float dh = to_f(dhy[idx]), h = to_f(hx[idx]);
+  const float dn = dh * (1.f - z) * (1.f - n * n);
+  const float dz = dh * (h - n) * z * (1.f - z);
+  const float dr = dn * hn * r * (1.f - r);
+  T* di = dig + b * 3 * H;
+  T* dhh = dhg + b * 3 * H;
+  di[j] = from_f<T>(dr);
+  di[H + j] = from_f<T>(dz);
+  di[2 * H + j] = from_f<T>(dn);
+  dhh[j] = from_f<T>(dr);
+  dhh[H + j] = from_f<T>(dz);
+  dhh[2 * H + j] = from_f<T>(dn * r);
+  dhx[idx] = from_f<T>(dh * z);
+}
+
+int lstm_cell_fwd(const void* ig, const void* hg, const void* bih, const void* bhh, const void* cx, void* hy,
+                  void* cy, float* ws, int64_t B, int64_t H, int dt, hipStream_t s) {
+  const int64_t n = B * H;
+  if (n == 0) return 0;
+  NM_DISPATCH(dt, T,
+      hipLaunchKernelGGL((lstm_fwd_kernel<T>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                         (const T*)ig, (const T*)hg, (const T*)bih, (const T*)bhh, (const T*)cx, (T*)hy,
+                         (T*)cy, ws, B, H));
+  return (int)hipGetLastError();
+}
+
+int lstm_cell_bwd(const void* dhy, const void* dcy, const void* cx, const float* ws, void* dgates, void* dcx,
+                  int64_t B, int64_t H, int dt, hipStream_t s) {
+  const int64_t n = B * H;
+  if (n == 0) return 0;
+  NM_DISPATCH(dt, T,
+      hipLaunchKernelGGL((lstm_bwd_kernel<T>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                         (const T*)dhy, (const T*)dcy, (const T*)cx, ws, (T*)dgates, (T*)dcx, B, H));
+  return (int)hipGetLastError();
+}
+
+int gru_cell_fwd(const void* ig, const void* hg, const void* bih, const void* bhh, const void* hx, void* hy,
+                 float* ws, int64_t B, int64_t H, int dt, hipStream_t s) {
+  const int64_t n = B * H;
+  if (n == 0) return 0;
+  NM_DISPATCH(dt, T,
+      hipLaunchKernelGGL((gru_fwd_kernel<T>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                         (const T*)ig, (const T*)hg, (const T*)bih, (const T*)bhh, (const T*)hx, (T*)hy, ws,
+                         B, H));
+  return (int)hipGetLastError();
+}
+
+int gru_cell_bwd(const void* dhy, const void* hx, const float* ws, void* dig, void* dhg, void* dhx, int64_t B,
+                 int64_t H, int dt, hipStream_t s) {
+  const int64_t n = B * H;
+  if (n == 0) return 0;
+  NM_DISPATCH(dt, T,
+      hipLaunchKernelGGL((gru_bwd_kernel<T>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                         (const T*)dhy, (const T*)hx, ws, (T*)dig, (T*)dhg, (T*)dhx, B, H));
+  return (int)hipGetLastError();
+}
+
+// ============================ SyncBatchNorm ==================================
+// Layout: NCHW -> element (n, c, s) at n*C*S + c*S + s ; NHWC -> (n*S + s)*C + c.
+struct Welford {
+  float mean, m2, n;
+};
+__device__ __forceinline__ Welford wf_merge(Welford a, Welford b) {
+  const float n = a.n + b.n;
+  if (n == 0.f) return a;
+  const float d = b.mean - a.mean;
+  const float wb = b.n / n;
+  Welford r;
+  r.mean = a.mean + d * wb;
+  r.m2 = a.m2 + b.m2 + d * d * a.n * wb;
+  r.n = n;
+  return r;
+}
+
+// grid (C, splits): partial Welford of channel c over its slice of the N*S elements
+template <typename T>
+__global__ void __launch_bounds__(256) bn_stats_kernel(const T* __restrict__ x, float* __restrict__ part,
+                                                      int64_t N, int64_t C, int64_t S, int nhwc) {
+  __shared__ float sm[3][4];
+  const int64_t c = blockIdx.x;
+  const int64_t total = N * S;
+  const int64_t per = (total + gridDim.y - 1) / gridDim.y;
+  const int64_t e0 = (int64_t)blockIdx.y * per, e1 = min(e0 + per, total);
+  Welford w{0.f, 0.f, 0.f};
+  for (int64_t e = e0 + threadIdx.x; e < e1; e += 256) {
+    const int64_t n = e / S, s2 = e % S;
+    const float v = to_f(nhwc ? x[e * C + c] : x[(n * C + c) * S + s2]);
+    w.n += 1.f;
+    const float d = v - w.mean;
+    w.mean += d / w.n;
+    w.m2 += d * (v - w.mean);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    Welford b{__shfl_xor(w.mean, o, 64), __shfl_xor(w.m2, o, 64), __shfl_xor(w.n, o, 64)};
+    w = wf_merge(w, b);
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) {
+    sm[0][wid] = w.mean;
+    sm[1][wid] = w.m2;
+    sm[2][wid] = w.n;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    Welford t{sm[0][0], sm[1][0], sm[2][0]};
+    for (int k = 1; k < 4; ++k) t = wf_merge(t, Welford{sm[0][k], sm[1][k], sm[2][k]});
+    float* p = part + (c * gridDim.y + blockIdx.y) * 3;
+    p[0] = t.mean;
+    p[1] = t.m2;
+    p[2] = t.n;
+  }
+}
+
+// combine `groups` Welford triples per channel: in[(g*C + c)*3 ...] (g-major, e.g. all-gathered)
+// or in[(c*groups + g)*3] (c-major, local splits). Writes mean, biased var, count per channel.
+__global__ void bn_combine_kernel(const float* __restrict__ in, int groups, int64_t C, int gmajor,
+                                  float* __restrict__ mean, float* __restrict__ var, float* __restrict__ count) {
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  Welford t{0.f, 0.f, 0.f};
+  for (int g = 0; g < groups; ++g) {
+    const float* p = in + (gmajor ? ((int64_t)g * C + c) : (c * groups + g)) * 3;
+    t = wf_merge(t, Welford{p[0], p[1], p[2]});
+  }
+  mean[c] = t.mean;
+  var[c] = t.n > 0.f ? t.m2 / t.n : 0.f;
+  if (count) count[c] = t.n;
+}
+
+template <typename T, typename W>
+__global__ void __launch_bounds__(256) bn_elemt_kernel(const T* __restrict__ x, const float* __restrict__ mean,
+                                                      const float* __restrict__ invstd, const W* __restrict__ w,
+                                                      const W* __restrict__ b, T* __restrict__ y, int64_t N,
+                                                      int64_t C, int64_t S, int nhwc, int relu) {
+  const int64_t total = N * C * S;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int64_t c = nhwc ? e % C : (e / S) % C;
+    float v = (to_f(x[e]) - mean[c]) * invstd[c];
+    if (w) v *= to_f(w[c]);
+    if (b) v += to_f(b[c]);
+    if (relu) v = fmaxf(v, 0.f);
+    y[e] = from_f<T>(v);
+  }
+}
+
+// partial sums per channel: sum(dy), sum(dy * (x - mean)) ; grid (C, splits)
+template <typename T>
+__global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                           const float* __restrict__ mean,
+                                                           float* __restrict__ part, int64_t N, int64_t C,
+                                                           int64_t S, int nhwc) {
+  __shared__ float red[4];
+  const int64_t c = blockIdx.x;
+  const int64_t total = N * S;
+  const int64_t per = (total + gridDim.y - 1) / gridDim.y;
+  const int64_t e0 = (int64_t)blockIdx.y * per, e1 = min(e0 + per, total);
+  const float mu = mean[c];
+  float s1 = 0.f, s2 = 0.f;
+  for (int64_t e = e0 + threadIdx.x; e < e1; e += 256) {
+    const int64_t n = e / S, s3 = e % S;
+    const int64_t off = nhwc ? e * C + c : (n * C + c) * S + s3;
+    const float d = to_f(dy[off]);
+    s1 += d;
+    s2 += d * (to_f(x[off]) - mu);
+  }
+  s1 = block_sum(s1, red);
+  s2 = block_sum(s2, red);
+  if (threadIdx.x == 0) {
+    part[(c * gridDim.y + blockIdx.y) * 2] = s1;
+    part[(c * gridDim.y + blockIdx.y) * 2 + 1] = s2;
+  }
+}
+
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int splits, int64_t C,
+                                       float* __restrict__ sum_dy, float* __restrict__ sum_dy_xmu) {
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float a = 0.f, b = 0.f;
+  for (int k = 0; k < splits; ++k) {
+    a += part[(c * splits + k) * 2];
+    b += part[(c * splits + k) * 2 + 1];
+  }
+  sum_dy[c] = a;
+  sum_dy_xmu[c] = b;
+}
+
+// dx = (dy - mean_dy - (x-mean)*invstd^2*mean_dy_xmu) * invstd * w ; count = global element count
+template <typename T, typename W>
+__global__ void __launch_bounds__(256) bn_bwd_elemt_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                          const float* __restrict__ mean,
+                                                          const float* __restrict__ invstd,
+                                                          const W* __restrict__ w, const float* __restrict__ sum_dy,
+                                                          const float* __restrict__ sum_dy_xmu, float inv_count,
+                                                          T* __restrict__ dx, int64_t N, int64_t C, int64_t S,
+                                                          int nhwc) {
+  const int64_t total = N * C * S;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int64_t c = nhwc ? e % C : (e / S) % C;
+    const float is = invstd[c];
+    const float mdy = sum_dy[c] * inv_count, mdx = sum_dy_xmu[c] * inv_count;
+    const float xm = to_f(x[e]) - mean[c];
+    float v = (to_f(dy[e]) - mdy - xm * is * is * mdx) * is;
+    if (w) v *= to_f(w[c]);
+    dx[e] = from_f<T>(v);
+  }
+}
+
+static inline int bn_splits(int64_t N, int64_t S, int64_t C) {
+  // enough blocks to fill the chip: ~2048 blocks total, each >= 1024 elements
+  int64_t per_c = (N * S + 1023) / 1024;
+  int64_t want = (2048 + C - 1) / C;
+  int64_t sp = per_c < want ? per_c : want;
+  if (sp < 1) sp = 1;
+  if (sp > 256) sp = 256;
+  return (int)sp;
+}
+
+int bn_stats(const void* x, float* part, int64_t N, int64_t C, int64_t S, int nhwc, int dt, int* splits_out,
+             hipStream_t s) {
+  const int sp = bn_splits(N, S, C);
+  *splits_out = sp;
+  if (C == 0) return 0;
+  NM_DISPATCH(dt, T,
+      hipLaunchKernelGGL((bn_stats_kernel<T>), dim3((unsigned)C, sp), dim3(256), 0, s, (const T*)x, part, N, C,
+                         S, nhwc));
+  return (int)hipGetLastError();
+}
+
+int bn_splits_for(int64_t N, int64_t C, int64_t S) { return bn_splits(N, S, C); }
+
+int bn_combine(const float* in, int groups, int64_t C, int gmajor, float* mean, float* var, float* count,
+               hipStream_t s) {
+  if (C == 0) return 0;
+  hipLaunchKernelGGL(bn_combine_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, in, groups, C,
+                     gmajor, mean, var, count);
+  return (int)hipGetLastError();
+}
+
+int bn_elemt(const void* x, const float* mean, const float* invstd, const void* w, const void* b, void* y,
+             int64_t N, int64_t C, int64_t S, int nhwc, int relu, int dt, int wdt, hipStream_t s) {
+  const int64_t total = N * C * S;
+  if (total == 0) return 0;
+  const int64_t grid = min((total + 255) / 256, (int64_t)8192);
+  if (!w && !b) wdt = kF32;
+  NM_DISPATCH(dt, T, NM_DISPATCH(wdt, W,
+      hipLaunchKernelGGL((bn_elemt_kernel<T, W>), dim3((unsigned)grid), dim3(256), 0, s, (const T*)x, mean,
+                         invstd, (const W*)w, (const W*)b, (T*)y, N, C, S, nhwc, relu)));
+  return (int)hipGetLastError();
+}
+
+int bn_bwd_reduce(const void* dy, const void* x, const float* mean, float* part, float* sum_dy,
+                  float* sum_dy_xmu, int64_t N, int64_t C, int64_t S, int nhwc, int dt, hipStream_t s) {
+  if (C == 0) return 0;
+  const int sp = bn_splits(N, S, C);
+  NM_DISPATCH(dt, T,
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<T>), dim3((unsigned)C, sp), dim3(256), 0, s, (const T*)dy,
+                         (const T*)x, mean, part, N, C, S, nhwc));
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, part, sp, C,
+                     sum_dy, sum_dy_xmu);
+  return (int)hipGetLastError();
+}
+
+int bn_bwd_elemt(const void* dy, const void* x, const float* mean, const float* invstd, const void* w,
+                 const float* sum_dy, const float* sum_dy_xmu, float inv_count, void* dx, int64_t N, int64_t C,
+                 int64_t S, int nhwc, int dt, int wdt, hipStream_t s) {
+  const int64_t total = N * C * S;
+  if (total == 0) return 0;
+  const int64_t grid = min((total + 255) / 256, (int64_t)8192);
+  if (!w) wdt = kF32;
+  NM_DISPATCH(dt, T, NM_DISPATCH(wdt, W,
+      hipLaunchKernelGGL((bn_bwd_elemt_kernel<T, W>), dim3((unsigned)grid), dim3(256), 0, s, (const T*)dy,
+                         (const T*)x, mean, invstd, (const W*)w, sum_dy, sum_dy_xmu, inv_count, (T*)dx, N, C,
+                         S, nhwc)));
+  return (int)hipGetLastError();
+}
+
+}  // namespace apex

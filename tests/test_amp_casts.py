@@ -20,10 +20,11 @@ H, B, C, K, T = 32, 8, 8, 3, 6
 
 CASES = [("cpu", torch.bfloat16)]
 if torch.cuda.is_available():
-    CASES += [("cuda", torch.float16), ("cuda", torch.bfloat16)]
+    CASES += [pytest.param(("cuda", torch.float16), marks=pytest.mark.gpu, id="cuda-float16"),
+              pytest.param(("cuda", torch.bfloat16), marks=pytest.mark.gpu, id="cuda-bfloat16")]
 
 
-@pytest.fixture(params=CASES, ids=lambda c: f"{c[0]}-{str(c[1])[6:]}")
+@pytest.fixture(params=CASES, ids=lambda c: f"{c[0]}-{str(c[1])[6:]}" if isinstance(c, tuple) else None)
 def env(request):
     dev, low = request.param
     amp_utils.set_cast_devices({dev})
