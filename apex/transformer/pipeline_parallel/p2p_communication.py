@@ -1,0 +1,93 @@
+"""Point-to-point activation exchange between pipeline stages (NS-08).
+
+Each call batches its sends/receives into one ``batch_isend_irecv`` (RCCL group call), so
+a 1F1B steady-state step "send activation forward + receive gradient backward" is a single
+grouped launch on the direct xGMI link between the two stage peers. Shapes/dtypes are
+agreed up front (``tensor_shape``), so no metadata exchange is needed per message.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from .. import parallel_state as ps
+
+
+def _device():
+    if torch.cuda.is_available() and dist.get_backend() == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def _communicate(tensor_send_next, tensor_send_prev, recv_prev, recv_next, tensor_shape, dtype):
+    dev = _device()
+    t_prev = torch.empty(tensor_shape, dtype=dtype, device=dev, requires_grad=True) if recv_prev else None
+    t_next = torch.empty(tensor_shape, dtype=dtype, device=dev, requires_grad=True) if recv_next else None
+    ops = []
+    group = ps.get_pipeline_model_parallel_group()
+    if tensor_send_prev is not None:
+        ops.append(dist.P2POp(dist.isend, tensor_send_prev.contiguous(), ps.get_pipeline_model_parallel_prev_rank(),
+                              group))
+    if t_prev is not None:
+        ops.append(dist.P2POp(dist.irecv, t_prev, ps.get_pipeline_model_parallel_prev_rank(), group))
+    if tensor_send_next is not None:
+        ops.append(dist.P2POp(dist.isend, tensor_send_next.contiguous(), ps.get_pipeline_model_parallel_next_rank(),
+                              group))
+    if t_next is not None:
+        ops.append(dist.P2POp(dist.irecv, t_next, ps.get_pipeline_model_parallel_next_rank(), group))
+    if ops:
+        # wait() orders the compute stream after RCCL's stream (no host synchronisation)
+        for r in dist.batch_isend_irecv(ops):
+            r.wait()
+    if t_prev is not None:
+        t_prev = t_prev.detach().requires_grad_(True)
+    if t_next is not None:
+        t_next = t_next.detach()
+    return t_prev, t_next
+
+
+def recv_forward(tensor_shape, dtype=torch.float32):
+    if ps.is_pipeline_first_stage():
+        return None
+    return _communicate(None, None, True, False, tensor_shape, dtype)[0]
+
+
+def recv_backward(tensor_shape, dtype=torch.float32):
+    if ps.is_pipeline_last_stage():
+        return None
+    return _communicate(None, None, False, True, tensor_shape, dtype)[1]
+
+
+def send_forward(output_tensor, tensor_shape=None, dtype=torch.float32):
+    if not ps.is_pipeline_last_stage():
+        _communicate(output_tensor, None, False, False, tensor_shape, dtype)
+
+
+def send_backward(input_tensor_grad, tensor_shape=None, dtype=torch.float32):
+    if not ps.is_pipeline_first_stage():
+        _communicate(None, input_tensor_grad, False, False, tensor_shape, dtype)
+
+
+def send_forward_recv_backward(output_tensor, tensor_shape, dtype=torch.float32):
+    if ps.is_pipeline_last_stage():
+        return None
+    return _communicate(output_tensor, None, False, True, tensor_shape, dtype)[1]
+
+
+def send_backward_recv_forward(input_tensor_grad, tensor_shape, dtype=torch.float32):
+    if ps.is_pipeline_first_stage():
+        return None
+    return _communicate(None, input_tensor_grad, True, False, tensor_shape, dtype)[0]
+
+
+def send_forward_recv_forward(output_tensor, recv_prev, tensor_shape, dtype=torch.float32):
+    return _communicate(output_tensor, None, recv_prev, False, tensor_shape, dtype)[0]
+
+
+def send_backward_recv_backward(input_tensor_grad, recv_next, tensor_shape, dtype=torch.float32):
+    return _communicate(None, input_tensor_grad, False, recv_next, tensor_shape, dtype)[1]
+
+
+def send_forward_backward_recv_forward_backward(output_tensor, input_tensor_grad, recv_prev, recv_next,
+                                                tensor_shape, dtype=torch.float32):
+    return _communicate(output_tensor, input_tensor_grad, recv_prev, recv_next, tensor_shape, dtype)

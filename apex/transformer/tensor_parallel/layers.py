@@ -1,0 +1,184 @@
+"""Tensor-parallel layers (NS-08): ColumnParallelLinear, RowParallelLinear,
+VocabParallelEmbedding.
+
+Column-parallel splits the output features across the TP group (W row blocks), so the
+forward needs no communication and the backward one all-reduce of the input gradient;
+row-parallel splits the input features (W column blocks) and all-reduces the partial
+outputs in the forward. A column -> row pair (attention QKV -> out-proj, MLP fc1 -> fc2)
+therefore costs exactly one all-reduce forward and one backward per block — on MI355X
+that is one RCCL ring over the TP group's direct xGMI links per sublayer.
+With ``sequence_parallel_enabled`` the all-reduces become reduce-scatter / all-gather
+along the sequence dimension (activations stay sharded between blocks).
+GEMMs + bias use apex.ops.fused.fused_dense (bias grad via HIP colsum).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+from torch.nn.parameter import Parameter
+
+from ...ops import fused as fops
+from .. import parallel_state as ps
+from .mappings import (copy_to_tensor_model_parallel_region, gather_from_sequence_parallel_region,
+                       gather_from_tensor_model_parallel_region, reduce_from_tensor_model_parallel_region,
+                       reduce_scatter_to_sequence_parallel_region, scatter_to_tensor_model_parallel_region)
+from .random import get_cuda_rng_tracker
+from .utils import VocabUtility, divide
+
+_MODEL_PARALLEL_ATTRIBUTE_DEFAULTS = {"tensor_model_parallel": False, "partition_dim": -1, "partition_stride": 1}
+
+
+def param_is_not_tensor_parallel_duplicate(param):
+    return (hasattr(param, "tensor_model_parallel") and param.tensor_model_parallel) or \
+        ps.get_tensor_model_parallel_rank() == 0
+
+
+def set_tensor_model_parallel_attributes(tensor, is_parallel, dim, stride):
+    setattr(tensor, "tensor_model_parallel", is_parallel)
+    setattr(tensor, "partition_dim", dim)
+    setattr(tensor, "partition_stride", stride)
+
+
+def set_defaults_if_not_set_tensor_model_parallel_attributes(tensor):
+    for k, v in _MODEL_PARALLEL_ATTRIBUTE_DEFAULTS.items():
+        if not hasattr(tensor, k):
+            setattr(tensor, k, v)
+
+
+def copy_tensor_model_parallel_attributes(destination, source):
+    for k in _MODEL_PARALLEL_ATTRIBUTE_DEFAULTS:
+        if hasattr(source, k):
+            setattr(destination, k, getattr(source, k))
+
+
+def _initialize_affine_weight(weight, output_size, input_size, per_partition_size, partition_dim,
+                              init_method, stride=1, return_master_weight=False, params_dtype=torch.float32):
+    """Initialise the FULL weight identically on every rank (seeded), keep this rank's slice:
+    results are independent of the TP degree (so TP runs match single-GPU runs)."""
+    set_tensor_model_parallel_attributes(weight, True, partition_dim, stride)
+    master = torch.empty(output_size, input_size, dtype=torch.float32, requires_grad=False)
+    init_method(master)
+    master = master.to(params_dtype)
+    per_stride = divide(per_partition_size, stride)
+    chunks = torch.split(master, per_stride, dim=partition_dim)
+    rank = ps.get_tensor_model_parallel_rank()
+    ws = ps.get_tensor_model_parallel_world_size()
+    mine = chunks[rank::ws]
+    with torch.no_grad():
+        weight.copy_(torch.cat(mine, dim=partition_dim))
+    return master if return_master_weight else None
+
+
+class VocabParallelEmbedding(nn.Module):
+    """Embedding with the vocabulary split across the TP group; out-of-range ids produce 0
+    locally and the all-reduce assembles the full lookup."""
+
+    def __init__(self, num_embeddings, embedding_dim, init_method=nn.init.xavier_normal_, *,
+                 params_dtype=torch.float32, use_cpu_initialization=False, device=None):
+        super().__init__()
+        self.num_embeddings = num_embeddings
+        self.embedding_dim = embedding_dim
+        self.tensor_model_parallel_size = ps.get_tensor_model_parallel_world_size()
+        self.vocab_start_index, self.vocab_end_index = VocabUtility.vocab_range_from_global_vocab_size(
+            num_embeddings, ps.get_tensor_model_parallel_rank(), self.tensor_model_parallel_size)
+        self.num_embeddings_per_partition = self.vocab_end_index - self.vocab_start_index
+        self.weight = Parameter(torch.empty(self.num_embeddings_per_partition, embedding_dim,
+                                            dtype=params_dtype, device=device))
+        _initialize_affine_weight(self.weight, num_embeddings, embedding_dim, self.num_embeddings_per_partition,
+                                  0, init_method, params_dtype=params_dtype)
+
+    def forward(self, input_):
+        if self.tensor_model_parallel_size > 1:
+            mask = (input_ < self.vocab_start_index) | (input_ >= self.vocab_end_index)
+            local = input_.clone() - self.vocab_start_index
+            local[mask] = 0
+        else:
+            local = input_
+        out = F.embedding(local, self.weight)
+        if self.tensor_model_parallel_size > 1:
+            out = out.masked_fill(mask.unsqueeze(-1), 0.0)
+        return reduce_from_tensor_model_parallel_region(out)
+
+
+class ColumnParallelLinear(nn.Module):
+    """Y = X A + b with A split by columns: A = [A_1 ... A_p]; rank i computes X A_i."""
+
+    def __init__(self, input_size, output_size, bias=True, gather_output=True, init_method=nn.init.xavier_normal_,
+                 stride=1, keep_master_weight_for_test=False, skip_bias_add=False, *,
+                 no_async_tensor_model_parallel_allreduce=True, params_dtype=torch.float32,
+                 use_cpu_initialization=False, gradient_accumulation_fusion=False,
+                 accumulation_in_fp16=False, sequence_parallel_enabled=False, device=None):
+        super().__init__()
+        self.input_size = input_size
+        self.output_size = output_size
+        self.gather_output = gather_output
+        ws = ps.get_tensor_model_parallel_world_size()
+        self.output_size_per_partition = divide(output_size, ws)
+        self.skip_bias_add = skip_bias_add
+        self.sequence_parallel_enabled = sequence_parallel_enabled
+        self.weight = Parameter(torch.empty(self.output_size_per_partition, input_size, dtype=params_dtype,
+                                            device=device))
+        self.master_weight = _initialize_affine_weight(self.weight, output_size, input_size,
+                                                       self.output_size_per_partition, 0, init_method, stride,
+                                                       keep_master_weight_for_test, params_dtype)
+        if bias:
+            self.bias = Parameter(torch.zeros(self.output_size_per_partition, dtype=params_dtype, device=device))
+            set_tensor_model_parallel_attributes(self.bias, True, 0, stride)
+        else:
+            self.register_parameter("bias", None)
+
+    def forward(self, input_):
+        if self.sequence_parallel_enabled:
+            x = gather_from_sequence_parallel_region(input_, True)
+        else:
+            x = copy_to_tensor_model_parallel_region(input_)
+        bias = self.bias if not self.skip_bias_add else None
+        out = fops.fused_dense(x, self.weight, bias)
+        if self.gather_output:
+            assert not self.sequence_parallel_enabled
+            out = gather_from_tensor_model_parallel_region(out)
+        return out, (self.bias if self.skip_bias_add else None)
+
+
+class RowParallelLinear(nn.Module):
+    """Y = X A + b with A split by rows (X split by columns); partial outputs all-reduced."""
+
+    def __init__(self, input_size, output_size, bias=True, input_is_parallel=False,
+                 init_method=nn.init.xavier_normal_, stride=1, keep_master_weight_for_test=False,
+                 skip_bias_add=False, *, params_dtype=torch.float32, use_cpu_initialization=False,
+                 gradient_accumulation_fusion=False, accumulation_in_fp16=False,
+                 sequence_parallel_enabled=False, device=None):
+        super().__init__()
+        self.input_size = input_size
+        self.output_size = output_size
+        self.input_is_parallel = input_is_parallel
+        ws = ps.get_tensor_model_parallel_world_size()
+        self.input_size_per_partition = divide(input_size, ws)
+        self.skip_bias_add = skip_bias_add
+        self.sequence_parallel_enabled = sequence_parallel_enabled
+        if sequence_parallel_enabled and not input_is_parallel:
+            raise RuntimeError("To enable `sequence_parallel_enabled`, `input_is_parallel` must be `True`")
+        self.weight = Parameter(torch.empty(output_size, self.input_size_per_partition, dtype=params_dtype,
+                                            device=device))
+        self.master_weight = _initialize_affine_weight(self.weight, output_size, input_size,
+                                                       self.input_size_per_partition, 1, init_method, stride,
+                                                       keep_master_weight_for_test, params_dtype)
+        if bias:
+            self.bias = Parameter(torch.zeros(output_size, dtype=params_dtype, device=device))
+            setattr(self.bias, "sequence_parallel_enabled", sequence_parallel_enabled)
+        else:
+            self.register_parameter("bias", None)
+
+    def forward(self, input_):
+        x = input_ if self.input_is_parallel else scatter_to_tensor_model_parallel_region(input_)
+        partial = fops.fused_dense(x, self.weight, None)
+        if self.sequence_parallel_enabled:
+            out = reduce_scatter_to_sequence_parallel_region(partial)
+        else:
+            out = reduce_from_tensor_model_parallel_region(partial)
+        if self.skip_bias_add:
+            return out, self.bias
+        return (out + self.bias if self.bias is not None else out), None

@@ -654,6 +654,41 @@ Tensor k_bn_bwd_elemt(Tensor dy, Tensor x, Tensor mean, Tensor invstd, const c10
   return dx;
 }
 
+// --------------------------------------------------------------------------
+// fused scale-mask softmax: x [..., sq, sk] (batch*heads flattened), mask uint8 [B, 1|H, sq, sk]
+// --------------------------------------------------------------------------
+bool k_smx_supported(int64_t cols) { return apex::scaled_softmax_supported((int)cols) != 0; }
+
+Tensor k_smx_fwd(Tensor x, const c10::optional<Tensor>& mask, double scale, int64_t mode, int64_t heads) {
+  TORCH_CHECK(x.is_contiguous() && x.dim() >= 2, "scaled_masked_softmax: contiguous input");
+  const int64_t cols = x.size(-1), sq = x.size(-2);
+  const int64_t rows = x.numel() / cols;
+  Tensor y = at::empty_like(x);
+  const uint8_t* mp = nullptr;
+  int mask_heads = 1;
+  if (mode == 1) {
+    TORCH_CHECK(mask.has_value() && mask->defined() && mask->is_contiguous(), "mask required");
+    TORCH_CHECK(mask->size(-1) == cols && mask->size(-2) == sq, "mask shape mismatch");
+    mp = (const uint8_t*)mask->data_ptr();
+    mask_heads = (int)mask->size(1);
+  }
+  check(apex::scaled_masked_softmax_fwd(x.data_ptr(), mp, y.data_ptr(), rows, (int)cols, (int)sq, (int)heads,
+                                        mask_heads, (float)scale, (int)mode, dt_code(x.scalar_type()),
+                                        cur_stream()),
+        "scaled_masked_softmax_fwd");
+  return y;
+}
+
+Tensor k_smx_bwd(Tensor dy, Tensor y, double scale) {
+  Tensor dyc = dy.contiguous();
+  const int64_t cols = y.size(-1), rows = y.numel() / cols;
+  Tensor dx = at::empty_like(y);
+  check(apex::scaled_masked_softmax_bwd(dyc.data_ptr(), y.data_ptr(), dx.data_ptr(), rows, (int)cols,
+                                        (float)scale, dt_code(y.scalar_type()), cur_stream()),
+        "scaled_masked_softmax_bwd");
+  return dx;
+}
+
 Tensor flash_dropout_mask(int64_t B, int64_t H, int64_t Sq, int64_t Sk, double p_drop, int64_t seed,
                           int64_t offset, at::Device dev) {
   Tensor out = at::empty({B, H, Sq, Sk}, at::TensorOptions().dtype(at::kByte).device(dev));
@@ -703,6 +738,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_elemt", &k_bn_elemt);
   m.def("bn_bwd_reduce", &k_bn_bwd_reduce);
   m.def("bn_bwd_elemt", &k_bn_bwd_elemt);
+  m.def("scaled_softmax_supported", &k_smx_supported);
+  m.def("scaled_masked_softmax_fwd", &k_smx_fwd);
+  m.def("scaled_masked_softmax_bwd", &k_smx_bwd);
   m.def("bias_act_fwd", &k_bias_act_fwd);
   m.def("bias_act_bwd", &k_bias_act_bwd);
   m.def("bias_dropout_add_fwd", &k_bda_fwd);

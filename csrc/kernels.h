@@ -150,6 +150,14 @@ int bn_bwd_elemt(const void* dy, const void* x, const float* mean, const float* 
                  const float* sum_dy, const float* sum_dy_xmu, float inv_count, void* dx, int64_t N, int64_t C,
                  int64_t S, int nhwc, int dt, int wdt, hipStream_t s);
 
+// ----------------------------- fused scale-mask softmax --------------------
+// mode 0: scale only, 1: byte mask [B, mask_heads, sq, cols] (nonzero masked), 2: causal
+int scaled_softmax_supported(int cols);
+int scaled_masked_softmax_fwd(const void* x, const uint8_t* mask, void* y, int64_t rows, int cols, int sq,
+                              int heads, int mask_heads, float scale, int mode, int dt, hipStream_t s);
+int scaled_masked_softmax_bwd(const void* dy, const void* y, void* dx, int64_t rows, int cols, float scale, int dt,
+                              hipStream_t s);
+
 // ----------------------------- softmax cross-entropy -----------------------
 int xentropy_fwd(const void* logits, const int64_t* labels, float* losses, float* lse, int64_t rows,
                  int V, float smoothing, int64_t ignore_index, int dt, hipStream_t s);
