@@ -151,6 +151,15 @@ class SyncBatchNorm(_BatchNorm):
         self._check_input_dim(input)
         if z is not None:
             input = input + z
+        if (not self.channel_last and input.dim() == 4 and input.shape[1] > 1
+                and input.is_contiguous(memory_format=torch.channels_last) and not input.is_contiguous()):
+            # torch channels_last (NCHW shape, NHWC storage): run the NHWC kernels on the
+            # zero-copy [N, H, W, C] view instead of transposing to NCHW and back
+            self.channel_last = True
+            try:
+                return self.forward(input.permute(0, 2, 3, 1)).permute(0, 3, 1, 2)
+            finally:
+                self.channel_last = False
         if self.training and self.track_running_stats:
             self.num_batches_tracked += 1
         use_batch_stats = self.training or not self.track_running_stats

@@ -1,0 +1,112 @@
+"""Shared benchmark harness (NS-09): one process per GPU, torch.distributed over RCCL,
+W untimed warmup steps, K timed steps bracketed by barrier + device synchronize on both
+sides, MAX elapsed over ranks, one JSON line from rank 0.
+
+The headline ``bench.py`` and every ``benchmarks/*.py`` workload script use the same
+timing contract, so numbers across configs are comparable.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+@dataclass
+class DistEnv:
+    rank: int
+    world: int
+    local_rank: int
+    device: torch.device
+
+    @property
+    def is_main(self):
+        return self.rank == 0
+
+
+def init_distributed(backend=None, device="cuda"):
+    """Read RANK/WORLD_SIZE/LOCAL_RANK (torchrun), bind the GPU, init the process group."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if device == "cuda":
+        torch.cuda.set_device(local_rank)
+        dev = torch.device("cuda", local_rank)
+    else:
+        dev = torch.device("cpu")
+    if world > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if dev.type == "cuda" else "gloo"
+        kw = {"device_id": dev} if dev.type == "cuda" else {}
+        dist.init_process_group(backend, **kw)
+    return DistEnv(rank, world, local_rank, dev)
+
+
+def _sync(env):
+    if env.device.type == "cuda":
+        torch.cuda.synchronize()
+
+
+def time_steps(env: DistEnv, step, steps: int, warmup: int):
+    """Run ``step(i)`` warmup + steps times; return (max-over-ranks seconds, last result)."""
+    out = None
+    for i in range(warmup):
+        out = step(i)
+    _sync(env)
+    if env.world > 1:
+        dist.barrier()
+    _sync(env)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        out = step(i)
+    _sync(env)
+    if env.world > 1:
+        dist.barrier()
+    _sync(env)
+    elapsed = time.perf_counter() - t0
+    if env.world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device=env.device if env.device.type == "cuda" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, out
+
+
+def emit(env: DistEnv, *, metric, items_per_step, unit, steps, warmup, elapsed, dtype, data, config,
+         baseline=None, scaling="weak", extra=None):
+    """Rank 0 prints the one-line JSON result; ``items_per_step`` is the whole-job count."""
+    rate = items_per_step * steps / elapsed
+    out = {
+        "metric": metric,
+        "value": round(rate, 3),
+        "unit": unit,
+        "n_gpus": env.world,
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": round(elapsed / steps * 1000.0, 3),
+        "higher_is_better": True,
+        "scaling": scaling,
+        "vs_baseline": None if baseline is None else round(rate / baseline, 4),
+        "dtype": dtype,
+        "data": data,
+        "config": config,
+    }
+    if extra:
+        out.update(extra)
+    if env.is_main:
+        print(json.dumps(out), flush=True)
+    return out
+
+
+def finish(env: DistEnv):
+    if env.world > 1 and dist.is_initialized():
+        dist.destroy_process_group()

@@ -1,0 +1,81 @@
+#!/usr/bin/env python3
+"""BASELINE.json config 2: ResNet-50, amp O2 bf16 + FusedSGD + SyncBatchNorm (+ apex DDP when
+N>1), img/s. Synthetic normalised images (NHWC/channels_last, MIOpen's fast bf16 layout) and
+random-init weights. Throughput = world x batch / step time (the reference's definition,
+examples/imagenet/main.py:348,354).
+
+  python benchmarks/resnet50.py [--batch 256] [--steps 20] [--warmup 5] [--no-syncbn] [--fp32]
+  torchrun --nproc-per-node N benchmarks/resnet50.py ...
+"""
+import argparse
+import os
+import sys
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--image-size", type=int, default=224)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--no-syncbn", action="store_true")
+    ap.add_argument("--nchw", action="store_true", help="keep NCHW activations")
+    ap.add_argument("--fp32", action="store_true")
+    args = ap.parse_args()
+
+    from apex.utils.bench import emit, finish, init_distributed, time_steps
+
+    env = init_distributed()
+    import apex
+    from apex import amp
+    from apex.models.resnet import resnet50, synthetic_batch
+    from apex.optimizers import FusedSGD
+    from apex.parallel import DistributedDataParallel as DDP
+    from apex.parallel import convert_syncbn_model
+
+    apex._ext.require()
+    torch.manual_seed(0)
+    model = resnet50()
+    if not args.no_syncbn:
+        model = convert_syncbn_model(model)  # channels_last inputs take the NHWC kernels
+    cl = not args.nchw
+    model = model.to(env.device, memory_format=torch.channels_last if cl else torch.contiguous_format)
+    opt = FusedSGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    if args.fp32:
+        model, opt = amp.initialize(model, opt, opt_level="O0", verbosity=0)
+    else:
+        model, opt = amp.initialize(model, opt, opt_level="O2", cast_model_type=torch.bfloat16, verbosity=0)
+    if env.world > 1:
+        model = DDP(model, message_size=int(os.environ.get("APEX_DDP_MESSAGE_SIZE", 25_000_000)))
+    g = torch.Generator(device=env.device).manual_seed(1 + env.rank)
+    dt = torch.float32 if args.fp32 else torch.bfloat16
+    batches = [synthetic_batch(args.batch, args.image_size, device=env.device, dtype=dt, channels_last=cl,
+                               generator=g) for _ in range(2)]
+
+    def step(i):
+        x, y = batches[i % 2]
+        loss = F.cross_entropy(model(x).float(), y)
+        with amp.scale_loss(loss, opt) as sl:
+            sl.backward()
+        opt.step()
+        opt.zero_grad()
+        return loss
+
+    elapsed, loss = time_steps(env, step, args.steps, args.warmup)
+    emit(env, metric="img/s ResNet-50 amp-O2 bf16 + FusedSGD + SyncBatchNorm", items_per_step=args.batch * env.world,
+         unit="img/s", steps=args.steps, warmup=args.warmup, elapsed=elapsed,
+         dtype="fp32" if args.fp32 else "bf16", data="synthetic normalised images; random-init weights",
+         config={"model": "ResNet-50", "global_batch": args.batch * env.world, "image_size": args.image_size,
+                 "parallelism": f"dp{env.world}", "syncbn": not args.no_syncbn,
+                 "memory_format": "channels_last" if cl else "nchw"},
+         extra={"final_loss": round(float(loss), 4)})
+    finish(env)
+
+
+if __name__ == "__main__":
+    main()

@@ -700,6 +700,36 @@ Tensor flash_dropout_mask(int64_t B, int64_t H, int64_t Sq, int64_t Sk, double p
   return out;
 }
 
+// --------------------------------------------------------------------------
+// K-09 input normalisation: x uint8 [B,H,W,C] (nhwc_in) or [B,C,H,W]; returns the normalised
+// tensor in `out_dtype`, NCHW-contiguous (channels_last=false) or channels_last.
+// --------------------------------------------------------------------------
+Tensor k_input_normalize(Tensor x, std::vector<double> mean, std::vector<double> stdv, bool nhwc_in,
+                         bool channels_last, at::ScalarType out_dtype) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kByte && x.dim() == 4, "input_normalize: uint8 4-D cuda");
+  Tensor xc = x.contiguous();
+  const int64_t B = xc.size(0);
+  const int64_t C = nhwc_in ? xc.size(3) : xc.size(1);
+  const int64_t H = nhwc_in ? xc.size(1) : xc.size(2), W = nhwc_in ? xc.size(2) : xc.size(3);
+  TORCH_CHECK((int64_t)mean.size() == C && (int64_t)stdv.size() == C, "mean/std need one value per channel");
+  TORCH_CHECK(!(channels_last && !nhwc_in), "NCHW uint8 input -> channels_last output is not supported");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(xc.data_ptr()) % 16 == 0, "input must be 16-byte aligned");
+  auto opts = xc.options().dtype(out_dtype);
+  Tensor y = channels_last ? at::empty({B, C, H, W}, opts.memory_format(at::MemoryFormat::ChannelsLast))
+                           : at::empty({B, C, H, W}, opts);
+  float m[4], sd[4];
+  for (int64_t c = 0; c < C && c < 4; ++c) {
+    m[c] = (float)mean[c];
+    sd[c] = (float)stdv[c];
+  }
+  const int layout = nhwc_in ? (channels_last ? 0 : 1) : 2;
+  const int rc = apex::input_normalize((const uint8_t*)xc.data_ptr(), y.data_ptr(), B, C, H * W, layout, m, sd,
+                                       dt_code(out_dtype), cur_stream());
+  TORCH_CHECK(rc != 1, "input_normalize: unsupported geometry (C<=4; NHWC->NCHW needs H*W % 8 == 0)");
+  check(rc, "input_normalize");
+  return y;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -749,4 +779,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bdaln_supported", &k_bdaln_supported);
   m.def("bdaln_fwd", &k_bdaln_fwd);
   m.def("bdaln_bwd", &k_bdaln_bwd);
+  m.def("input_normalize", &k_input_normalize);
 }

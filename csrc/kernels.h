@@ -165,4 +165,10 @@ int xentropy_bwd(const void* dloss, int64_t dloss_stride, int dloss_dt, const vo
                  const float* lse, const int64_t* labels, void* dlogits, int64_t rows, int V,
                  float smoothing, int64_t ignore_index, int dt, hipStream_t s);
 
+// ----------------------------- input pipeline (K-09) -----------------------
+// layout: 0 NHWC->NHWC, 1 NHWC->NCHW (hw % 8 == 0, C in {1,3,4}), 2 NCHW->NCHW. Returns 1 if
+// the geometry is unsupported.
+int input_normalize(const uint8_t* x, void* y, int64_t B, int64_t C, int64_t hw, int layout, const float* mean,
+                    const float* stdv, int ydt, hipStream_t s);
+
 }  // namespace apex
