@@ -82,14 +82,16 @@ class FP16_Optimizer:
                 if set_grads_to_None:
                     p.grad = None
                 elif p.grad is not None:
-                    p.grad.detach_()
+                    if p.grad._base is None:
+                        p.grad.detach_()
                     p.grad.zero_()
         for fp16_group in self.fp16_groups:
             for param in fp16_group:
                 if set_grads_to_None:
                     param.grad = None
                 elif param.grad is not None:
-                    param.grad.detach_()
+                    if param.grad._base is None:  # DDP bucket views cannot detach_ in place
+                        param.grad.detach_()
                     param.grad.zero_()
 
     def _check_overflow(self):
@@ -129,17 +131,24 @@ class FP16_Optimizer:
         return -1
 
     def state_dict(self):
+        """Plain containers + tensors only (the reference pickled the scaler object), so a
+        checkpoint loads with ``torch.load(..., weights_only=True)``."""
         sd = {}
-        sd["loss_scaler"] = self.loss_scaler
+        sd["loss_scaler"] = self.loss_scaler.state_dict()
         sd["dynamic_loss_scale"] = self.dynamic_loss_scale
         sd["overflow"] = self.overflow
         sd["first_closure_call_this_step"] = self.first_closure_call_this_step
         sd["optimizer_state_dict"] = self.optimizer.state_dict()
-        sd["fp32_from_fp16"] = self.fp32_from_fp16_groups
+        sd["fp32_from_fp16"] = [[m.detach() for m in g] for g in self.fp32_from_fp16_groups]
         return sd
 
     def load_state_dict(self, state_dict):
-        self.loss_scaler = state_dict["loss_scaler"]
+        scaler = state_dict["loss_scaler"]
+        if isinstance(scaler, dict):
+            self.loss_scaler = DynamicLossScaler() if state_dict["dynamic_loss_scale"] else LossScaler()
+            self.loss_scaler.load_state_dict(scaler)
+        else:  # a scaler object (in-process round trip)
+            self.loss_scaler = scaler
         self.dynamic_loss_scale = state_dict["dynamic_loss_scale"]
         self.overflow = state_dict["overflow"]
         self.first_closure_call_this_step = state_dict["first_closure_call_this_step"]

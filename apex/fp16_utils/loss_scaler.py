@@ -66,6 +66,12 @@ class LossScaler:
         scaled_loss = loss * self.loss_scale
         scaled_loss.backward()
 
+    def state_dict(self):
+        return dict(cur_scale=self.cur_scale)
+
+    def load_state_dict(self, sd):
+        self.cur_scale = sd["cur_scale"]
+
 
 class DynamicLossScaler:
     """Dynamic loss scale: back off on overflow, grow every ``scale_window`` clean iters."""

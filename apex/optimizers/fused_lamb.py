@@ -36,8 +36,8 @@ class FusedLAMB(FusedOptimizerBase):
     def _state_for(self, p):
         st = self.state[p]
         if len(st) == 0:
-            st["exp_avg"] = torch.zeros_like(p, dtype=torch.float32, memory_format=torch.contiguous_format)
-            st["exp_avg_sq"] = torch.zeros_like(p, dtype=torch.float32, memory_format=torch.contiguous_format)
+            st["exp_avg"] = torch.zeros_like(p, dtype=torch.float32)
+            st["exp_avg_sq"] = torch.zeros_like(p, dtype=torch.float32)
         return st
 
     def _group_step(self, gi, group, device):

@@ -386,7 +386,10 @@ class DistributedDataParallel(Module):
             for i in idxs:
                 p = self._params[i]
                 n = p.numel()
-                v = flat[off:off + n].view_as(p)
+                if p.is_contiguous() or not p.is_non_overlapping_and_dense():
+                    v = flat[off:off + n].view_as(p)
+                else:  # e.g. channels_last conv weight: the grad view keeps the param's strides
+                    v = flat[off:off + n].as_strided(p.shape, p.stride())
                 if p.grad is not None:
                     v.copy_(p.grad)
                 p.grad = v

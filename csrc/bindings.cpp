@@ -58,7 +58,11 @@ struct MTPlan {
       for (int t = 0; t < ntensors; ++t) {
         const Tensor& x = lists[l][t];
         TORCH_CHECK(x.is_cuda(), "multi-tensor op requires device tensors");
-        TORCH_CHECK(x.is_contiguous(), "multi-tensor op requires contiguous tensors");
+        // elementwise ops only need dense storage walked in the same order in every list
+        // (e.g. channels_last conv weights, their grads and optimizer state)
+        TORCH_CHECK((x.is_contiguous() && lists[0][t].is_contiguous()) ||
+                        (x.is_non_overlapping_and_dense() && x.strides() == lists[0][t].strides()),
+                    "multi-tensor op requires dense tensors with matching strides across lists");
         TORCH_CHECK(dt_code(x.scalar_type()) == dtypes[l], "list ", l, " mixes dtypes");
         TORCH_CHECK(x.numel() == lists[0][t].numel(), "tensor size mismatch across lists");
         dev = x.device();
