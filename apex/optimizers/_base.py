@@ -68,6 +68,18 @@ class FusedOptimizerBase(Optimizer):
                         p.grad.requires_grad_(False)
                     p.grad.zero_()
 
+    @staticmethod
+    def _split_by_dtype(lists):
+        """Partition parallel tensor lists so every partition has ONE dtype per list (a plan's
+        requirement). Groups mixing dtypes — e.g. amp O2 with fp32 BatchNorm next to bf16
+        convs — become one launch per dtype combination. Returns [(dtype_key, lists)]."""
+        parts = {}
+        for i in range(len(lists[0])):
+            parts.setdefault(tuple(l[i].dtype for l in lists), []).append(i)
+        if len(parts) == 1:
+            return [(next(iter(parts)), lists)]
+        return [(k, [[l[i] for i in idx] for l in lists]) for k, idx in parts.items()]
+
     def _native(self, tensors):
         return len(tensors) > 0 and _ext.use_native(tensors[0])
 

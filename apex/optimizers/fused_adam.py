@@ -51,10 +51,11 @@ class FusedAdam(FusedOptimizerBase):
             if self._native(gs):
                 bc1 = 1 - b1 ** group["step"] if group["bias_correction"] else 1.0
                 bc2 = 1 - b2 ** group["step"] if group["bias_correction"] else 1.0
-                self._plan(("adam", gi), lists).adam(
-                    float(group["lr"]), float(b1), float(b2), float(group["eps"]),
-                    float(group["weight_decay"]), bc1, bc2, self.adam_w_mode == 1,
-                    scale_f, scale_t, self._amp_noop)
+                for key, sub in self._split_by_dtype(lists):
+                    self._plan(("adam", gi, key), sub).adam(
+                        float(group["lr"]), float(b1), float(b2), float(group["eps"]),
+                        float(group["weight_decay"]), bc1, bc2, self.adam_w_mode == 1,
+                        scale_f, scale_t, self._amp_noop)
             else:
                 mt_ops.multi_tensor_adam(0, self._amp_noop, lists, group["lr"], b1, b2,
                                          group["eps"], group["step"], self.adam_w_mode,

@@ -87,13 +87,16 @@ class FusedLAMB(FusedOptimizerBase):
             lists = [gs, ps, [s["exp_avg"] for s in states], [s["exp_avg_sq"] for s in states], ubuf]
             if models is not None:
                 lists.append(models)
-            step_t = self._group_step(gi, group, dev)
-            self._plan(("lamb", gi), lists).lamb(
-                float(group["lr"]), float(b1), float(b2), float(group["eps"]),
-                float(group["weight_decay"]), float(group["max_grad_norm"]),
-                self.adam_w_mode == 1, bool(group["bias_correction"]),
-                bool(group["grad_averaging"]), bool(self.use_nvlamb), scale_f, scale_t, noop, None,
-                step_t, gnorm)
+            for key, sub in self._split_by_dtype(lists):
+                # the prep kernel advances its step counter once per launch: one counter per
+                # dtype partition keeps every partition at the group's true step
+                step_t = self._group_step((gi, key) if len(sub[0]) != len(gs) else gi, group, dev)
+                self._plan(("lamb", gi, key), sub).lamb(
+                    float(group["lr"]), float(b1), float(b2), float(group["eps"]),
+                    float(group["weight_decay"]), float(group["max_grad_norm"]),
+                    self.adam_w_mode == 1, bool(group["bias_correction"]),
+                    bool(group["grad_averaging"]), bool(self.use_nvlamb), scale_f, scale_t, noop, None,
+                    step_t, gnorm)
 
     def _step_reference(self, per_group, all_grads):
         scale = float(self._amp_grad_scale.item()) if self._amp_grad_scale is not None else 1.0

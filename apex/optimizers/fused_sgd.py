@@ -48,10 +48,11 @@ class FusedSGD(FusedOptimizerBase):
                 moms.append(st["momentum_buffer"])
             lists = [gs, ps, moms] + ([models] if models is not None else [])
             if self._native(gs):
-                self._plan(("sgd", gi), lists).sgd(
-                    float(group["lr"]), float(group["momentum"]), float(group["dampening"]),
-                    float(group["weight_decay"]), bool(group["nesterov"]), first_run,
-                    self.wd_after_momentum, scale_f, scale_t, self._amp_noop)
+                for key, sub in self._split_by_dtype(lists):
+                    self._plan(("sgd", gi, key), sub).sgd(
+                        float(group["lr"]), float(group["momentum"]), float(group["dampening"]),
+                        float(group["weight_decay"]), bool(group["nesterov"]), first_run,
+                        self.wd_after_momentum, scale_f, scale_t, self._amp_noop)
             else:
                 mt_ops.multi_tensor_sgd(0, self._amp_noop, lists, group["weight_decay"],
                                         group["momentum"], group["dampening"], group["lr"],

@@ -21,6 +21,24 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+_RESULT_STREAM = None
+
+
+def protect_stdout():
+    """Reserve the process's stdout for the one JSON result line.
+
+    Native libraries print banners to fd 1 (RCCL prints its version block on communicator
+    init), which would break the one-line contract; fd 1 is pointed at stderr for the rest of
+    the process and the original stdout is kept for :func:`emit`. Idempotent."""
+    global _RESULT_STREAM
+    if _RESULT_STREAM is None:
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        _RESULT_STREAM = os.fdopen(saved, "w", buffering=1)
+    return _RESULT_STREAM
+
+
 @dataclass
 class DistEnv:
     rank: int
@@ -35,6 +53,7 @@ class DistEnv:
 
 def init_distributed(backend=None, device="cuda"):
     """Read RANK/WORLD_SIZE/LOCAL_RANK (torchrun), bind the GPU, init the process group."""
+    protect_stdout()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -103,7 +122,8 @@ def emit(env: DistEnv, *, metric, items_per_step, unit, steps, warmup, elapsed, 
     if extra:
         out.update(extra)
     if env.is_main:
-        print(json.dumps(out), flush=True)
+        stream = _RESULT_STREAM if _RESULT_STREAM is not None else sys.stdout
+        print(json.dumps(out), file=stream, flush=True)
     return out
 
 

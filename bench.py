@@ -14,13 +14,10 @@ Rank 0 prints ONE JSON line on stdout.
 from __future__ import annotations
 
 import argparse
-import json
 import os
 import sys
-import time
 
 import torch
-import torch.distributed as dist
 
 METRIC = "seq/sec BERT-Large amp-O2+FusedLAMB DDP at 1/2/4/8 MI355X; step speedup vs fp32"
 BASELINE_VALUE = None  # BASELINE.json "published": {} -> no reference number
@@ -40,21 +37,16 @@ def parse():
     return ap.parse_args()
 
 
-def log(*a):
-    print(*a, file=sys.stderr, flush=True)
-
-
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    from apex.utils.bench import emit, finish, init_distributed, log, time_steps
+    from apex.utils.gemm_tuning import enable_tuned_gemms
+
+    tuned = enable_tuned_gemms()  # committed hipBLASLt/rocBLAS selections, read-only
+    env = init_distributed()  # also reserves stdout for the result line
+    if env.world != args.gpus:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={env.world}; using WORLD_SIZE")
+    dev = env.device
 
     import apex
     from apex import amp
@@ -74,11 +66,11 @@ def main():
     else:
         model, opt = amp.initialize(model, opt, opt_level="O2", cast_model_type=torch.bfloat16,
                                     verbosity=0)
-    if world > 1:
+    if env.world > 1:
         model = DDP(model, message_size=int(os.environ.get("APEX_DDP_MESSAGE_SIZE", 25_000_000)))
 
     g = torch.Generator(device=dev)
-    g.manual_seed(42 + rank)
+    g.manual_seed(42 + env.rank)
     batches = [synthetic_batch(cfg, args.batch, args.seq, device=dev, generator=g) for _ in range(4)]
 
     def step(i):
@@ -90,59 +82,28 @@ def main():
         opt.zero_grad()
         return loss
 
-    for i in range(args.warmup):
-        loss = step(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        loss = step(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed, loss = time_steps(env, step, args.steps, args.warmup)
     final_loss = float(loss.float().item())
-    ms = elapsed / args.steps * 1000.0
-    seqs = args.batch * world * args.steps / elapsed
-    if rank == 0:
-        out = {
-            "metric": METRIC,
-            "value": round(seqs, 3),
-            "unit": "seq/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None if BASELINE_VALUE is None else round(seqs / BASELINE_VALUE, 4),
-            "dtype": "fp32" if args.fp32 else "bf16",
-            "data": "synthetic (random token ids, 15% masked positions, random NSP labels); random-init weights",
-            "config": {
-                "model": "BERT-Large (24L, H1024, A16, FFN4096, vocab 30522)" if args.layers == 24
-                else f"BERT-Large-{args.layers}L (DEBUG, not the metric config)",
-                "global_batch": args.batch * world,
-                "per_gpu_batch": args.batch,
-                "seq_len": args.seq,
-                "max_predictions_per_seq": max(1, int(round(args.seq * 0.15))),
-                "parallelism": f"dp{world}",
-                "amp": "O0" if args.fp32 else "O2 bf16",
-                "optimizer": "FusedLAMB",
-                "norm": "FusedLayerNorm",
-                "ddp": "apex.parallel.DistributedDataParallel (RCCL)" if world > 1 else "none (1 GPU)",
-            },
-            "final_loss": round(final_loss, 4),
-        }
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    world = env.world
+    emit(env, metric=METRIC, items_per_step=args.batch * world, unit="seq/s", steps=args.steps,
+         warmup=args.warmup, elapsed=elapsed, baseline=BASELINE_VALUE, dtype="fp32" if args.fp32 else "bf16",
+         data="synthetic (random token ids, 15% masked positions, random NSP labels); random-init weights",
+         config={
+             "model": "BERT-Large (24L, H1024, A16, FFN4096, vocab 30522)" if args.layers == 24
+             else f"BERT-Large-{args.layers}L (DEBUG, not the metric config)",
+             "global_batch": args.batch * world,
+             "per_gpu_batch": args.batch,
+             "seq_len": args.seq,
+             "max_predictions_per_seq": max(1, int(round(args.seq * 0.15))),
+             "parallelism": f"dp{world}",
+             "amp": "O0" if args.fp32 else "O2 bf16",
+             "optimizer": "FusedLAMB",
+             "norm": "FusedLayerNorm",
+             "ddp": "apex.parallel.DistributedDataParallel (RCCL)" if world > 1 else "none (1 GPU)",
+             "gemm_selection": "TunableOp pre-tuned (tuning/)" if tuned else "hipBLASLt default",
+         },
+         extra={"final_loss": round(final_loss, 4)})
+    finish(env)
 
 
 if __name__ == "__main__":

@@ -51,6 +51,15 @@ __device__ __forceinline__ s16x4 lds_tr16(const void* p) {
       (__attribute__((address_space(3))) s16x4*)(p));
 }
 
+// Workgroup barrier ordering LDS traffic only: the fences are restricted to the "local"
+// address space, so outstanding global loads (register prefetches) are NOT drained at the
+// barrier the way __syncthreads()'s full workgroup fence drains them.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 template <typename V8>
 __device__ __forceinline__ V8 join4(s16x4 lo, s16x4 hi) {
   typedef short s16x8 __attribute__((ext_vector_type(8)));
@@ -156,9 +165,9 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
 
   if (ntiles > 0) gload(0);
   for (int kt = 0; kt < ntiles; ++kt) {
-    __syncthreads();  // previous tile fully consumed
+    lds_barrier();  // previous tile fully consumed
     lstore();
-    __syncthreads();
+    lds_barrier();
     if (kt + 1 < ntiles) gload(kt + 1);
     const int kb = kt * kFwdKB;
 
@@ -288,7 +297,7 @@ constexpr int kBwdBK = 32 * kBwdWaves;  // 128 keys per workgroup
 constexpr int kBwdBQ = 32;              // queries per inner step
 
 template <typename T, int D, bool CAUSAL, bool DROPOUT>
-__global__ void __launch_bounds__(256, 1) attn_bwd_kernel(AttnArgs a, const void* dout, float* dq_acc,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 64 ? 2 : 1, D == 64 ? 2 : 1))) attn_bwd_kernel(AttnArgs a, const void* dout, float* dq_acc,
                                                          void* dk_out, void* dv_out) {
   using M = MfmaT<T>;
   using V8 = typename M::V8;
@@ -353,47 +362,67 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_kernel(AttnArgs a, const void
   const float rkeep = a.drop_scale;
   const bool single_kblock = (a.Sk <= kBwdBK);
 
-  for (int qb = qstart; qb < nq; qb += kBwdBQ) {
-    __syncthreads();
-    // stage Q, dO tiles (32 x D) + lse; delta = rowsum(dO * O) computed here from O
-    // (CPR consecutive threads own one row -> xor-shuffle reduce), no separate pass.
-    constexpr int CPR = D / 8;
+  // Q / dO / O tiles (32 x D), lse and the dropout words of the NEXT query block are loaded
+  // into registers while the current block computes (software pipelining); the barriers
+  // below only wait for LDS traffic so these global loads stay in flight across them.
+  constexpr int CPR = D / 8;
+  constexpr int NLD = kBwdBQ * CPR / 256;
+  uint4 pf_q[NLD], pf_do[NLD], pf_o[NLD];
+  float pf_lse = INFINITY;
+  uint16_t pf_mask = 0;
+  auto fetch = [&](int qb) {
 #pragma unroll
-    for (int c = 0; c < kBwdBQ * CPR / 256; ++c) {
+    for (int c = 0; c < NLD; ++c) {
       const int idx = threadIdx.x + 256 * c;
       const int row = idx / CPR, col = (idx % CPR) * 8;
       const int q = qb + row;
-      uint4 qv = make_uint4(0, 0, 0, 0), dv4 = make_uint4(0, 0, 0, 0);
-      float part = 0.f;
       if (q < nq) {
-        qv = *(const uint4*)(qp + (int64_t)q * a.q_ss + col);
-        dv4 = *(const uint4*)(dop + (int64_t)q * a.do_ss + col);
-        float ov[8], dov[8];
-        load_f<T, 8>(op + (int64_t)q * a.o_ss + col, ov);
-        load_f<T, 8>((const T*)&dv4, dov);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) part += ov[e] * dov[e];
+        pf_q[c] = *(const uint4*)(qp + (int64_t)q * a.q_ss + col);
+        pf_do[c] = *(const uint4*)(dop + (int64_t)q * a.do_ss + col);
+        pf_o[c] = *(const uint4*)(op + (int64_t)q * a.o_ss + col);
+      } else {
+        pf_q[c] = pf_do[c] = pf_o[c] = make_uint4(0, 0, 0, 0);
       }
-#pragma unroll
-      for (int o = CPR / 2; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
-      if ((idx % CPR) == 0) lds_delta[row] = part;
-      *(uint4*)(lds_q + row * LDR + col) = qv;
-      *(uint4*)(lds_do + row * LDR + col) = dv4;
     }
     if (threadIdx.x < kBwdBQ) {
       const int q = qb + threadIdx.x;
-      lds_lse[threadIdx.x] = q < nq ? lsep[q] * kLog2e : INFINITY;
+      pf_lse = q < nq ? lsep[q] * kLog2e : INFINITY;
     }
     if (DROPOUT) {
       // dropout bits written by the forward pass: [q][32-key block][half] uint16 words
       const int qi = threadIdx.x >> 3, w = threadIdx.x & 7;
       const int q = qb + qi, blk = (k0 >> 5) + (w >> 1);
-      uint16_t word = 0;
-      if (q < nq && blk * 32 < a.Sk)
-        word = a.dmask[((int64_t)bh * a.Sq + q) * a.mask_words + blk * 2 + (w & 1)];
-      lds_mask[threadIdx.x] = word;
+      pf_mask = (q < nq && blk * 32 < a.Sk)
+                    ? a.dmask[((int64_t)bh * a.Sq + q) * a.mask_words + blk * 2 + (w & 1)]
+                    : (uint16_t)0;
     }
-    __syncthreads();
+  };
+  if (qstart < nq) fetch(qstart);
+
+  for (int qb = qstart; qb < nq; qb += kBwdBQ) {
+    lds_barrier();
+    // stage the prefetched tiles; delta = rowsum(dO * O) is computed here from O
+    // (CPR consecutive threads own one row -> xor-shuffle reduce), no separate pass.
+#pragma unroll
+    for (int c = 0; c < NLD; ++c) {
+      const int idx = threadIdx.x + 256 * c;
+      const int row = idx / CPR, col = (idx % CPR) * 8;
+      float ov[8], dov[8];
+      load_f<T, 8>((const T*)&pf_o[c], ov);
+      load_f<T, 8>((const T*)&pf_do[c], dov);
+      float part = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) part += ov[e] * dov[e];
+#pragma unroll
+      for (int o = CPR / 2; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+      if ((idx % CPR) == 0) lds_delta[row] = part;
+      *(uint4*)(lds_q + row * LDR + col) = pf_q[c];
+      *(uint4*)(lds_do + row * LDR + col) = pf_do[c];
+    }
+    if (threadIdx.x < kBwdBQ) lds_lse[threadIdx.x] = pf_lse;
+    if (DROPOUT) lds_mask[threadIdx.x] = pf_mask;
+    if (qb + kBwdBQ < nq) fetch(qb + kBwdBQ);
+    lds_barrier();
 
     // S = Q . K^T  [32 q x 32 keys]: A = Q rows (LDS), B = K rows (regs)
     f32x16 sacc = f32x16{}, dpacc = f32x16{};
@@ -448,7 +477,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_kernel(AttnArgs a, const void
       const int qi = (i & 3) + 8 * (i >> 2) + 4 * hl;
       lds_ds[qi * LDS_S + 32 * wid + r] = (T)ds[i];
     }
-    __syncthreads();
+    lds_barrier();
     // dQ [32 q x D]: waves split the D/32 column blocks and the 128-key contraction:
     // wave w: column block (w % (D/32)), key range half/quarter when D/32 < 4
     {
@@ -476,7 +505,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_kernel(AttnArgs a, const void
 #pragma unroll
           for (int i = 0; i < 16; ++i) lds_dqred[((ks - 1) * NCB + cb) * 1024 + i * 64 + lane] = dq[i];
         }
-        __syncthreads();
+        lds_barrier();
         if (ks == 0) {
 #pragma unroll
           for (int k2 = 1; k2 < KSPLIT; ++k2)
