@@ -18,6 +18,8 @@ results are reproducible under ``torch.manual_seed`` and no mask tensor is store
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -37,6 +39,44 @@ def _native(*ts):
 
 def _2d(x):
     return x.reshape(-1, x.shape[-1])
+
+
+_WGRAD_SPLITK = os.environ.get("APEX_WGRAD_SPLITK", "auto")
+
+
+def _wgrad_splits(M, N, K):
+    """K-slices for dW[N,K] = dY[M,N]^T X[M,K] (M = tokens, the contraction).
+
+    A 1024x1024 weight gradient is only 16 output tiles of 256x256 — a sixteenth of the 256
+    CUs — however long its M=32k contraction is, so the library GEMM runs at ~0.5 PF/s.
+    Slicing M into S batched GEMMs fills the chip (S*tiles ~ 128-256 workgroups); the fp32
+    slabs are combined by one HIP reduction that writes the grad dtype. Measured on MI355X
+    (tools/gemm_bench.py, BERT-Large shapes, M = 32768): 1024x1024 199 -> 79 us (S=8),
+    3072x1024 288 -> 199 us (S=4), 4096x1024 316 -> 262 us (S=4).
+    """
+    if _WGRAD_SPLITK == "0":
+        return 1
+    if _WGRAD_SPLITK not in ("auto", ""):
+        s = int(_WGRAD_SPLITK)
+        return s if M % s == 0 else 1
+    if M < 8192:
+        return 1
+    tiles = ((N + 255) // 256) * ((K + 255) // 256)
+    s = 1
+    while s < 8 and 2 * s * tiles <= 256 and M % (2 * s) == 0 and M // (2 * s) >= 1024:
+        s *= 2
+    return s
+
+
+def _wgrad(dy2, x2):
+    """Weight gradient dy2^T @ x2 in dy2's dtype (split-K batched GEMM when it pays)."""
+    M, N = dy2.shape
+    K = x2.shape[1]
+    s = _wgrad_splits(M, N, K) if dy2.dtype in (torch.bfloat16, torch.float16) else 1
+    if s == 1 or not (dy2.is_contiguous() and x2.is_contiguous()):
+        return torch.mm(dy2.t(), x2)
+    slabs = torch.bmm(dy2.view(s, M // s, N).transpose(1, 2), x2.view(s, M // s, K), out_dtype=torch.float32)
+    return _ext.require().splitk_reduce(slabs, dy2.dtype)
 
 
 # ---------------------------------------------------------------------------
@@ -73,7 +113,7 @@ class _FusedDense(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = torch.mm(dy2, w).view(*dy.shape[:-1], w.shape[1])
         if ctx.needs_input_grad[1]:
-            dw = torch.mm(dy2.t(), x2)
+            dw = _wgrad(dy2, x2)
         if ctx.has_b and ctx.needs_input_grad[2]:
             db = _ext.require().colsum(dy2, ctx.bdtype)
         return dx, dw, db
@@ -102,7 +142,7 @@ class _DenseAct(torch.autograd.Function):
         x2, w, h, b = ctx.saved_tensors
         dh, db = C.bias_act_bwd(_2d(dy), h, b, ctx.act)
         dx = torch.mm(dh, w).view(*dy.shape[:-1], w.shape[1]) if ctx.needs_input_grad[0] else None
-        dw = torch.mm(dh.t(), x2) if ctx.needs_input_grad[1] else None
+        dw = _wgrad(dh, x2) if ctx.needs_input_grad[1] else None
         return dx, dw, (db if b is not None else None), None
 
 
@@ -176,7 +216,7 @@ class _DenseBDALN(torch.autograd.Function):
         p, seed, off, has_b = ctx.cfg
         dres, dt, dg, dbeta, db = C.bdaln_bwd(_2d(dy), s, gamma, mean, rstd, float(p), seed, off, has_b)
         dx = torch.mm(dt, w).view(*dy.shape[:-1], w.shape[1]) if ctx.needs_input_grad[0] else None
-        dw = torch.mm(dt.t(), x2) if ctx.needs_input_grad[1] else None
+        dw = _wgrad(dt, x2) if ctx.needs_input_grad[1] else None
         return dx, dw, (db if has_b else None), dres.view_as(dy), dg, dbeta, None, None
 
 

@@ -16,6 +16,7 @@ from __future__ import annotations
 import torch
 
 from ..multi_tensor_apply import ops as mt_ops
+from ..utils import prof
 from ._base import FusedOptimizerBase
 
 
@@ -54,10 +55,11 @@ class FusedLAMB(FusedOptimizerBase):
         all_grads = [g for (gs, _, _) in per_group for g in gs]
         if not all_grads:
             return loss
-        if self._native(all_grads):
-            self._step_native(per_group, all_grads)
-        else:
-            self._step_reference(per_group, all_grads)
+        with prof.range("apex.optim.FusedLAMB.step"):
+            if self._native(all_grads):
+                self._step_native(per_group, all_grads)
+            else:
+                self._step_reference(per_group, all_grads)
         return loss
 
     # ------------------------------------------------------------------

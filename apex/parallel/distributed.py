@@ -37,6 +37,8 @@ import torch
 import torch.distributed as dist
 from torch.nn.modules import Module
 
+from ..utils import prof
+
 # ----------------------------------------------------------------------------
 # flat collective helpers (R-17)
 # ----------------------------------------------------------------------------
@@ -323,10 +325,11 @@ class DistributedDataParallel(Module):
         return self._reduce_inner(buf, async_op)
 
     def _reduce_inner(self, buf, async_op):
-        if not self.gradient_average:
-            return dist.all_reduce(buf, group=self.group, async_op=async_op)
-        return _all_reduce_avg(buf, self.group, async_op=async_op,
-                               predivide=self.gradient_predivide_factor)
+        with prof.range("apex.ddp.allreduce[{}]".format(buf.numel())):
+            if not self.gradient_average:
+                return dist.all_reduce(buf, group=self.group, async_op=async_op)
+            return _all_reduce_avg(buf, self.group, async_op=async_op,
+                                   predivide=self.gradient_predivide_factor)
 
     def _end_of_backward(self):
         if not self._layout_ready:

@@ -457,6 +457,19 @@ Tensor k_colsum(Tensor x, at::ScalarType out_dtype) {
   return out;
 }
 
+// split-K combine: slabs fp32 [S, ...] -> sum over S in out_dtype, shape slabs.shape[1:]
+Tensor k_splitk_reduce(Tensor slabs, at::ScalarType out_dtype) {
+  TORCH_CHECK(slabs.is_cuda() && slabs.scalar_type() == at::kFloat && slabs.dim() >= 2, "splitk_reduce: fp32 slabs");
+  Tensor sc = slabs.contiguous();
+  Tensor out = at::empty(sc.sizes().slice(1), sc.options().dtype(out_dtype));
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(sc.data_ptr()) % 16 == 0 && (out.numel() % 4 == 0 || sc.size(0) == 1),
+              "splitk_reduce: alignment");
+  check(apex::splitk_reduce(sc.data_ptr<float>(), out.data_ptr(), out.numel(), (int)sc.size(0), dt_code(out_dtype),
+                            cur_stream()),
+        "splitk_reduce");
+  return out;
+}
+
 bool k_bdaln_supported(int64_t cols) { return apex::bdaln_supported((int)cols) != 0; }
 
 std::vector<Tensor> k_bdaln_fwd(Tensor x, const c10::optional<Tensor>& b, Tensor res, Tensor gamma,
@@ -780,6 +793,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bias_dropout_add_fwd", &k_bda_fwd);
   m.def("bias_dropout_add_bwd", &k_bda_bwd);
   m.def("colsum", &k_colsum);
+  m.def("splitk_reduce", &k_splitk_reduce);
   m.def("bdaln_supported", &k_bdaln_supported);
   m.def("bdaln_fwd", &k_bdaln_fwd);
   m.def("bdaln_bwd", &k_bdaln_bwd);

@@ -468,6 +468,56 @@ int colsum(const void* x, void* out, float* ws, int64_t rows, int cols, int xdt,
   return bias_dropout_add_bwd(x, nullptr, out, ws, rows, cols, 0, 0, 0, 1.f, xdt, odt, s);
 }
 
+// ---------------------------------------------------------------------------
+// split-K combine for the weight-gradient GEMMs: out[n] = sum_s slabs[s][n] (fp32 slabs from
+// a batched GEMM over K slices) written once in the output dtype. 8 elements per lane, slabs
+// walked with independent loads (no dependency between slices).
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ slabs, T* __restrict__ out,
+                                                            int64_t n, int nsplit) {
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (i >= n) return;
+  if (i + 8 <= n) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < nsplit; ++s) {
+      float a[4], b[4];
+      load_f<float, 4>(slabs + (int64_t)s * n + i, a);
+      load_f<float, 4>(slabs + (int64_t)s * n + i + 4, b);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        acc[e] += a[e];
+        acc[4 + e] += b[e];
+      }
+    }
+    if constexpr (sizeof(T) == 4) {
+      float lo[4] = {acc[0], acc[1], acc[2], acc[3]}, hi[4] = {acc[4], acc[5], acc[6], acc[7]};
+      store_f<T, 4>(out + i, lo);
+      store_f<T, 4>(out + i + 4, hi);
+    } else {
+      store_f<T, 8>(out + i, acc);
+    }
+  } else {
+    for (int64_t j = i; j < n; ++j) {
+      float acc = 0.f;
+      for (int s = 0; s < nsplit; ++s) acc += slabs[(int64_t)s * n + j];
+      out[j] = from_f<T>(acc);
+    }
+  }
+}
+
+int splitk_reduce(const float* slabs, void* out, int64_t n, int nsplit, int odt, hipStream_t s) {
+  if (n == 0) return 0;
+  const unsigned grid = (unsigned)((n / 8 + 256) / 256);
+  if (odt == kF32)
+    hipLaunchKernelGGL((splitk_reduce_kernel<float>), dim3(grid), dim3(256), 0, s, slabs, (float*)out, n, nsplit);
+  else if (odt == kF16)
+    hipLaunchKernelGGL((splitk_reduce_kernel<f16>), dim3(grid), dim3(256), 0, s, slabs, (f16*)out, n, nsplit);
+  else
+    hipLaunchKernelGGL((splitk_reduce_kernel<bf16>), dim3(grid), dim3(256), 0, s, slabs, (bf16*)out, n, nsplit);
+  return (int)hipGetLastError();
+}
+
 static inline int bdaln_vpt(int cols) {
   if (cols % 8) return 0;
   const int nvec = cols / 8;

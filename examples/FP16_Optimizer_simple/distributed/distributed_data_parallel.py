@@ -18,6 +18,8 @@ from apex.parallel import DistributedDataParallel as DDP
 ap = argparse.ArgumentParser()
 ap.add_argument("--local_rank", "--local-rank", default=int(os.environ.get("LOCAL_RANK", 0)), type=int)
 ap.add_argument("--steps", type=int, default=500)
+ap.add_argument("--torch-ddp", action="store_true",
+                help="wrap with torch.nn.parallel.DistributedDataParallel instead of apex's (interop check)")
 args = ap.parse_args()
 
 cuda = torch.cuda.is_available()
@@ -30,7 +32,11 @@ N, D_in, D_out = 64, 1024, 16
 torch.manual_seed(dist.get_rank())
 x = torch.randn(N, D_in, device=dev).to(low)
 y = torch.randn(N, D_out, device=dev).to(low)
-model = DDP(torch.nn.Linear(D_in, D_out).to(dev, low))
+net = torch.nn.Linear(D_in, D_out).to(dev, low)
+if args.torch_ddp:
+    model = torch.nn.parallel.DistributedDataParallel(net, device_ids=[args.local_rank] if cuda else None)
+else:
+    model = DDP(net)
 optimizer = FP16_Optimizer(torch.optim.SGD(model.parameters(), lr=1e-3), verbose=False)
 loss_fn = torch.nn.MSELoss()
 for t in range(args.steps):

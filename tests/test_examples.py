@@ -28,9 +28,10 @@ def test_fp16_optimizer_simple(name, tmp_path):
         assert "identical params: True" in out
 
 
-def test_fp16_optimizer_simple_distributed(tmp_path):
+@pytest.mark.parametrize("torch_ddp", [False, True])
+def test_fp16_optimizer_simple_distributed(tmp_path, torch_ddp):
     out = _run([os.path.join(EX, "FP16_Optimizer_simple", "distributed", "distributed_data_parallel.py"),
-                "--steps", "5"], tmp_path, torchrun=2)
+                "--steps", "5"] + (["--torch-ddp"] if torch_ddp else []), tmp_path, torchrun=2)
     assert out.count("final loss") == 2
 
 
