@@ -15,6 +15,7 @@ MI355X choices:
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -22,6 +23,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from ..normalization import FusedLayerNorm
+from ..ops import blocks as fblocks
 from ..ops import fused as fops
 
 
@@ -112,7 +114,13 @@ class BertLayer(nn.Module):
         self.p = c.hidden_dropout_prob
         self.eps = c.layer_norm_eps
 
+    use_sublayer_fusion = os.environ.get("APEX_BERT_SUBLAYER_FUSION", "1") != "0"
+
     def forward(self, x, k_lens):
+        if self.use_sublayer_fusion:
+            y = self._forward_sublayers(x, k_lens)
+            if y is not None:
+                return y
         p = self.p if self.training else 0.0
         ctx = self.attention.context(x, k_lens)
         d = self.attention.dense
@@ -121,6 +129,25 @@ class BertLayer(nn.Module):
         h = fops.dense_gelu(x, self.intermediate.weight, self.intermediate.bias)
         return fops.dense_bias_dropout_add_ln(h, self.output.weight, self.output.bias, x,
                                               self.out_ln.weight, self.out_ln.bias, p, self.eps)
+
+    def _forward_sublayers(self, x, k_lens):
+        """Both sublayers as whole-sublayer Functions (apex/ops/blocks.py): the residual
+        gradients ride in the input-gradient GEMMs' epilogues. None -> op-by-op path."""
+        a = self.attention
+        y = fblocks.attention_sublayer(x, a.qkv.weight, a.qkv.bias, a.dense.weight, a.dense.bias,
+                                       self.attn_ln.weight, self.attn_ln.bias, a.h, a.p_attn, self.p,
+                                       self.eps, k_lens=k_lens, training=self.training)
+        if y is None:
+            return None
+        out = fblocks.ffn_sublayer(y, self.intermediate.weight, self.intermediate.bias, self.output.weight,
+                                   self.output.bias, self.out_ln.weight, self.out_ln.bias, self.p, self.eps,
+                                   training=self.training)
+        if out is None:
+            return fops.dense_bias_dropout_add_ln(
+                fops.dense_gelu(y, self.intermediate.weight, self.intermediate.bias), self.output.weight,
+                self.output.bias, y, self.out_ln.weight, self.out_ln.bias, self.p if self.training else 0.0,
+                self.eps)
+        return out
 
 
 class BertModel(nn.Module):

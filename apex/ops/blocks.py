@@ -1,0 +1,124 @@
+"""Whole-sublayer autograd Functions for post-LN transformer encoders (BERT).
+
+A post-LN encoder layer uses its input twice per sublayer — as the GEMM input and as the
+residual — so autograd would sum two gradients with a separate elementwise kernel per
+sublayer (two full [tokens, hidden] read-read-write passes per layer). As one Function,
+the backward folds the residual gradient into the input-gradient GEMM's epilogue
+(``addmm(dres, dY, W)``: hipBLASLt reads C once in the epilogue), and every elementwise
+stage stays a single fused HIP kernel:
+
+  attention sublayer: y = LN(x + dropout(Attn(x Wqkv^T + bqkv) Wo^T + bo))
+      fwd: GEMM(+bias) -> flash attn fwd (MFMA) -> GEMM -> bias+dropout+residual+LN
+      bwd: bdaln bwd -> GEMM (dctx) + split-K wgrad -> flash attn bwd -> bias colsum +
+           split-K wgrad -> GEMM with the residual grad accumulated in its epilogue
+  FFN sublayer:       y = LN(x + dropout(act(x W1^T + b1) W2^T + b2))
+      fwd: GEMM -> bias+act -> GEMM -> bias+dropout+residual+LN
+      bwd: bdaln bwd -> GEMM + wgrad -> bias+act bwd (bias grad folded in) -> wgrad ->
+           GEMM with the residual grad accumulated in its epilogue
+
+The numerics are those of the unfused composition in apex.ops.fused (tests compare them).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .. import _ext
+from .fused import ACT_GELU, _2d, _seed, _wgrad
+
+
+class _AttnSublayer(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, wqkv, bqkv, wo, bo, gamma, beta, heads, p_attn, p_hidden, eps, causal, k_lens):
+        C = _ext.require()
+        B, S, E = x.shape
+        d = E // heads
+        scale = 1.0 / math.sqrt(d)
+        x2 = _2d(x)
+        qkv = torch.addmm(bqkv, x2, wqkv.t()) if bqkv is not None else torch.mm(x2, wqkv.t())
+        q, k, v = qkv.view(B, S, 3, heads, d).unbind(2)
+        sa, oa = _seed() if p_attn > 0 else (0, 0)
+        o, lse, dmask = C.flash_attn_fwd(q, k, v, bool(causal), scale, float(p_attn), sa, oa, k_lens)
+        o2 = o.view(B * S, E)
+        t = torch.mm(o2, wo.t())
+        sh, oh = _seed() if p_hidden > 0 else (0, 0)
+        y, s, mean, rstd = C.bdaln_fwd(t, bo, x2.contiguous(), gamma, beta, float(eps), float(p_hidden), sh, oh)
+        ctx.save_for_backward(x2, wqkv, qkv, o, lse, k_lens, dmask, wo, s, gamma, mean, rstd)
+        ctx.cfg = (B, S, E, heads, d, scale, causal, p_attn, sa, oa, p_hidden, sh, oh, bqkv is not None,
+                   bo is not None, bqkv.dtype if bqkv is not None else None)
+        return y.view(B, S, E)
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = _ext.require()
+        x2, wqkv, qkv, o, lse, k_lens, dmask, wo, s, gamma, mean, rstd = ctx.saved_tensors
+        B, S, E, heads, d, scale, causal, p_attn, sa, oa, p_hidden, sh, oh, has_bqkv, has_bo, bdt = ctx.cfg
+        dres, dt, dgamma, dbeta, dbo = C.bdaln_bwd(_2d(dy), s, gamma, mean, rstd, float(p_hidden), sh, oh, has_bo)
+        dwo = _wgrad(dt, o.view(B * S, E))
+        dctx = torch.mm(dt, wo).view(B, S, heads, d)
+        q, k, v = qkv.view(B, S, 3, heads, d).unbind(2)
+        dqkv = torch.empty_like(qkv)
+        dq, dk, dv = dqkv.view(B, S, 3, heads, d).unbind(2)
+        C.flash_attn_bwd(dctx, q, k, v, o, lse, dq, dk, dv, bool(causal), scale, float(p_attn), sa, oa, k_lens,
+                         dmask)
+        dbqkv = C.colsum(dqkv, bdt) if has_bqkv else None
+        dwqkv = _wgrad(dqkv, x2)
+        dx = torch.addmm(dres, dqkv, wqkv)  # residual grad accumulated in the GEMM epilogue
+        return (dx.view(B, S, E), dwqkv, dbqkv, dwo, dbo if has_bo else None, dgamma, dbeta,
+                None, None, None, None, None, None)
+
+
+class _FFNSublayer(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, gamma, beta, p, eps, act):
+        C = _ext.require()
+        x2 = _2d(x)
+        h = torch.mm(x2, w1.t())
+        g = C.bias_act_fwd(h, b1, act)
+        t = torch.mm(g, w2.t())
+        seed, off = _seed() if p > 0 else (0, 0)
+        y, s, mean, rstd = C.bdaln_fwd(t, b2, x2.contiguous(), gamma, beta, float(eps), float(p), seed, off)
+        ctx.save_for_backward(x2, w1, b1, h, g, w2, s, gamma, mean, rstd)
+        ctx.cfg = (p, seed, off, act, b2 is not None)
+        return y.view_as(x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = _ext.require()
+        x2, w1, b1, h, g, w2, s, gamma, mean, rstd = ctx.saved_tensors
+        p, seed, off, act, has_b2 = ctx.cfg
+        dres, dt, dgamma, dbeta, db2 = C.bdaln_bwd(_2d(dy), s, gamma, mean, rstd, float(p), seed, off, has_b2)
+        dw2 = _wgrad(dt, g)
+        dg = torch.mm(dt, w2)
+        dh, db1 = C.bias_act_bwd(dg, h, b1, act)
+        dw1 = _wgrad(dh, x2)
+        dx = torch.addmm(dres, dh, w1)  # residual grad accumulated in the GEMM epilogue
+        return (dx.view_as(dy), dw1, db1 if b1 is not None else None, dw2, db2 if has_b2 else None, dgamma, dbeta,
+                None, None, None)
+
+
+def _ok(x, *dims):
+    return _ext.use_native(x) and x.dtype in (torch.float16, torch.bfloat16) and x.is_contiguous() and \
+        all(d % 8 == 0 for d in dims) and _ext.require().bdaln_supported(x.shape[-1])
+
+
+def attention_sublayer(x, wqkv, bqkv, wo, bo, gamma, beta, heads, p_attn=0.0, p_hidden=0.0, eps=1e-12,
+                       causal=False, k_lens=None, training=True):
+    """LN(x + dropout(MHA(x) Wo^T + bo)) for x [B, S, E]; returns None when the fused path does
+    not apply (caller falls back to the op-by-op composition)."""
+    E = x.shape[-1]
+    d = E // heads
+    if not (_ok(x, E) and d in (64, 128) and gamma is not None and beta is not None):
+        return None
+    p_attn = p_attn if training else 0.0
+    p_hidden = p_hidden if training else 0.0
+    return _AttnSublayer.apply(x, wqkv, bqkv, wo, bo, gamma, beta, int(heads), float(p_attn), float(p_hidden),
+                               float(eps), bool(causal), k_lens)
+
+
+def ffn_sublayer(x, w1, b1, w2, b2, gamma, beta, p=0.0, eps=1e-12, act=ACT_GELU, training=True):
+    """LN(x + dropout(act(x W1^T + b1) W2^T + b2)); None when the fused path does not apply."""
+    if not (_ok(x, x.shape[-1], w1.shape[0]) and gamma is not None and beta is not None):
+        return None
+    return _FFNSublayer.apply(x, w1, b1, w2, b2, gamma, beta, float(p if training else 0.0), float(eps), int(act))

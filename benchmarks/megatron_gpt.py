@@ -21,7 +21,7 @@ def main():
     ap.add_argument("--pp", type=int, default=2)
     ap.add_argument("--hidden", type=int, default=2560)
     ap.add_argument("--layers", type=int, default=32)
-    ap.add_argument("--heads", type=int, default=32)
+    ap.add_argument("--heads", type=int, default=20, help="head dim 128 (2560/20) runs the MFMA flash kernel")
     ap.add_argument("--seq", type=int, default=2048)
     ap.add_argument("--micro-batch", type=int, default=4)
     ap.add_argument("--global-batch", type=int, default=32)

@@ -166,3 +166,32 @@ def test_splitk_reduce_tail():
     torch.testing.assert_close(C.splitk_reduce(slabs, torch.float32), slabs.sum(0))
     slabs = torch.randn(4, 20, device=DEV)
     torch.testing.assert_close(C.splitk_reduce(slabs, torch.bfloat16).float(), slabs.sum(0).bfloat16().float())
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_bert_sublayer_fusion_matches_op_by_op(p):
+    """Whole-sublayer Functions (residual grads in the GEMM epilogues) vs the op-by-op path."""
+    from apex.models.bert import BertConfig, BertLayer
+
+    torch.manual_seed(0)
+    c = BertConfig(hidden_size=256, num_attention_heads=4, intermediate_size=1024, num_hidden_layers=1,
+                   hidden_dropout_prob=p, attention_probs_dropout_prob=p)
+    layer = BertLayer(c).to(DEV).bfloat16()
+    x = torch.randn(4, 64, 256, device=DEV).bfloat16()
+    k_lens = torch.tensor([64, 40, 64, 17], device=DEV, dtype=torch.int32)
+    outs = []
+    for fused in (True, False):
+        layer.use_sublayer_fusion = fused
+        layer.zero_grad()
+        xi = x.clone().requires_grad_(True)
+        torch.manual_seed(123)
+        y = layer(xi, k_lens)
+        torch.manual_seed(7)
+        dy = torch.randn_like(y)
+        y.backward(dy)
+        outs.append((y.float(), xi.grad.float(), {n: q.grad.float() for n, q in layer.named_parameters()}))
+    (y1, dx1, g1), (y2, dx2, g2) = outs
+    torch.testing.assert_close(y1, y2, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(dx1, dx2, rtol=3e-2, atol=3e-2)
+    for n in g1:
+        torch.testing.assert_close(g1[n], g2[n], rtol=5e-2, atol=5e-2, msg=n)

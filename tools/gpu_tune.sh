@@ -14,3 +14,5 @@ timeout -k 10 120 python bench.py --steps 20 --warmup 5 > $O/bench_old.json 2> $
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 120 rocprofv3 -L > $O/counters_avail.txt 2>&1
 echo "all done"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof_gpt2 -o prof --output-format csv -- python benchmarks/gpt2.py --steps 3 --warmup 1 > $O/gpt2_prof.json 2> $O/gpt2_prof.err || exit 9
+echo "gpt2 prof done"
