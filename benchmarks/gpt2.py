@@ -25,6 +25,9 @@ def main():
     args = ap.parse_args()
 
     from apex.utils.bench import emit, finish, init_distributed, time_steps
+    from apex.utils.gemm_tuning import enable_tuned_gemms
+
+    enable_tuned_gemms()
 
     env = init_distributed()
     import apex

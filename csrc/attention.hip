@@ -21,6 +21,8 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <type_traits>
+
 namespace apex {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -182,23 +184,34 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
         st[sb] = M::mma(kf, qf[s], st[sb]);
       }
     }
-    // ---- scale + mask + running max
+    // ---- mask (boundary tiles only) + running max on the RAW scores; the softmax scale is
+    // folded into the exp2 argument (one FMA per element) and exp2 is the bare v_exp_f32
+    // (no denormal range reduction: underflow to 0 is what softmax wants).
+    const bool interior = (kb + kFwdKB <= Sk) && (!CAUSAL || kb + kFwdKB - 1 <= q0 + 32 * wid);
     float tmax = -INFINITY;
+    if (interior) {
 #pragma unroll
-    for (int sb = 0; sb < 2; ++sb) {
+      for (int sb = 0; sb < 2; ++sb)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int key = kb + 32 * sb + (i & 3) + 8 * (i >> 2) + 4 * hl;
-        float t = st[sb][i] * a.scale_log2;
-        if (key >= Sk || (CAUSAL && key > qrow)) t = -INFINITY;
-        st[sb][i] = t;
-        tmax = fmaxf(tmax, t);
+        for (int i = 0; i < 16; ++i) tmax = fmaxf(tmax, st[sb][i]);
+    } else {
+#pragma unroll
+      for (int sb = 0; sb < 2; ++sb) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int key = kb + 32 * sb + (i & 3) + 8 * (i >> 2) + 4 * hl;
+          float t = st[sb][i];
+          if (key >= Sk || (CAUSAL && key > qrow)) t = -INFINITY;
+          st[sb][i] = t;
+          tmax = fmaxf(tmax, t);
+        }
       }
     }
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
     const float mnew = fmaxf(m, tmax);
     const float muse = mnew == -INFINITY ? 0.f : mnew;
-    const float alpha = exp2f(m - muse);
+    const float alpha = __builtin_amdgcn_exp2f((m - muse) * a.scale_log2);
+    const float mscaled = -muse * a.scale_log2;
     m = mnew;
     float psum = 0.f;
 #pragma unroll
@@ -227,7 +240,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int i = 4 * g + e;
-          const float p = exp2f(st[sb][i] - muse);
+          const float p = __builtin_amdgcn_exp2f(fmaf(st[sb][i], a.scale_log2, mscaled));
           psum += p;
           float pd = p;
           if (DROPOUT) {
@@ -285,7 +298,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
       }
     }
     if (hl == 0 && a.lse)
-      a.lse[(int64_t)bh * a.Sq + qrow] = ltot > 0.f ? (m + log2f(ltot)) * kLn2 : INFINITY;
+      a.lse[(int64_t)bh * a.Sq + qrow] = ltot > 0.f ? (m * a.scale_log2 + log2f(ltot)) * kLn2 : INFINITY;
   }
 }
 
@@ -437,6 +450,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 6
     float pd[16], ds[16];
     // this lane's key within its 32-key block: forward stored it as bit kbit of half khalf
     const int khalf = (r >> 2) & 1, kbit = (r & 3) + 4 * (r >> 3);
+    // exp2 is the bare v_exp_f32 (no denormal range reduction)
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int qr0 = (g * 8) + 4 * hl;
@@ -445,9 +459,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 6
         const int i = 4 * g + e;
         const int qi = qr0 + e;
         const int q = qb + qi;
-        float t = sacc[i] * a.scale_log2 - lds_lse[qi];
-        bool valid = (mykey < Sk) && (q < nq) && !(CAUSAL && mykey > q);
-        const float p = valid ? exp2f(t) : 0.f;
+        const float t = sacc[i] * a.scale_log2 - lds_lse[qi];
+        const bool valid = (mykey < Sk) && (q < nq) && !(CAUSAL && mykey > q);
+        const float p = valid ? __builtin_amdgcn_exp2f(t) : 0.f;
         float keep = 1.f;
         if (DROPOUT) keep = ((lds_mask[qi * 8 + wid * 2 + khalf] >> kbit) & 1) ? rkeep : 0.f;
         pd[i] = p * keep;                                   // dropped P (for dV)

@@ -9,7 +9,12 @@ import argparse
 import json
 import math
 
+import os
+import sys
+
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 SHAPES = {
     "bert": dict(B=256, S=128, H=16, D=64, causal=False),
