@@ -114,10 +114,9 @@ class BertLayer(nn.Module):
         self.p = c.hidden_dropout_prob
         self.eps = c.layer_norm_eps
 
-    # whole-sublayer Functions: numerically equivalent, but measured 1 % slower end to end on
-    # MI355X (the beta=1 input-gradient GEMM picks a slower hipBLASLt kernel than the plain
-    # GEMM + add), so opt-in
-    use_sublayer_fusion = os.environ.get("APEX_BERT_SUBLAYER_FUSION", "0") == "1"
+    # whole-sublayer Functions (apex/ops/blocks.py) on the MFMA GEMM with fused epilogues;
+    # APEX_BERT_SUBLAYER_FUSION=0 selects the op-by-op composition (same numerics)
+    use_sublayer_fusion = os.environ.get("APEX_BERT_SUBLAYER_FUSION", "1") == "1"
 
     def forward(self, x, k_lens):
         if self.use_sublayer_fusion:

@@ -3,18 +3,18 @@
 A post-LN encoder layer uses its input twice per sublayer — as the GEMM input and as the
 residual — so autograd would sum two gradients with a separate elementwise kernel per
 sublayer (two full [tokens, hidden] read-read-write passes per layer). As one Function,
-the backward folds the residual gradient into the input-gradient GEMM's epilogue
-(``addmm(dres, dY, W)``: hipBLASLt reads C once in the epilogue), and every elementwise
-stage stays a single fused HIP kernel:
+the backward folds the residual gradient into the input-gradient GEMM's epilogue, and the
+dense layers run on the hand-written MFMA GEMM (apex/ops/gemm.py, csrc/gemm.hip) with the
+bias / GELU / dGELU(+bias grad) / residual work fused into its epilogue:
 
   attention sublayer: y = LN(x + dropout(Attn(x Wqkv^T + bqkv) Wo^T + bo))
-      fwd: GEMM(+bias) -> flash attn fwd (MFMA) -> GEMM -> bias+dropout+residual+LN
+      fwd: GEMM+bias -> flash attn fwd (MFMA) -> GEMM -> bias+dropout+residual+LN
       bwd: bdaln bwd -> GEMM (dctx) + split-K wgrad -> flash attn bwd -> bias colsum +
-           split-K wgrad -> GEMM with the residual grad accumulated in its epilogue
-  FFN sublayer:       y = LN(x + dropout(act(x W1^T + b1) W2^T + b2))
-      fwd: GEMM -> bias+act -> GEMM -> bias+dropout+residual+LN
-      bwd: bdaln bwd -> GEMM + wgrad -> bias+act bwd (bias grad folded in) -> wgrad ->
-           GEMM with the residual grad accumulated in its epilogue
+           split-K wgrad -> GEMM with the residual grad added in its epilogue
+  FFN sublayer:       y = LN(x + dropout(gelu(x W1^T + b1) W2^T + b2))
+      fwd: GEMM+bias+GELU (stores h and gelu(h)) -> GEMM -> bias+dropout+residual+LN
+      bwd: bdaln bwd -> GEMM with dGELU(h) epilogue + bias-grad partials -> wgrads ->
+           GEMM with the residual grad added in its epilogue
 
 The numerics are those of the unfused composition in apex.ops.fused (tests compare them).
 """
@@ -25,6 +25,7 @@ import math
 import torch
 
 from .. import _ext
+from . import gemm as G
 from .fused import ACT_GELU, _2d, _seed, _wgrad
 
 
@@ -36,12 +37,12 @@ class _AttnSublayer(torch.autograd.Function):
         d = E // heads
         scale = 1.0 / math.sqrt(d)
         x2 = _2d(x)
-        qkv = torch.addmm(bqkv, x2, wqkv.t()) if bqkv is not None else torch.mm(x2, wqkv.t())
+        qkv = G.linear(x2, wqkv, bqkv)
         q, k, v = qkv.view(B, S, 3, heads, d).unbind(2)
         sa, oa = _seed() if p_attn > 0 else (0, 0)
         o, lse, dmask = C.flash_attn_fwd(q, k, v, bool(causal), scale, float(p_attn), sa, oa, k_lens)
         o2 = o.view(B * S, E)
-        t = torch.mm(o2, wo.t())
+        t = G.linear(o2, wo)
         sh, oh = _seed() if p_hidden > 0 else (0, 0)
         y, s, mean, rstd = C.bdaln_fwd(t, bo, x2.contiguous(), gamma, beta, float(eps), float(p_hidden), sh, oh)
         ctx.save_for_backward(x2, wqkv, qkv, o, lse, k_lens, dmask, wo, s, gamma, mean, rstd)
@@ -55,16 +56,16 @@ class _AttnSublayer(torch.autograd.Function):
         x2, wqkv, qkv, o, lse, k_lens, dmask, wo, s, gamma, mean, rstd = ctx.saved_tensors
         B, S, E, heads, d, scale, causal, p_attn, sa, oa, p_hidden, sh, oh, has_bqkv, has_bo, bdt = ctx.cfg
         dres, dt, dgamma, dbeta, dbo = C.bdaln_bwd(_2d(dy), s, gamma, mean, rstd, float(p_hidden), sh, oh, has_bo)
+        dctx = G.dgrad(dt, wo).view(B, S, heads, d)
         dwo = _wgrad(dt, o.view(B * S, E))
-        dctx = torch.mm(dt, wo).view(B, S, heads, d)
         q, k, v = qkv.view(B, S, 3, heads, d).unbind(2)
         dqkv = torch.empty_like(qkv)
         dq, dk, dv = dqkv.view(B, S, 3, heads, d).unbind(2)
         C.flash_attn_bwd(dctx, q, k, v, o, lse, dq, dk, dv, bool(causal), scale, float(p_attn), sa, oa, k_lens,
                          dmask)
         dbqkv = C.colsum(dqkv, bdt) if has_bqkv else None
+        dx = G.dgrad_resid(dqkv, wqkv, dres)  # residual grad accumulated in the GEMM epilogue
         dwqkv = _wgrad(dqkv, x2)
-        dx = torch.addmm(dres, dqkv, wqkv)  # residual grad accumulated in the GEMM epilogue
         return (dx.view(B, S, E), dwqkv, dbqkv, dwo, dbo if has_bo else None, dgamma, dbeta,
                 None, None, None, None, None, None)
 
@@ -74,28 +75,35 @@ class _FFNSublayer(torch.autograd.Function):
     def forward(ctx, x, w1, b1, w2, b2, gamma, beta, p, eps, act):
         C = _ext.require()
         x2 = _2d(x)
-        h = torch.mm(x2, w1.t())
-        g = C.bias_act_fwd(h, b1, act)
-        t = torch.mm(g, w2.t())
+        if act == ACT_GELU and b1 is not None:
+            g, h = G.linear_gelu(x2, w1, b1)  # h = x W1^T + b1 (pre-activation), g = gelu(h)
+            hb = None
+        else:
+            h = torch.mm(x2, w1.t())
+            g = C.bias_act_fwd(h, b1, act)
+            hb = b1
+        t = G.linear(g, w2)
         seed, off = _seed() if p > 0 else (0, 0)
         y, s, mean, rstd = C.bdaln_fwd(t, b2, x2.contiguous(), gamma, beta, float(eps), float(p), seed, off)
-        ctx.save_for_backward(x2, w1, b1, h, g, w2, s, gamma, mean, rstd)
-        ctx.cfg = (p, seed, off, act, b2 is not None)
+        ctx.save_for_backward(x2, w1, hb, h, g, w2, s, gamma, mean, rstd)
+        ctx.cfg = (p, seed, off, act, b2 is not None, b1.dtype if b1 is not None else None)
         return y.view_as(x)
 
     @staticmethod
     def backward(ctx, dy):
         C = _ext.require()
-        x2, w1, b1, h, g, w2, s, gamma, mean, rstd = ctx.saved_tensors
-        p, seed, off, act, has_b2 = ctx.cfg
+        x2, w1, hb, h, g, w2, s, gamma, mean, rstd = ctx.saved_tensors
+        p, seed, off, act, has_b2, b1dt = ctx.cfg
         dres, dt, dgamma, dbeta, db2 = C.bdaln_bwd(_2d(dy), s, gamma, mean, rstd, float(p), seed, off, has_b2)
+        if hb is None and act == ACT_GELU and b1dt is not None:
+            dh, db1 = G.dgrad_dgelu(dt, w2, h, b1dt)  # (dt W2) * gelu'(h) and its column sums
+        else:
+            dh, db1 = C.bias_act_bwd(G.dgrad(dt, w2), h, hb, act)
         dw2 = _wgrad(dt, g)
-        dg = torch.mm(dt, w2)
-        dh, db1 = C.bias_act_bwd(dg, h, b1, act)
+        dx = G.dgrad_resid(dh, w1, dres)  # residual grad accumulated in the GEMM epilogue
         dw1 = _wgrad(dh, x2)
-        dx = torch.addmm(dres, dh, w1)  # residual grad accumulated in the GEMM epilogue
-        return (dx.view_as(dy), dw1, db1 if b1 is not None else None, dw2, db2 if has_b2 else None, dgamma, dbeta,
-                None, None, None)
+        return (dx.view_as(dy), dw1, db1 if b1dt is not None else None, dw2, db2 if has_b2 else None, dgamma,
+                dbeta, None, None, None)
 
 
 def _ok(x, *dims):

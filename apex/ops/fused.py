@@ -12,7 +12,8 @@ the PyTorch reference formulation on CPU (also the numerics reference for the te
   bias_dropout_add(x, b, res, p)            y = res + dropout(x + b)
   attention_qkv_packed / softmax_cross_entropy
 
-GEMMs are plain library GEMMs (hipBLASLt through torch); everything around them is ours.
+Forward and input-gradient GEMMs run on the hand-written MFMA kernel (apex.ops.gemm, with
+bias / bias+GELU in its epilogue where it applies); weight gradients are hipBLASLt with split-K.
 Dropout masks are regenerated from a Philox seed drawn from torch's CPU generator, so
 results are reproducible under ``torch.manual_seed`` and no mask tensor is stored.
 """
@@ -98,8 +99,10 @@ def softmax_cross_entropy(logits, labels, ignore_index=-100, smoothing=0.0, redu
 class _FusedDense(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b):
+        from . import gemm as G
+
         x2 = _2d(x)
-        y = torch.addmm(b, x2, w.t()) if b is not None else torch.mm(x2, w.t())
+        y = G.linear(x2, w, b)
         ctx.save_for_backward(x2, w)
         ctx.has_b = b is not None
         ctx.bdtype = b.dtype if b is not None else None
@@ -111,7 +114,9 @@ class _FusedDense(torch.autograd.Function):
         dy2 = _2d(dy).contiguous()
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = torch.mm(dy2, w).view(*dy.shape[:-1], w.shape[1])
+            from . import gemm as G
+
+            dx = G.dgrad(dy2, w).view(*dy.shape[:-1], w.shape[1])
         if ctx.needs_input_grad[1]:
             dw = _wgrad(dy2, x2)
         if ctx.has_b and ctx.needs_input_grad[2]:
@@ -128,20 +133,36 @@ def fused_dense(x, weight, bias=None):
 class _DenseAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, act):
+        from . import gemm as G
+
         C = _ext.require()
         x2 = _2d(x)
-        h = torch.mm(x2, w.t())
-        y = C.bias_act_fwd(h, b, act)
-        ctx.save_for_backward(x2, w, h, b)
+        if act == ACT_GELU and b is not None and G.use_mfma(x2, w) and b.dtype == x2.dtype:
+            # one MFMA GEMM with bias+GELU in the epilogue; h (with bias) kept for backward
+            y, h = G.linear_gelu(x2, w, b)
+            ctx.save_for_backward(x2, w, h, None)
+            ctx.bdtype = b.dtype
+        else:
+            h = torch.mm(x2, w.t())
+            y = C.bias_act_fwd(h, b, act)
+            ctx.save_for_backward(x2, w, h, b)
+            ctx.bdtype = None
         ctx.act = act
         return y.view(*x.shape[:-1], w.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
+        from . import gemm as G
+
         C = _ext.require()
         x2, w, h, b = ctx.saved_tensors
-        dh, db = C.bias_act_bwd(_2d(dy), h, b, ctx.act)
-        dx = torch.mm(dh, w).view(*dy.shape[:-1], w.shape[1]) if ctx.needs_input_grad[0] else None
+        if ctx.bdtype is not None:
+            dh, db = C.bias_act_bwd(_2d(dy), h, None, ctx.act)
+            db = C.colsum(dh, ctx.bdtype)
+            b = db
+        else:
+            dh, db = C.bias_act_bwd(_2d(dy), h, b, ctx.act)
+        dx = G.dgrad(dh, w).view(*dy.shape[:-1], w.shape[1]) if ctx.needs_input_grad[0] else None
         dw = _wgrad(dh, x2) if ctx.needs_input_grad[1] else None
         return dx, dw, (db if b is not None else None), None
 
@@ -199,9 +220,11 @@ def bias_gelu(h, bias):
 class _DenseBDALN(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, res, gamma, beta, p, eps):
+        from . import gemm as G
+
         C = _ext.require()
         x2 = _2d(x)
-        t = torch.mm(x2, w.t())
+        t = G.linear(x2, w)
         seed, off = _seed() if p > 0 else (0, 0)
         y, s, mean, rstd = C.bdaln_fwd(t, b, _2d(res).contiguous(), gamma, beta, float(eps), float(p),
                                        seed, off)
@@ -215,7 +238,9 @@ class _DenseBDALN(torch.autograd.Function):
         x2, w, s, gamma, mean, rstd = ctx.saved_tensors
         p, seed, off, has_b = ctx.cfg
         dres, dt, dg, dbeta, db = C.bdaln_bwd(_2d(dy), s, gamma, mean, rstd, float(p), seed, off, has_b)
-        dx = torch.mm(dt, w).view(*dy.shape[:-1], w.shape[1]) if ctx.needs_input_grad[0] else None
+        from . import gemm as G
+
+        dx = G.dgrad(dt, w).view(*dy.shape[:-1], w.shape[1]) if ctx.needs_input_grad[0] else None
         dw = _wgrad(dt, x2) if ctx.needs_input_grad[1] else None
         return dx, dw, (db if has_b else None), dres.view_as(dy), dg, dbeta, None, None
 

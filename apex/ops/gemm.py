@@ -1,0 +1,129 @@
+"""Dense-layer GEMMs on the hand-written MFMA kernel (csrc/gemm.hip) with fused epilogues.
+
+  linear(x, W, b)              y = x W^T (+ b)                      EPI_NONE / EPI_BIAS
+  linear_gelu(x, W, b)         h = x W^T + b, y = gelu(h) -> (y, h)  EPI_BIAS_GELU
+  dgrad(dy, W)                 dx = dy W        (via W^T, K-contiguous)
+  dgrad_resid(dy, W, r)        dx = dy W + r                         EPI_RESID
+  dgrad_dgelu(dy, W, h)        dh = (dy W) * gelu'(h), db = sum(dh)  EPI_DGELU
+
+The kernel takes both operands K-contiguous (A[M,K], B[N,K]); the input-gradient GEMMs use a
+transposed copy of W made by a HIP transpose kernel (cheap next to the GEMM: 2 bytes/weight
+each way). Weight gradients (contraction over tokens) stay on hipBLASLt with split-K
+(apex.ops.fused._wgrad).
+
+Policy (``APEX_GEMM``):
+  auto (default)  the MFMA kernel where its fused epilogue removes a separate [M, N] pass
+                  (bias+GELU, dGELU+bias-grad, residual add), the library GEMM for plain and
+                  bias-only products, where hipBLASLt's assembly main loop is faster than ours.
+                  Measured per call on MI355X, BERT-Large layer at M = 32768
+                  (tools/gemm_policy_bench.py, profiles/r1_gemm_policy.jsonl):
+                    library wins   qkv fwd 164 vs 177 us, attn-out fwd 56 vs 60, FFN2 fwd 180 vs 209,
+                                   attn-out dgrad 66 vs 66 (+ transpose)
+                    MFMA wins      FFN1 fwd+bias+GELU 299 vs 328 (mm + bias_act), FFN2 dgrad+dGELU
+                                   318 vs 402 (mm + bias_act_bwd), QKV dgrad+residual 171 vs 199
+                                   (addmm), FFN1 dgrad+residual 221 vs 242
+  mfma            every supported GEMM on the MFMA kernel (A/B and coverage runs)
+  blas            library GEMM + separate HIP epilogue kernels everywhere
+Each function falls back to the library path when the operands do not fit the MFMA kernel
+(K % 64, N % 8, dtype, alignment). Numerics follow the unfused composition: the GEMM result is
+rounded to the activation dtype before the bias/activation.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from .. import _ext
+
+_MODE = os.environ.get("APEX_GEMM", "auto")
+
+
+def _C():
+    return _ext.require()
+
+
+def _2d(x):
+    return x.reshape(-1, x.shape[-1])
+
+
+def use_mfma(a, w, fused=True) -> bool:
+    """MFMA kernel for this call? ``fused``: the call carries an epilogue the library lacks."""
+    if _MODE == "blas" or not a.is_cuda or (_MODE == "auto" and not fused):
+        return False
+    return _C().gemm_supported(a, w)
+
+
+def transpose(w):
+    """W^T contiguous (HIP transpose kernel for 16-bit dtypes)."""
+    if w.is_cuda and w.dtype in (torch.bfloat16, torch.float16) and w.dim() == 2:
+        return _C().transpose(w)
+    return w.t().contiguous()
+
+
+def linear(x, w, b=None):
+    """x [..., K] @ w[N, K]^T (+ b) in x's dtype."""
+    a = _2d(x)
+    if use_mfma(a, w, fused=False) and (b is None or b.dtype == x.dtype):
+        C = _C()
+        y, _ = C.gemm(a, w, C.EPI_BIAS if b is not None else C.EPI_NONE, b)
+    else:
+        y = torch.addmm(b, a, w.t()) if b is not None else torch.mm(a, w.t())
+    return y.view(*x.shape[:-1], w.shape[0])
+
+
+def linear_gelu(x, w, b):
+    """(gelu(h), h) with h = x w^T + b (erf GELU); h is kept for the backward."""
+    a = _2d(x)
+    if use_mfma(a, w) and b is not None and b.dtype == x.dtype:
+        C = _C()
+        y, h = C.gemm(a, w, C.EPI_BIAS_GELU, b)
+    else:
+        C = _C()
+        h = torch.mm(a, w.t())
+        y = C.bias_act_fwd(h, b, 0)
+        h = h + b if b is not None else h  # the pre-activation as the fused path stores it
+    shp = (*x.shape[:-1], w.shape[0])
+    return y.view(shp), h.view(shp)
+
+
+def dgrad(dy, w, wT=None):
+    """dy [..., N] @ w [N, K] -> [..., K]."""
+    a = _2d(dy)
+    if _MODE == "mfma" and a.is_cuda:
+        wT = transpose(w) if wT is None else wT
+        if use_mfma(a, wT, fused=False):
+            C = _C()
+            out, _ = C.gemm(a, wT, C.EPI_NONE)
+            return out.view(*dy.shape[:-1], w.shape[1])
+    return torch.mm(a, w).view(*dy.shape[:-1], w.shape[1])
+
+
+def dgrad_resid(dy, w, r, wT=None):
+    """dy @ w + r (the residual-branch gradient accumulated in the epilogue)."""
+    a = _2d(dy)
+    r2 = _2d(r)
+    if _MODE != "blas" and a.is_cuda and r2.is_contiguous() and r2.dtype == a.dtype:
+        wT = transpose(w) if wT is None else wT
+        if use_mfma(a, wT):
+            C = _C()
+            out, _ = C.gemm(a, wT, C.EPI_RESID, None, r2)
+            return out.view(*dy.shape[:-1], w.shape[1])
+    return torch.addmm(r2, a, w).view(*dy.shape[:-1], w.shape[1])
+
+
+def dgrad_dgelu(dy, w, h, bias_dtype, wT=None):
+    """(dh, db): dh = (dy @ w) * gelu'(h), db = column sums of dh (in bias_dtype)."""
+    a = _2d(dy)
+    h2 = _2d(h)
+    if _MODE != "blas" and a.is_cuda and h2.is_contiguous() and h2.dtype == a.dtype:
+        wT = transpose(w) if wT is None else wT
+        if use_mfma(a, wT):
+            C = _C()
+            dh, db = C.gemm(a, wT, C.EPI_DGELU, None, h2, bias_dtype)
+            return dh, db
+    C = _C()
+    dg = torch.mm(a, w)
+    dh, _ = C.bias_act_bwd(dg, h2, None, 0)
+    db = C.colsum(dh, bias_dtype) if bias_dtype is not None else None
+    return dh, db

@@ -747,6 +747,90 @@ Tensor k_input_normalize(Tensor x, std::vector<double> mean, std::vector<double>
   return y;
 }
 
+// ---------------------------------------------------------------------------
+// MFMA GEMM (gemm.hip): C = epi(A[M,K] . B[N,K]^T). Returns [C, H] (H: pre-activation for
+// EPI_BIAS_GELU) or [C, dbias] (EPI_DGELU). A may be any [..., K] view with a unit inner stride.
+// ---------------------------------------------------------------------------
+bool k_gemm_supported(Tensor a, Tensor b) {
+  if (!a.is_cuda() || a.dim() < 2 || b.dim() != 2 || a.scalar_type() != b.scalar_type()) return false;
+  if (a.scalar_type() != at::kBFloat16 && a.scalar_type() != at::kHalf) return false;
+  if (a.stride(-1) != 1 || b.stride(1) != 1) return false;
+  const int64_t K = a.size(-1), N = b.size(0);
+  const int64_t M = a.numel() / std::max<int64_t>(K, 1);
+  if (b.size(1) != K || M >= (1ll << 31) || N >= (1ll << 31)) return false;
+  // rows of A must be evenly strided when A is viewed as [M, K]
+  if (a.dim() > 2 && !a.is_contiguous()) return false;
+  const int64_t lda = a.dim() == 2 ? a.stride(0) : K;
+  auto al = [](const Tensor& t) { return reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0; };
+  return al(a) && al(b) && apex::gemm_supported((int)M, (int)N, (int)K, lda, b.stride(0), N);
+}
+
+std::vector<Tensor> k_gemm(Tensor a, Tensor b, int64_t epi, const c10::optional<Tensor>& bias,
+                           const c10::optional<Tensor>& aux, c10::optional<at::ScalarType> bias_grad_dtype,
+                           int64_t variant) {
+  TORCH_CHECK(k_gemm_supported(a, b), "gemm: unsupported operands (bf16/fp16, K % 64 == 0, N % 8 == 0, "
+              "16-byte aligned, unit inner stride)");
+  const int64_t K = a.size(-1), N = b.size(0), M = a.numel() / K;
+  const int64_t lda = a.dim() == 2 ? a.stride(0) : K;
+  std::vector<int64_t> osz(a.sizes().begin(), a.sizes().end());
+  osz.back() = N;
+  Tensor c = at::empty(osz, a.options());
+  apex::GemmArgs g{};
+  g.A = a.data_ptr();
+  g.B = b.data_ptr();
+  g.C = c.data_ptr();
+  g.M = (int)M;
+  g.N = (int)N;
+  g.K = (int)K;
+  g.lda = lda;
+  g.ldb = b.stride(0);
+  g.ldc = N;
+  g.epi = (int)epi;
+  g.variant = (int)variant;
+  Tensor extra;
+  if (epi == apex::EPI_BIAS || epi == apex::EPI_BIAS_GELU) {
+    TORCH_CHECK(bias.has_value() && bias->defined() && bias->is_contiguous() && bias->numel() == N &&
+                    bias->scalar_type() == a.scalar_type(),
+                "gemm: bias must be a contiguous [N] tensor of the operand dtype");
+    g.bias = bias->data_ptr();
+  }
+  if (epi == apex::EPI_BIAS_GELU) {
+    extra = at::empty(osz, a.options());
+    g.aux_out = extra.data_ptr();
+  }
+  Tensor part;
+  if (epi == apex::EPI_DGELU || epi == apex::EPI_RESID) {
+    TORCH_CHECK(aux.has_value() && aux->defined() && aux->scalar_type() == a.scalar_type() &&
+                    aux->numel() == M * N && aux->stride(-1) == 1 && aux->is_contiguous(),
+                "gemm: aux must be a contiguous [M, N] tensor of the operand dtype");
+    g.aux = aux->data_ptr();
+    g.ldaux = N;
+  }
+  if (epi == apex::EPI_DGELU) {
+    part = at::empty({apex::gemm_part_rows((int)M), N}, a.options().dtype(at::kFloat));
+    g.part = part.data_ptr<float>();
+  }
+  check(apex::gemm_nt(g, dt_code(a.scalar_type()), cur_stream()), "gemm");
+  if (epi == apex::EPI_DGELU && bias_grad_dtype.has_value()) {
+    extra = at::empty({N}, a.options().dtype(*bias_grad_dtype));
+    check(apex::gemm_bias_grad(part.data_ptr<float>(), (int)part.size(0), (int)N, extra.data_ptr(),
+                               dt_code(*bias_grad_dtype), cur_stream()),
+          "gemm_bias_grad");
+  }
+  return {c, extra};
+}
+
+Tensor k_transpose(Tensor x) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 2, "transpose: 2-D device tensor");
+  Tensor xc = x.contiguous();
+  if (reinterpret_cast<uintptr_t>(xc.data_ptr()) % 16 != 0) xc = xc.clone();
+  Tensor out = at::empty({xc.size(1), xc.size(0)}, xc.options());
+  check(apex::transpose_2d(xc.data_ptr(), out.data_ptr(), (int)xc.size(0), (int)xc.size(1),
+                           dt_code(xc.scalar_type()), cur_stream()),
+        "transpose");
+  return out;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -798,4 +882,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bdaln_fwd", &k_bdaln_fwd);
   m.def("bdaln_bwd", &k_bdaln_bwd);
   m.def("input_normalize", &k_input_normalize);
+  m.def("gemm_supported", &k_gemm_supported);
+  m.def("gemm", &k_gemm, py::arg("a"), py::arg("b"), py::arg("epi") = 0, py::arg("bias") = py::none(),
+        py::arg("aux") = py::none(), py::arg("bias_grad_dtype") = py::none(), py::arg("variant") = 0);
+  m.def("transpose", &k_transpose);
+  m.attr("EPI_NONE") = (int)apex::EPI_NONE;
+  m.attr("EPI_BIAS") = (int)apex::EPI_BIAS;
+  m.attr("EPI_BIAS_GELU") = (int)apex::EPI_BIAS_GELU;
+  m.attr("EPI_DGELU") = (int)apex::EPI_DGELU;
+  m.attr("EPI_RESID") = (int)apex::EPI_RESID;
 }

@@ -1,0 +1,610 @@
+// Hand-written MFMA GEMM for gfx950 with fused epilogues (the transformer dense layers).
+//
+//   C[M,N] = epilogue( A[M,K] . B[N,K]^T )      A, B, C row-major, bf16 or fp16, fp32 accumulate
+//
+// Both operands are K-contiguous ("NT"): the forward projections (X . W^T) directly, and the
+// input-gradient GEMMs (dY . W) through a transposed copy of W (transpose_2d below).
+// Weight gradients (contraction over tokens) stay on hipBLASLt with split-K (fused.py).
+//
+// Epilogues (fused into the tile write, so the activation never makes an extra HBM round
+// trip — the separate bias/GELU/residual kernels they replace each read+wrote [M,N]):
+//   EPI_NONE      C = acc
+//   EPI_BIAS      C = acc + bias[n]
+//   EPI_BIAS_GELU H = acc + bias[n] (pre-activation, kept for backward), C = gelu(H)
+//   EPI_DGELU     C = acc * gelu'(H[m,n])   and per-(256-row tile, wave row) column partial sums
+//                 of C written to `part` (the bias gradient, finished by partial_colsum)
+//   EPI_RESID     C = acc + R[m,n]          (residual-gradient accumulation)
+//
+// Tiling (CDNA4, cdna_hip_programming.md §5):
+//  * 256x256 output tile, BK = 64, 512 threads = 8 waves as 2 (M) x 4 (N); each wave owns a
+//    128 x 64 sub-tile = 8 x 4 fragments of v_mfma_f32_16x16x32 (128 fp32 accumulators/lane).
+//  * The MFMA is issued "swapped" (A-operand = B rows, B-operand = A rows) so each lane ends
+//    with 4 consecutive N-columns of one M-row: 8-byte vector epilogue loads/stores.
+//  * Global -> LDS by global_load_lds_dwordx4 (16 B per lane, no VGPR round trip), double
+//    buffered (2 x 64 KB), the next K-tile in flight across the barrier (counted vmcnt, raw
+//    s_barrier — never __syncthreads(), whose fence would drain the prefetch).
+//  * LDS image: 128-byte rows (64 bf16 of K), 16-byte chunk c of row r stored at chunk
+//    c ^ ((r >> 1) & 7). glds writes lane-linear, so the XOR is applied to the per-lane SOURCE
+//    address and again on the ds_read_b128: every 16-lane ds_read_b128 group then touches 16
+//    distinct 16-B slots of the 256-B bank row (conflict-free).
+//  * blockIdx -> tile: bijective XCD remap (each XCD gets a contiguous tile range) then
+//    GROUP_M=8 panel ordering, so concurrently running tiles on one XCD share A/B panels in L2.
+#include "common.h"
+#include "kernels.h"
+
+#include <type_traits>
+
+namespace apex {
+namespace {
+
+constexpr int GB_M = 256, GB_N = 256, GB_K = 64, G_THREADS = 512, G_GROUP_M = 8;
+constexpr int G_TILE_BYTES = GB_M * GB_K * 2;       // one operand tile: 32 KB
+constexpr int G_BUF_BYTES = 2 * G_TILE_BYTES;       // A + B: 64 KB
+constexpr int G_LDS_BYTES = 2 * G_BUF_BYTES;        // double buffered: 128 KB
+
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <typename T> __device__ __forceinline__ f32x4 mfma16(const s16x8& a, const s16x8& b, const f32x4& c);
+template <> __device__ __forceinline__ f32x4 mfma16<bf16>(const s16x8& a, const s16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+template <> __device__ __forceinline__ f32x4 mfma16<f16>(const s16x8& a, const s16x8& b, const f32x4& c) {
+  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16((h8)a, (h8)b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void glds16(const void* g, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+// Branch-free erf (Abramowitz & Stegun 7.1.26, |error| <= 1.5e-7): one v_rcp, one v_exp and
+// seven FMAs instead of ocml's erff (whose inlined branches made the epilogue 10x larger).
+__device__ __forceinline__ float erf_fast(float x, float e_neg_x2) {
+  const float ax = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, ax, 1.f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float r = fmaf(-p * t, e_neg_x2, 1.f);
+  return copysignf(r, x);
+}
+// exp(-x^2/2) via v_exp_f32 (2^y)
+__device__ __forceinline__ float exp_neg_half_sq(float x) { return __builtin_amdgcn_exp2f(-0.72134752044448170f * x * x); }
+__device__ __forceinline__ float gelu_f(float x) {
+  return 0.5f * x * (1.f + erf_fast(x * 0.70710678118654752f, exp_neg_half_sq(x)));
+}
+__device__ __forceinline__ float gelu_grad_f(float x) {
+  const float e = exp_neg_half_sq(x);
+  const float cdf = 0.5f * (1.f + erf_fast(x * 0.70710678118654752f, e));
+  return fmaf(x * 0.39894228040143268f, e, cdf);
+}
+
+template <typename T>
+__device__ __forceinline__ void load4(const T* p, float (&v)[4]) {
+  Pack<T, 4> pk = *reinterpret_cast<const Pack<T, 4>*>(p);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = to_f(pk.v[i]);
+}
+template <typename T>
+__device__ __forceinline__ void store4(T* p, const float (&v)[4]) {
+  Pack<T, 4> pk;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) pk.v[i] = from_f<T>(v[i]);
+  *reinterpret_cast<Pack<T, 4>*>(p) = pk;
+}
+
+__device__ __forceinline__ s16x8 lds_frag(const char* tile, int r, int c) {
+  return *reinterpret_cast<const s16x8*>(tile + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+}
+
+__device__ __forceinline__ void bar() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// One operand K-tile = 32 glds pieces (8 rows x 128 B); wave `wid` owns pieces wid*4 .. wid*4+3.
+// stage_pieces issues pieces [p0, p0+2) of the wave's four.
+template <typename T>
+__device__ __forceinline__ void stage_pieces(const T* __restrict__ g, int64_t ld, int row0, int rows, int k0,
+                                             char* lds_tile, int wid, int lane, int p0) {
+#pragma unroll
+  for (int j = p0; j < p0 + 2; ++j) {
+    const int piece = wid * 4 + j;
+    const int r = piece * 8 + (lane >> 3);
+    const int chunk = (lane & 7) ^ ((r >> 1) & 7);
+    int gr = row0 + r;
+    gr = gr < rows ? gr : rows - 1;
+    glds16(g + (int64_t)gr * ld + k0 + chunk * 8, lds_tile + piece * 1024);
+  }
+}
+
+// Main loop schedule ("ping-pong", cdna_hip_programming.md §5 256² template, own phase plan):
+// the 8 waves form two groups by M half (wr); group 1 runs one barrier behind group 0, so in
+// every barrier interval one group issues its 16 MFMAs while the other issues its LDS reads
+// and global->LDS copies on the same SIMDs. Per K-tile and wave, four phases, each
+//   R: ds_read subtile, 2 glds pieces, [vmcnt], lgkmcnt(0)  | barrier
+//   M: 16 x mfma_16x16x32 (one 64x32 quadrant, K = 64)      | barrier
+//     p1  R: A rows mh=0 (8 frags) + B cols nh=0 (4)   stage A(t+1) pieces 0,1 -> other buffer
+//     p2  R: B cols nh=1 (4)                           stage A(t+1) pieces 2,3
+//     p3  R: A rows mh=1 (8)                           stage B(t+2) pieces 0,1 -> this buffer
+//     p4  R: -                                         stage B(t+2) pieces 2,3; vmcnt(4)
+//     quadrants (mh,nh): p1 (0,0)  p2 (0,1)  p3 (1,1)  p4 (1,0)
+// WAR: B of this buffer is last read in p2 and A in p3; lgkmcnt(0) before each barrier retires
+// the reads, so restaging one phase later (B(t+2) in p3) is safe; A(t+1) goes to the buffer whose
+// A was last read in the previous tile's p3. RAW: vmcnt(4) in p4 retires everything but B(t+2)
+// (i.e. A(t+1), B(t+1)) before the barrier that precedes the next tile's first read.
+template <typename T>
+__device__ __forceinline__ void mainloop_bk64(const T* __restrict__ A, const T* __restrict__ B, int M, int N, int K,
+                                              int64_t lda, int64_t ldb, int m0, int n0, char* smem, int wid, int wr,
+                                              int wc, int lane, f32x4 (&acc)[4][8]) {
+  const int nt = K / GB_K;
+  const int lr = lane & 15, lk = lane >> 4;
+  // prologue: A(0), B(0) -> buf0, B(1) -> buf1; retire tile 0
+  stage_pieces<T>(A, lda, m0, M, 0, smem, wid, lane, 0);
+  stage_pieces<T>(A, lda, m0, M, 0, smem, wid, lane, 2);
+  stage_pieces<T>(B, ldb, n0, N, 0, smem + G_TILE_BYTES, wid, lane, 0);
+  stage_pieces<T>(B, ldb, n0, N, 0, smem + G_TILE_BYTES, wid, lane, 2);
+  if (nt > 1) {
+    stage_pieces<T>(B, ldb, n0, N, GB_K, smem + G_BUF_BYTES + G_TILE_BYTES, wid, lane, 0);
+    stage_pieces<T>(B, ldb, n0, N, GB_K, smem + G_BUF_BYTES + G_TILE_BYTES, wid, lane, 2);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  bar();
+  if (wr == 1) bar();  // stagger group 1 by one barrier
+
+  s16x8 fa[4][2], fb0[2][2], fb1[2][2];
+  for (int t = 0; t < nt; ++t) {
+    char* cur = smem + (t & 1) * G_BUF_BYTES;
+    char* oth = smem + ((t + 1) & 1) * G_BUF_BYTES;
+    const char* ta = cur;
+    const char* tb = cur + G_TILE_BYTES;
+    const bool ld_a = t + 1 < nt, ld_b = t + 2 < nt;
+    // ---------------- p1: A mh=0, B nh=0; stage A(t+1) pieces 0,1 ----------------
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) fb0[j][s] = lds_frag(tb, wc * 64 + j * 16 + lr, s * 4 + lk);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) fa[i][s] = lds_frag(ta, wr * 128 + i * 16 + lr, s * 4 + lk);
+    if (ld_a) stage_pieces<T>(A, lda, m0, M, (t + 1) * GB_K, oth, wid, lane, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[j][i] = mfma16<T>(fb0[j][s], fa[i][s], acc[j][i]);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+    // ---------------- p2: B nh=1; stage A(t+1) pieces 2,3 ----------------
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) fb1[j][s] = lds_frag(tb, wc * 64 + 32 + j * 16 + lr, s * 4 + lk);
+    if (ld_a) stage_pieces<T>(A, lda, m0, M, (t + 1) * GB_K, oth, wid, lane, 2);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[2 + j][i] = mfma16<T>(fb1[j][s], fa[i][s], acc[2 + j][i]);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+    // ---------------- p3: A mh=1; stage B(t+2) pieces 0,1 into this buffer ----------------
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) fa[i][s] = lds_frag(ta, wr * 128 + 64 + i * 16 + lr, s * 4 + lk);
+    if (ld_b) stage_pieces<T>(B, ldb, n0, N, (t + 2) * GB_K, cur + G_TILE_BYTES, wid, lane, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[2 + j][4 + i] = mfma16<T>(fb1[j][s], fa[i][s], acc[2 + j][4 + i]);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+    // ---------------- p4: stage B(t+2) pieces 2,3; retire A(t+1), B(t+1) ----------------
+    if (ld_b) {
+      stage_pieces<T>(B, ldb, n0, N, (t + 2) * GB_K, cur + G_TILE_BYTES, wid, lane, 2);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    bar();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[j][4 + i] = mfma16<T>(fb0[j][s], fa[i][s], acc[j][4 + i]);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+  }
+}
+
+// BK = 32 variant: four 32 KB LDS buffers (A 256x32 + B 256x32 each, 64-B rows), ONE phase per
+// K-tile: R = 12 ds_read_b128 (8 A + 4 B fragments) | barrier | M = 32 MFMAs with the 4 glds pieces
+// of tile t+3 issued among them, then vmcnt retiring tile t+1 | barrier. Half the barriers of the
+// BK=64 4-phase loop per K element, and loads run 3 tiles ahead (2 sections of slack + one tile).
+// LDS image: 16-B chunk c of row r at chunk c ^ f((r >> 2) & 3), f = {0,2,3,1}: every 16-lane
+// ds_read_b128 group (rows r..r+15, chunks lk / lk+1) hits 16 distinct slots of the bank row.
+__device__ __forceinline__ int swz32(int r) { return (0x78 >> (((r >> 2) & 3) * 2)) & 3; }
+
+template <typename T>
+__device__ __forceinline__ void stage32(const T* __restrict__ g, int64_t ld, int row0, int rows, int k0,
+                                        char* lds_tile, int wid, int lane) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int piece = wid * 2 + j;  // 16 pieces of 16 rows x 64 B per operand tile
+    const int r = piece * 16 + (lane >> 2);
+    const int chunk = (lane & 3) ^ swz32(r);
+    int gr = row0 + r;
+    gr = gr < rows ? gr : rows - 1;
+    glds16(g + (int64_t)gr * ld + k0 + chunk * 8, lds_tile + piece * 1024);
+  }
+}
+
+__device__ __forceinline__ s16x8 lds_frag32(const char* tile, int r, int c) {
+  return *reinterpret_cast<const s16x8*>(tile + r * 64 + ((c ^ swz32(r)) << 4));
+}
+
+template <typename T>
+__device__ __forceinline__ void mainloop_bk32(const T* __restrict__ A, const T* __restrict__ B, int M, int N, int K,
+                                              int64_t lda, int64_t ldb, int m0, int n0, char* smem, int wid, int wr,
+                                              int wc, int lane, f32x4 (&acc)[4][8]) {
+  constexpr int BK = 32, TB = 256 * BK * 2, BUF = 2 * TB;
+  const int nt = K / BK;
+  const int lr = lane & 15, lk = lane >> 4;
+  // prologue: tiles 0, 1, 2 in flight, tile 0 retired
+#pragma unroll
+  for (int p = 0; p < 3; ++p) {
+    if (p < nt) {
+      stage32<T>(A, lda, m0, M, p * BK, smem + p * BUF, wid, lane);
+      stage32<T>(B, ldb, n0, N, p * BK, smem + p * BUF + TB, wid, lane);
+    }
+  }
+  if (nt >= 3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (nt == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  bar();
+  if (wr == 1) bar();  // stagger group 1 by one barrier
+
+  s16x8 fa[8], fb[4];
+  for (int t = 0; t < nt; ++t) {
+    const char* ta = smem + (t & 3) * BUF;
+    const char* tb = ta + TB;
+    // ---- R: fragments of tile t ----
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fb[j] = lds_frag32(tb, wc * 64 + j * 16 + lr, lk);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) fa[i] = lds_frag32(ta, wr * 128 + i * 16 + lr, lk);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar();
+    // ---- M: 32 MFMAs; tile t+3 -> buffer (t+3)&3 (= (t-1)&3, last read one section ago) ----
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[j][i] = mfma16<T>(fb[j], fa[i], acc[j][i]);
+    __builtin_amdgcn_s_setprio(0);
+    if (t + 3 < nt) {
+      char* nb = smem + ((t + 3) & 3) * BUF;
+      stage32<T>(A, lda, m0, M, (t + 3) * BK, nb, wid, lane);
+      stage32<T>(B, ldb, n0, N, (t + 3) * BK, nb + TB, wid, lane);
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int j = 2; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[j][i] = mfma16<T>(fb[j], fa[i], acc[j][i]);
+    __builtin_amdgcn_s_setprio(0);
+    // retire tile t+1 (younger in flight: t+2, t+3 when they exist)
+    const int younger = min(nt - 1, t + 3) - (t + 1);
+    if (younger >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+  }
+}
+
+template <typename T, int EPI, int VAR>
+__global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(const T* __restrict__ A, const T* __restrict__ B,
+                                                            T* __restrict__ C, int M, int N, int K, int64_t lda,
+                                                            int64_t ldb, int64_t ldc, const T* __restrict__ bias,
+                                                            const T* __restrict__ aux, int64_t ldaux,
+                                                            T* __restrict__ aux_out, float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) char smem[G_LDS_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+  const int lr = lane & 15, lk = lane >> 4;
+
+  // ---- tile mapping: bijective XCD remap, then GROUP_M panel order ----
+  const int tiles_m = (M + GB_M - 1) / GB_M, tiles_n = (N + GB_N - 1) / GB_N;
+  const int nwg = tiles_m * tiles_n;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
+  const int wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  const int group = G_GROUP_M * tiles_n;
+  const int first_m = (wg / group) * G_GROUP_M;
+  const int gm = min(tiles_m - first_m, G_GROUP_M);
+  const int tm = first_m + (wg % group) % gm;
+  const int tn = (wg % group) / gm;
+  const int m0 = tm * GB_M, n0 = tn * GB_N;
+
+  f32x4 acc[4][8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if constexpr (VAR == 0)
+    mainloop_bk64<T>(A, B, M, N, K, lda, ldb, m0, n0, smem, wid, wr, wc, lane, acc);
+  else
+    mainloop_bk32<T>(A, B, M, N, K, lda, ldb, m0, n0, smem, wid, wr, wc, lane, acc);
+  if (wr == 0) bar();  // re-align the groups
+  bar();               // every wave is past its last ds_read: LDS is free for the epilogue
+
+  // ---- epilogue ----
+  // acc[j][i] holds rows wr*128 + i*16 + lr, cols wc*64 + j*16 + 4*lk .. +3 of the tile. The fp32
+  // accumulators are rounded to T and transposed through the wave's own 16 KB LDS region
+  // ([128 rows][64 cols], 16-B chunks XOR-swizzled by row, 8-B halves swapped on rows 8..15 of every
+  // 16 so the ds_write_b64 groups are conflict-free); then every lane owns 8 consecutive columns of
+  // 16 rows, and the epilogue math (bias, GELU, dGELU, residual) runs on 16-byte vectors with
+  // 16-byte loads/stores (8 lanes = one 128-B row run). Rounding before the bias matches the unfused
+  // composition (GEMM output in T, then the bias/activation kernel in fp32).
+  // All LDS reads are issued before the first global access (hipcc drains vmcnt before an LDS access
+  // while VMEM ops are pending), and the interior tiles take a branch-free path (a per-element
+  // guarded load makes hipcc wait vmcnt(0) per element).
+  char* reg = smem + wid * 16384;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int row = i * 16 + lr;
+      const int chunk = (2 * j + (lk >> 1)) ^ (row & 7);
+      const int half = (lk & 1) ^ ((row >> 3) & 1);
+      Pack<T, 4> pk;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) pk.v[e] = from_f<T>(acc[j][i][e]);
+      *reinterpret_cast<Pack<T, 4>*>(reg + row * 128 + chunk * 16 + half * 8) = pk;
+    }
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+  u32x4 rc[16];
+#pragma unroll
+  for (int it = 0; it < 16; ++it) {
+    const int row = it * 8 + (lane >> 3), c = lane & 7;
+    u32x4 x = *reinterpret_cast<const u32x4*>(reg + row * 128 + ((c ^ (row & 7)) << 4));
+    if ((row >> 3) & 1) x = u32x4{x[2], x[3], x[0], x[1]};
+    rc[it] = x;
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+
+  const int ncol = n0 + wc * 64 + (lane & 7) * 8;
+  const int mrow = m0 + wr * 128 + (lane >> 3);
+  const bool full = m0 + GB_M <= M && n0 + GB_N <= N;
+  auto unpack = [&](const u32x4& x, float (&v)[8]) {
+    Pack<T, 8> pk = *reinterpret_cast<const Pack<T, 8>*>(&x);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = to_f(pk.v[e]);
+  };
+  auto pack = [&](const float (&v)[8]) {
+    Pack<T, 8> pk;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) pk.v[e] = from_f<T>(v[e]);
+    return *reinterpret_cast<const u32x4*>(&pk);
+  };
+  // guarded 16-byte access for edge tiles (N % 8 == 4 leaves a 4-column tail)
+  auto ld16 = [&](const T* base, int64_t ld, int m) -> u32x4 {
+    // branch-free: clamp the address into the tensor, then shift/mask the 4-column tail
+    const int mc = m < M ? m : M - 1;
+    const int nc = ncol + 8 <= N ? ncol : (N >= 8 ? N - 8 : 0);
+    u32x4 r = *reinterpret_cast<const u32x4*>(base + (int64_t)mc * ld + nc);
+    if (nc != ncol) r = u32x4{r[2], r[3], 0u, 0u};
+    return r;
+  };
+  auto st16 = [&](T* base, int m, const u32x4& x) {
+    if (m < M && ncol < N) {
+      T* p = base + (int64_t)m * ldc + ncol;
+      if (ncol + 8 <= N) *reinterpret_cast<u32x4*>(p) = x;
+      else *reinterpret_cast<u32x2*>(p) = u32x2{x[0], x[1]};
+    }
+  };
+
+  auto body = [&](auto full_tag) {
+    constexpr bool F = decltype(full_tag)::value;
+    float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
+      u32x4 braw;
+      if constexpr (F) braw = *reinterpret_cast<const u32x4*>(bias + ncol);
+      else braw = ld16(bias, 0, 0);  // (bias is [N]: row 0 of a 1-row tensor)
+      unpack(braw, bv);
+    }
+    u32x4 ra[16];
+    if constexpr (EPI == EPI_DGELU || EPI == EPI_RESID) {
+#pragma unroll
+      for (int it = 0; it < 16; ++it) {
+        const int m = mrow + it * 8;
+        if constexpr (F) ra[it] = *reinterpret_cast<const u32x4*>(aux + (int64_t)m * ldaux + ncol);
+        else ra[it] = ld16(aux, ldaux, m);
+      }
+    }
+    float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      const int m = mrow + it * 8;
+      u32x4 out = rc[it];
+      if constexpr (EPI != EPI_NONE) {
+        float v[8];
+        unpack(rc[it], v);
+        if constexpr (EPI == EPI_BIAS) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += bv[e];
+        } else if constexpr (EPI == EPI_BIAS_GELU) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += bv[e];
+          const u32x4 hraw = pack(v);
+          if constexpr (F) *reinterpret_cast<u32x4*>(aux_out + (int64_t)m * ldc + ncol) = hraw;
+          else st16(aux_out, m, hraw);
+          unpack(hraw, v);  // GELU of the stored pre-activation
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = gelu_f(v[e]);
+        } else {
+          float x[8];
+          unpack(ra[it], x);
+          const bool ok = F || (m < M && ncol < N);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            if constexpr (EPI == EPI_DGELU) {
+              v[e] = ok ? v[e] * gelu_grad_f(x[e]) : 0.f;
+            } else {
+              v[e] += x[e];
+            }
+          }
+        }
+        out = pack(v);
+        if constexpr (EPI == EPI_DGELU) {
+          float r[8];
+          unpack(out, r);  // the bias grad sums the stored (rounded) values
+#pragma unroll
+          for (int e = 0; e < 8; ++e) csum[e] += r[e];
+        }
+      }
+      if constexpr (F) *reinterpret_cast<u32x4*>(C + (int64_t)m * ldc + ncol) = out;
+      else st16(C, m, out);
+    }
+    if constexpr (EPI == EPI_DGELU) {
+      // lanes l, l^8, l^16, ... share the column chunk: reduce over the wave's 8 row slots
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float x = csum[e];
+        x += __shfl_xor(x, 8, 64);
+        x += __shfl_xor(x, 16, 64);
+        x += __shfl_xor(x, 32, 64);
+        csum[e] = x;
+      }
+      // waves wc = 0..3 of one wr cover disjoint columns: one partial row per (tile, wr)
+      if (lane < 8 && ncol < N) {
+        float* pp = part + (int64_t)(tm * 2 + wr) * N + ncol;
+        *reinterpret_cast<f32x4*>(pp) = f32x4{csum[0], csum[1], csum[2], csum[3]};
+        if (ncol + 8 <= N) *reinterpret_cast<f32x4*>(pp + 4) = f32x4{csum[4], csum[5], csum[6], csum[7]};
+      }
+    }
+  };
+  if (full) body(std::integral_constant<bool, true>{});
+  else body(std::integral_constant<bool, false>{});
+}
+
+// 2-D transpose out[C][R] = in[R][C] (16-bit elements). Each lane transposes an 8x8 block in
+// registers: 8 x 16-B row loads, 8 x 16-B row stores. A wave is 8 (along C) x 8 (along R) blocks,
+// so every load and every store instruction moves whole 128-B row runs. Edge blocks fall back to
+// element-wise accesses.
+template <typename T>
+__global__ void __launch_bounds__(256) transpose_kernel(const T* __restrict__ in, T* __restrict__ out, int R, int Cc) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int bc = lane & 7, br = lane >> 3;
+  // block tile = 64 (C) x 256 (R) per workgroup: 4 waves along R
+  const int c0 = blockIdx.x * 64 + bc * 8;
+  const int r0 = blockIdx.y * 256 + wid * 64 + br * 8;
+  if (c0 + 8 <= Cc && r0 + 8 <= R && (Cc % 8) == 0 && (R % 8) == 0) {
+    s16x8 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const s16x8*>(in + (int64_t)(r0 + k) * Cc + c0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      s16x8 o;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = v[k][i];
+      *reinterpret_cast<s16x8*>(out + (int64_t)(c0 + i) * R + r0) = o;
+    }
+  } else {
+    for (int k = 0; k < 8; ++k)
+      for (int i = 0; i < 8; ++i)
+        if (r0 + k < R && c0 + i < Cc) out[(int64_t)(c0 + i) * R + r0 + k] = in[(int64_t)(r0 + k) * Cc + c0 + i];
+  }
+}
+
+template <typename T, int EPI, int VAR>
+void launch_gemm_v(const GemmArgs& g, hipStream_t s) {
+  const int tiles = ((g.M + GB_M - 1) / GB_M) * ((g.N + GB_N - 1) / GB_N);
+  hipLaunchKernelGGL((gemm_nt_kernel<T, EPI, VAR>), dim3(tiles), dim3(G_THREADS), 0, s, (const T*)g.A, (const T*)g.B,
+                     (T*)g.C, g.M, g.N, g.K, g.lda, g.ldb, g.ldc, (const T*)g.bias, (const T*)g.aux, g.ldaux,
+                     (T*)g.aux_out, g.part);
+}
+
+template <typename T, int EPI>
+void launch_gemm(const GemmArgs& g, hipStream_t s) {
+  if (g.variant == 1) launch_gemm_v<T, EPI, 1>(g, s);
+  else launch_gemm_v<T, EPI, 0>(g, s);
+}
+
+template <typename T>
+int gemm_dispatch(const GemmArgs& g, hipStream_t s) {
+  switch (g.epi) {
+    case EPI_NONE: launch_gemm<T, EPI_NONE>(g, s); break;
+    case EPI_BIAS: launch_gemm<T, EPI_BIAS>(g, s); break;
+    case EPI_BIAS_GELU: launch_gemm<T, EPI_BIAS_GELU>(g, s); break;
+    case EPI_DGELU: launch_gemm<T, EPI_DGELU>(g, s); break;
+    case EPI_RESID: launch_gemm<T, EPI_RESID>(g, s); break;
+    default: return -3;
+  }
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+bool gemm_supported(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc) {
+  return M > 0 && N > 0 && K > 0 && K % GB_K == 0 && N % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 && ldc % 8 == 0 &&
+         (int64_t)M * lda < (1ll << 40);
+}
+
+int64_t gemm_part_rows(int M) { return (int64_t)((M + GB_M - 1) / GB_M) * 2; }
+
+int gemm_nt(const GemmArgs& g, int dt, hipStream_t s) {
+  if (!gemm_supported(g.M, g.N, g.K, g.lda, g.ldb, g.ldc)) return -2;
+  if (dt == kBF16Code) return gemm_dispatch<bf16>(g, s);
+  if (dt == kF16Code) return gemm_dispatch<f16>(g, s);
+  return -1;
+}
+
+int gemm_bias_grad(const float* part, int parts, int N, void* out, int odt, hipStream_t s) {
+  if (odt == kBF16Code) launch_partial_colsum<bf16>(part, parts, N, N, (bf16*)out, s);
+  else if (odt == kF16Code) launch_partial_colsum<f16>(part, parts, N, N, (f16*)out, s);
+  else if (odt == kF32Code) launch_partial_colsum<float>(part, parts, N, N, (float*)out, s);
+  else return -1;
+  return (int)hipGetLastError();
+}
+
+int transpose_2d(const void* in, void* out, int R, int C, int dt, hipStream_t s) {
+  if (R == 0 || C == 0) return 0;
+  dim3 grid((C + 63) / 64, (R + 255) / 256);
+  if (dt == kBF16Code)
+    hipLaunchKernelGGL((transpose_kernel<bf16>), grid, dim3(256), 0, s, (const bf16*)in, (bf16*)out, R, C);
+  else if (dt == kF16Code)
+    hipLaunchKernelGGL((transpose_kernel<f16>), grid, dim3(256), 0, s, (const f16*)in, (f16*)out, R, C);
+  else
+    return -1;
+  return (int)hipGetLastError();
+}
+
+}  // namespace apex

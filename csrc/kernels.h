@@ -166,6 +166,28 @@ int xentropy_bwd(const void* dloss, int64_t dloss_stride, int dloss_dt, const vo
                  const float* lse, const int64_t* labels, void* dlogits, int64_t rows, int V,
                  float smoothing, int64_t ignore_index, int dt, hipStream_t s);
 
+// ----------------------------- MFMA GEMM (gemm.hip) ------------------------
+enum GemmEpi : int { EPI_NONE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_DGELU = 3, EPI_RESID = 4 };
+struct GemmArgs {
+  const void* A;  // [M, K] row-major, lda
+  const void* B;  // [N, K] row-major, ldb
+  void* C;        // [M, N] row-major, ldc
+  int M, N, K;
+  int64_t lda, ldb, ldc;
+  const void* bias;  // [N]            EPI_BIAS, EPI_BIAS_GELU
+  const void* aux;   // [M, N], ldaux  EPI_DGELU (pre-activation H), EPI_RESID (residual)
+  int64_t ldaux;
+  void* aux_out;     // [M, N], ldc    EPI_BIAS_GELU (pre-activation H)
+  float* part;       // [gemm_part_rows(M), N] fp32  EPI_DGELU (bias-grad partials)
+  int epi;
+  int variant;       // main loop: 0 = BK 64 / 4 phases / 2 buffers, 1 = BK 32 / 1 phase / 4 buffers
+};
+bool gemm_supported(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc);
+int64_t gemm_part_rows(int M);
+int gemm_nt(const GemmArgs& g, int dt, hipStream_t s);
+int gemm_bias_grad(const float* part, int parts, int N, void* out, int odt, hipStream_t s);
+int transpose_2d(const void* in, void* out, int R, int C, int dt, hipStream_t s);
+
 // ----------------------------- input pipeline (K-09) -----------------------
 // layout: 0 NHWC->NHWC, 1 NHWC->NCHW (hw % 8 == 0, C in {1,3,4}), 2 NCHW->NCHW. Returns 1 if
 // the geometry is unsupported.

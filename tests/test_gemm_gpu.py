@@ -1,0 +1,124 @@
+"""Hand-written MFMA GEMM (csrc/gemm.hip) and its fused epilogues vs fp32 PyTorch references."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _C():
+    import apex._ext as e
+
+    return e.require()
+
+
+def _ref_mm(a, b):
+    return a.float().reshape(-1, a.shape[-1]) @ b.float().t()
+
+
+def _close(x, ref, tol):
+    err = float((x.float() - ref).abs().max())
+    scale = float(ref.abs().max()) + 1e-6
+    assert err <= tol * scale, (err, scale)
+
+
+SHAPES = [(512, 256, 64), (256, 512, 128), (300, 200, 128), (1000, 1600, 1600), (4096, 1024, 1024),
+          (77, 8, 64), (2048, 3072, 1024)]
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M,N,K", SHAPES + [(512, 512, 64), (512, 512, 128), (768, 256, 192)])
+def test_gemm_plain(dt, M, N, K, variant):
+    C = _C()
+    torch.manual_seed(M + N + K)
+    a = torch.randn(M, K, device=DEV).to(dt)
+    b = torch.randn(N, K, device=DEV).to(dt)
+    c, _ = C.gemm(a, b, C.EPI_NONE, variant=variant)
+    _close(c, _ref_mm(a, b), 1e-2)
+
+
+def test_gemm_identity_asymmetric():
+    """A = I with an asymmetric B catches a transposed C-write (cdna guide §3)."""
+    C = _C()
+    n = 256
+    a = torch.eye(n, device=DEV, dtype=torch.bfloat16)
+    b = (torch.arange(n * n, device=DEV).reshape(n, n) % 97).to(torch.bfloat16)
+    c, _ = C.gemm(a, b, C.EPI_NONE)
+    torch.testing.assert_close(c.float(), b.float().t(), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 1600, 1600), (4096, 1024, 1024), (300, 200, 128)])
+def test_gemm_bias(M, N, K):
+    C = _C()
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    b = torch.randn(N, K, device=DEV).bfloat16()
+    bias = torch.randn(N, device=DEV).bfloat16()
+    c, _ = C.gemm(a, b, C.EPI_BIAS, bias)
+    _close(c, _ref_mm(a, b) + bias.float(), 1e-2)
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 1600, 1600), (4096, 4096, 1024), (300, 200, 128)])
+def test_gemm_bias_gelu(M, N, K):
+    C = _C()
+    a = (torch.randn(M, K, device=DEV) / K ** 0.5).bfloat16()
+    b = torch.randn(N, K, device=DEV).bfloat16()
+    bias = torch.randn(N, device=DEV).bfloat16()
+    y, h = C.gemm(a, b, C.EPI_BIAS_GELU, bias)
+    href = _ref_mm(a, b) + bias.float()
+    _close(h, href, 1e-2)
+    _close(y, F.gelu(href), 1.5e-2)
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 1600, 1600), (4096, 4096, 1024), (300, 200, 128)])
+def test_gemm_dgelu_bias_grad(M, N, K):
+    C = _C()
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    b = (torch.randn(N, K, device=DEV) / K ** 0.5).bfloat16()
+    h = torch.randn(M, N, device=DEV).bfloat16()
+    dh, db = C.gemm(a, b, C.EPI_DGELU, None, h, torch.float32)
+    hr = h.float().requires_grad_(True)
+    F.gelu(hr).backward(_ref_mm(a, b))
+    _close(dh, hr.grad, 1.5e-2)
+    torch.testing.assert_close(db, dh.float().sum(0), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 1600, 1600), (4096, 1024, 4096)])
+def test_gemm_resid(M, N, K):
+    C = _C()
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    b = (torch.randn(N, K, device=DEV) / K ** 0.5).bfloat16()
+    r = torch.randn(M, N, device=DEV).bfloat16()
+    c, _ = C.gemm(a, b, C.EPI_RESID, None, r)
+    _close(c, _ref_mm(a, b) + r.float(), 1e-2)
+
+
+def test_gemm_strided_and_3d():
+    C = _C()
+    base = torch.randn(512, 3 * 1024, device=DEV).bfloat16()
+    a = base[:, 1024:2048]  # row stride 3072
+    b = torch.randn(256, 1024, device=DEV).bfloat16()
+    c, _ = C.gemm(a, b, C.EPI_NONE)
+    _close(c, _ref_mm(a, b), 1e-2)
+    a3 = torch.randn(4, 128, 1024, device=DEV).bfloat16()
+    c3, _ = C.gemm(a3, b, C.EPI_NONE)
+    assert c3.shape == (4, 128, 256)
+    _close(c3.reshape(-1, 256), _ref_mm(a3, b), 1e-2)
+
+
+def test_transpose():
+    C = _C()
+    for r, c in [(1024, 4096), (1000, 33), (1, 64)]:
+        x = torch.randn(r, c, device=DEV).bfloat16()
+        torch.testing.assert_close(C.transpose(x), x.t().contiguous(), rtol=0, atol=0)
+
+
+def test_gemm_supported_rejects():
+    C = _C()
+    a = torch.randn(64, 128, device=DEV).bfloat16()
+    assert not C.gemm_supported(a, torch.randn(12, 128, device=DEV).bfloat16())  # N % 8
+    assert not C.gemm_supported(torch.randn(64, 96, device=DEV).bfloat16(),
+                                torch.randn(16, 96, device=DEV).bfloat16())  # K % 64
+    assert not C.gemm_supported(a.float(), torch.randn(16, 128, device=DEV))  # fp32
+    assert C.gemm_supported(a, torch.randn(16, 128, device=DEV).bfloat16())
