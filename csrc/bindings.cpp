@@ -766,8 +766,7 @@ bool k_gemm_supported(Tensor a, Tensor b) {
 }
 
 std::vector<Tensor> k_gemm(Tensor a, Tensor b, int64_t epi, const c10::optional<Tensor>& bias,
-                           const c10::optional<Tensor>& aux, c10::optional<at::ScalarType> bias_grad_dtype,
-                           int64_t variant) {
+                           const c10::optional<Tensor>& aux, c10::optional<at::ScalarType> bias_grad_dtype) {
   TORCH_CHECK(k_gemm_supported(a, b), "gemm: unsupported operands (bf16/fp16, K % 64 == 0, N % 8 == 0, "
               "16-byte aligned, unit inner stride)");
   const int64_t K = a.size(-1), N = b.size(0), M = a.numel() / K;
@@ -786,7 +785,6 @@ std::vector<Tensor> k_gemm(Tensor a, Tensor b, int64_t epi, const c10::optional<
   g.ldb = b.stride(0);
   g.ldc = N;
   g.epi = (int)epi;
-  g.variant = (int)variant;
   Tensor extra;
   if (epi == apex::EPI_BIAS || epi == apex::EPI_BIAS_GELU) {
     TORCH_CHECK(bias.has_value() && bias->defined() && bias->is_contiguous() && bias->numel() == N &&
@@ -884,7 +882,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("input_normalize", &k_input_normalize);
   m.def("gemm_supported", &k_gemm_supported);
   m.def("gemm", &k_gemm, py::arg("a"), py::arg("b"), py::arg("epi") = 0, py::arg("bias") = py::none(),
-        py::arg("aux") = py::none(), py::arg("bias_grad_dtype") = py::none(), py::arg("variant") = 0);
+        py::arg("aux") = py::none(), py::arg("bias_grad_dtype") = py::none());
   m.def("transpose", &k_transpose);
   m.attr("EPI_NONE") = (int)apex::EPI_NONE;
   m.attr("EPI_BIAS") = (int)apex::EPI_BIAS;

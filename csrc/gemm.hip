@@ -137,6 +137,11 @@ __device__ __forceinline__ void stage_pieces(const T* __restrict__ g, int64_t ld
 // the reads, so restaging one phase later (B(t+2) in p3) is safe; A(t+1) goes to the buffer whose
 // A was last read in the previous tile's p3. RAW: vmcnt(4) in p4 retires everything but B(t+2)
 // (i.e. A(t+1), B(t+1)) before the barrier that precedes the next tile's first read.
+// Measured alternatives (profiles/r1_gemm_ksweep_variants.jsonl, same box, interleaved): LDS wait
+// after the barrier with the glds moved to p2/p4 — within 1 %; BK = 32 with four buffers and one
+// 32-MFMA phase per K-tile (half the barriers, loads 3 tiles ahead) — 12-15 % slower (the glds
+// issue then sits inside the MFMA section). rocprof on the 32768x1024x4096 case: MFMA busy 65 %
+// of SIMD cycles at 1.98 GHz, zero LDS bank conflicts.
 template <typename T>
 __device__ __forceinline__ void mainloop_bk64(const T* __restrict__ A, const T* __restrict__ B, int M, int N, int K,
                                               int64_t lda, int64_t ldb, int m0, int n0, char* smem, int wid, int wr,
@@ -240,92 +245,7 @@ __device__ __forceinline__ void mainloop_bk64(const T* __restrict__ A, const T* 
   }
 }
 
-// BK = 32 variant: four 32 KB LDS buffers (A 256x32 + B 256x32 each, 64-B rows), ONE phase per
-// K-tile: R = 12 ds_read_b128 (8 A + 4 B fragments) | barrier | M = 32 MFMAs with the 4 glds pieces
-// of tile t+3 issued among them, then vmcnt retiring tile t+1 | barrier. Half the barriers of the
-// BK=64 4-phase loop per K element, and loads run 3 tiles ahead (2 sections of slack + one tile).
-// LDS image: 16-B chunk c of row r at chunk c ^ f((r >> 2) & 3), f = {0,2,3,1}: every 16-lane
-// ds_read_b128 group (rows r..r+15, chunks lk / lk+1) hits 16 distinct slots of the bank row.
-__device__ __forceinline__ int swz32(int r) { return (0x78 >> (((r >> 2) & 3) * 2)) & 3; }
-
-template <typename T>
-__device__ __forceinline__ void stage32(const T* __restrict__ g, int64_t ld, int row0, int rows, int k0,
-                                        char* lds_tile, int wid, int lane) {
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int piece = wid * 2 + j;  // 16 pieces of 16 rows x 64 B per operand tile
-    const int r = piece * 16 + (lane >> 2);
-    const int chunk = (lane & 3) ^ swz32(r);
-    int gr = row0 + r;
-    gr = gr < rows ? gr : rows - 1;
-    glds16(g + (int64_t)gr * ld + k0 + chunk * 8, lds_tile + piece * 1024);
-  }
-}
-
-__device__ __forceinline__ s16x8 lds_frag32(const char* tile, int r, int c) {
-  return *reinterpret_cast<const s16x8*>(tile + r * 64 + ((c ^ swz32(r)) << 4));
-}
-
-template <typename T>
-__device__ __forceinline__ void mainloop_bk32(const T* __restrict__ A, const T* __restrict__ B, int M, int N, int K,
-                                              int64_t lda, int64_t ldb, int m0, int n0, char* smem, int wid, int wr,
-                                              int wc, int lane, f32x4 (&acc)[4][8]) {
-  constexpr int BK = 32, TB = 256 * BK * 2, BUF = 2 * TB;
-  const int nt = K / BK;
-  const int lr = lane & 15, lk = lane >> 4;
-  // prologue: tiles 0, 1, 2 in flight, tile 0 retired
-#pragma unroll
-  for (int p = 0; p < 3; ++p) {
-    if (p < nt) {
-      stage32<T>(A, lda, m0, M, p * BK, smem + p * BUF, wid, lane);
-      stage32<T>(B, ldb, n0, N, p * BK, smem + p * BUF + TB, wid, lane);
-    }
-  }
-  if (nt >= 3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if (nt == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  bar();
-  if (wr == 1) bar();  // stagger group 1 by one barrier
-
-  s16x8 fa[8], fb[4];
-  for (int t = 0; t < nt; ++t) {
-    const char* ta = smem + (t & 3) * BUF;
-    const char* tb = ta + TB;
-    // ---- R: fragments of tile t ----
-#pragma unroll
-    for (int j = 0; j < 4; ++j) fb[j] = lds_frag32(tb, wc * 64 + j * 16 + lr, lk);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) fa[i] = lds_frag32(ta, wr * 128 + i * 16 + lr, lk);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    bar();
-    // ---- M: 32 MFMAs; tile t+3 -> buffer (t+3)&3 (= (t-1)&3, last read one section ago) ----
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) acc[j][i] = mfma16<T>(fb[j], fa[i], acc[j][i]);
-    __builtin_amdgcn_s_setprio(0);
-    if (t + 3 < nt) {
-      char* nb = smem + ((t + 3) & 3) * BUF;
-      stage32<T>(A, lda, m0, M, (t + 3) * BK, nb, wid, lane);
-      stage32<T>(B, ldb, n0, N, (t + 3) * BK, nb + TB, wid, lane);
-    }
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int j = 2; j < 4; ++j)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) acc[j][i] = mfma16<T>(fb[j], fa[i], acc[j][i]);
-    __builtin_amdgcn_s_setprio(0);
-    // retire tile t+1 (younger in flight: t+2, t+3 when they exist)
-    const int younger = min(nt - 1, t + 3) - (t + 1);
-    if (younger >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    bar();
-  }
-}
-
-template <typename T, int EPI, int VAR>
+template <typename T, int EPI>
 __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(const T* __restrict__ A, const T* __restrict__ B,
                                                             T* __restrict__ C, int M, int N, int K, int64_t lda,
                                                             int64_t ldb, int64_t ldc, const T* __restrict__ bias,
@@ -356,10 +276,7 @@ __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(const T* __restrict_
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if constexpr (VAR == 0)
-    mainloop_bk64<T>(A, B, M, N, K, lda, ldb, m0, n0, smem, wid, wr, wc, lane, acc);
-  else
-    mainloop_bk32<T>(A, B, M, N, K, lda, ldb, m0, n0, smem, wid, wr, wc, lane, acc);
+  mainloop_bk64<T>(A, B, M, N, K, lda, ldb, m0, n0, smem, wid, wr, wc, lane, acc);
   if (wr == 0) bar();  // re-align the groups
   bar();               // every wave is past its last ds_read: LDS is free for the epilogue
 
@@ -544,18 +461,12 @@ __global__ void __launch_bounds__(256) transpose_kernel(const T* __restrict__ in
   }
 }
 
-template <typename T, int EPI, int VAR>
-void launch_gemm_v(const GemmArgs& g, hipStream_t s) {
-  const int tiles = ((g.M + GB_M - 1) / GB_M) * ((g.N + GB_N - 1) / GB_N);
-  hipLaunchKernelGGL((gemm_nt_kernel<T, EPI, VAR>), dim3(tiles), dim3(G_THREADS), 0, s, (const T*)g.A, (const T*)g.B,
-                     (T*)g.C, g.M, g.N, g.K, g.lda, g.ldb, g.ldc, (const T*)g.bias, (const T*)g.aux, g.ldaux,
-                     (T*)g.aux_out, g.part);
-}
-
 template <typename T, int EPI>
 void launch_gemm(const GemmArgs& g, hipStream_t s) {
-  if (g.variant == 1) launch_gemm_v<T, EPI, 1>(g, s);
-  else launch_gemm_v<T, EPI, 0>(g, s);
+  const int tiles = ((g.M + GB_M - 1) / GB_M) * ((g.N + GB_N - 1) / GB_N);
+  hipLaunchKernelGGL((gemm_nt_kernel<T, EPI>), dim3(tiles), dim3(G_THREADS), 0, s, (const T*)g.A, (const T*)g.B,
+                     (T*)g.C, g.M, g.N, g.K, g.lda, g.ldb, g.ldc, (const T*)g.bias, (const T*)g.aux, g.ldaux,
+                     (T*)g.aux_out, g.part);
 }
 
 template <typename T>

@@ -180,7 +180,6 @@ struct GemmArgs {
   void* aux_out;     // [M, N], ldc    EPI_BIAS_GELU (pre-activation H)
   float* part;       // [gemm_part_rows(M), N] fp32  EPI_DGELU (bias-grad partials)
   int epi;
-  int variant;       // main loop: 0 = BK 64 / 4 phases / 2 buffers, 1 = BK 32 / 1 phase / 4 buffers
 };
 bool gemm_supported(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc);
 int64_t gemm_part_rows(int M);
