@@ -55,9 +55,23 @@ class FusedOptimizerBase(Optimizer):
         set_none = self.set_grad_none if set_to_none is None else set_to_none
         groups = self._amp_model_params if self._amp_model_params is not None else \
             [g["params"] for g in self.param_groups]
+        # grads that are views of an apex DDP bucket buffer: one fill per buffer instead of one
+        # launch per parameter, when every parameter of that buffer belongs to this optimizer
+        flats, members = {}, {}
+        for ps in groups:
+            for p in ps:
+                f = getattr(p, "_apex_bucket_flat", None)
+                if p.grad is not None and f is not None and getattr(p, "_apex_grad_is_bucket_view", False):
+                    flats[id(f)] = f
+                    members[id(f)] = members.get(id(f), 0) + 1
+        whole = {k for k, f in flats.items() if members[k] == getattr(f, "_apex_nparams", -1)}
+        for k in whole:
+            flats[k].zero_()
         for ps in groups:
             for p in ps:
                 if p.grad is None:
+                    continue
+                if whole and id(getattr(p, "_apex_bucket_flat", None)) in whole:
                     continue
                 if set_none and not getattr(p, "_apex_grad_is_bucket_view", False):
                     p.grad = None

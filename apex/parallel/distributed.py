@@ -383,6 +383,7 @@ class DistributedDataParallel(Module):
             total = sum(self._params[i].numel() for i in idxs)
             dev = self._params[idxs[0]].device
             flat = torch.zeros(total, dtype=dt, device=dev)
+            flat._apex_nparams = len(idxs)  # lets fused optimizers zero the grads with one fill
             self._flat[dt] = flat
             off, start, cur = 0, 0, []
             limit = self.first_bucket_size or self.message_size
@@ -397,6 +398,7 @@ class DistributedDataParallel(Module):
                     v.copy_(p.grad)
                 p.grad = v
                 p._apex_grad_is_bucket_view = True
+                p._apex_bucket_flat = flat
                 self._views[i] = v
                 cur.append(i)
                 off += n

@@ -140,3 +140,47 @@ def test_ddp_matches_full_batch_training():
     for p in procs:
         p.join(timeout=60)
     assert all(r[1] == "ok" for r in res), res
+
+
+def _zero_grad_worker(rank, world, port, q):
+    try:
+        _init(rank, world, port)
+        from apex.optimizers import FusedSGD
+        from apex.parallel import DistributedDataParallel as DDP
+
+        torch.manual_seed(0)
+        net = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 4))
+        model = DDP(net, message_size=50)
+        opt = FusedSGD(model.parameters(), lr=0.1)
+        for i in range(3):
+            opt.zero_grad()
+            model(torch.randn(5, 8)).sum().backward()
+            if i:
+                # grads stay views of the one bucket buffer and are correct after a whole-buffer zero
+                flat = net[0].weight._apex_bucket_flat
+                assert all(p.grad.data_ptr() >= flat.data_ptr() for p in net.parameters())
+            opt.step()
+        opt.zero_grad()
+        assert all(float(p.grad.abs().sum()) == 0.0 for p in net.parameters())
+        assert net[0].weight._apex_bucket_flat._apex_nparams == 4
+        q.put((rank, "ok"))
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_fused_optimizer_zero_grad_on_ddp_buckets():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_zero_grad_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[1] == "ok" for r in res), res

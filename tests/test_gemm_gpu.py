@@ -34,7 +34,7 @@ def test_gemm_plain(dt, M, N, K):
     torch.manual_seed(M + N + K)
     a = torch.randn(M, K, device=DEV).to(dt)
     b = torch.randn(N, K, device=DEV).to(dt)
-    c, _ = C.gemm(a, b, C.EPI_NONEiant)
+    c, _ = C.gemm(a, b, C.EPI_NONE)
     _close(c, _ref_mm(a, b), 1e-2)
 
 
