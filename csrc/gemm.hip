@@ -61,25 +61,38 @@ __device__ __forceinline__ void glds16(const void* g, void* lds_wave_base) {
 
 // Branch-free erf (Abramowitz & Stegun 7.1.26, |error| <= 1.5e-7): one v_rcp, one v_exp and
 // seven FMAs instead of ocml's erff (whose inlined branches made the epilogue 10x larger).
-__device__ __forceinline__ float erf_fast(float x, float e_neg_x2) {
-  const float ax = fabsf(x);
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, ax, 1.f));
-  float p = fmaf(1.061405429f, t, -1.453152027f);
-  p = fmaf(p, t, 1.421413741f);
-  p = fmaf(p, t, -0.284496736f);
-  p = fmaf(p, t, 0.254829592f);
-  const float r = fmaf(-p * t, e_neg_x2, 1.f);
-  return copysignf(r, x);
+// Two values at a time: the polynomial runs on packed f32 (v_pk_fma_f32 / v_pk_mul_f32), the
+// epilogue is VALU-bound on the GELU work (it runs after the MFMA main loop, not beside it).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f32x2 splat(float v) { return f32x2{v, v}; }
+
+// erf(x) given e = exp(-x^2) (shared with the GELU derivative's pdf)
+__device__ __forceinline__ f32x2 erf2(f32x2 x, f32x2 e) {
+  const f32x2 ax = __builtin_elementwise_abs(x);
+  const f32x2 d = pk_fma(splat(0.3275911f), ax, splat(1.f));
+  const f32x2 t = f32x2{__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+  f32x2 p = pk_fma(splat(1.061405429f), t, splat(-1.453152027f));
+  p = pk_fma(p, t, splat(1.421413741f));
+  p = pk_fma(p, t, splat(-0.284496736f));
+  p = pk_fma(p, t, splat(0.254829592f));
+  const f32x2 r = pk_fma(-p * t, e, splat(1.f));
+  return f32x2{copysignf(r[0], x[0]), copysignf(r[1], x[1])};
 }
 // exp(-x^2/2) via v_exp_f32 (2^y)
-__device__ __forceinline__ float exp_neg_half_sq(float x) { return __builtin_amdgcn_exp2f(-0.72134752044448170f * x * x); }
-__device__ __forceinline__ float gelu_f(float x) {
-  return 0.5f * x * (1.f + erf_fast(x * 0.70710678118654752f, exp_neg_half_sq(x)));
+__device__ __forceinline__ f32x2 exp_neg_half_sq2(f32x2 x) {
+  const f32x2 y = splat(-0.72134752044448170f) * x * x;
+  return f32x2{__builtin_amdgcn_exp2f(y[0]), __builtin_amdgcn_exp2f(y[1])};
 }
-__device__ __forceinline__ float gelu_grad_f(float x) {
-  const float e = exp_neg_half_sq(x);
-  const float cdf = 0.5f * (1.f + erf_fast(x * 0.70710678118654752f, e));
-  return fmaf(x * 0.39894228040143268f, e, cdf);
+__device__ __forceinline__ f32x2 gelu2(f32x2 x) {
+  const f32x2 c = erf2(x * splat(0.70710678118654752f), exp_neg_half_sq2(x));
+  return splat(0.5f) * x * (splat(1.f) + c);
+}
+__device__ __forceinline__ f32x2 gelu_grad2(f32x2 x) {
+  const f32x2 e = exp_neg_half_sq2(x);
+  const f32x2 cdf = splat(0.5f) * (splat(1.f) + erf2(x * splat(0.70710678118654752f), e));
+  return pk_fma(x * splat(0.39894228040143268f), e, cdf);
 }
 
 template <typename T>
@@ -140,7 +153,9 @@ __device__ __forceinline__ void stage_pieces(const T* __restrict__ g, int64_t ld
 // Measured alternatives (profiles/r1_gemm_ksweep_variants.jsonl, same box, interleaved): LDS wait
 // after the barrier with the glds moved to p2/p4 — within 1 %; BK = 32 with four buffers and one
 // 32-MFMA phase per K-tile (half the barriers, loads 3 tiles ahead) — 12-15 % slower (the glds
-// issue then sits inside the MFMA section). rocprof on the 32768x1024x4096 case: MFMA busy 65 %
+// issue then sits inside the MFMA section); 256x128 tiles at two workgroups per CU (BK 32, three
+// stages, no ping-pong; profiles/r1_gemm_*_2wg_variant.jsonl) — its epilogue does overlap the
+// other workgroup's MFMAs (K = 64: 55 vs 65 us at N = 4096) but the main loop is ~60 % slower. rocprof on the 32768x1024x4096 case: MFMA busy 65 %
 // of SIMD cycles at 1.98 GHz, zero LDS bank conflicts.
 template <typename T>
 __device__ __forceinline__ void mainloop_bk64(const T* __restrict__ A, const T* __restrict__ B, int M, int N, int K,
@@ -245,41 +260,13 @@ __device__ __forceinline__ void mainloop_bk64(const T* __restrict__ A, const T* 
   }
 }
 
-template <typename T, int EPI>
-__global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(const T* __restrict__ A, const T* __restrict__ B,
-                                                            T* __restrict__ C, int M, int N, int K, int64_t lda,
-                                                            int64_t ldb, int64_t ldc, const T* __restrict__ bias,
-                                                            const T* __restrict__ aux, int64_t ldaux,
-                                                            T* __restrict__ aux_out, float* __restrict__ part) {
-  __shared__ __attribute__((aligned(16))) char smem[G_LDS_BYTES];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wid >> 2, wc = wid & 3;
+// Epilogue shared by both kernels (wave tile 128 x 64 at rows m0 + wr*128, cols n0 + wc*64).
+template <typename T, int EPI, int TBM, int TBN>
+__device__ __forceinline__ void epilogue(const f32x4 (&acc)[4][8], char* reg, T* __restrict__ C, int M, int N,
+                                         int64_t ldc, const T* __restrict__ bias, const T* __restrict__ aux,
+                                         int64_t ldaux, T* __restrict__ aux_out, float* __restrict__ part, int m0,
+                                         int n0, int tm, int wr, int wc, int lane) {
   const int lr = lane & 15, lk = lane >> 4;
-
-  // ---- tile mapping: bijective XCD remap, then GROUP_M panel order ----
-  const int tiles_m = (M + GB_M - 1) / GB_M, tiles_n = (N + GB_N - 1) / GB_N;
-  const int nwg = tiles_m * tiles_n;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
-  const int wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
-  const int group = G_GROUP_M * tiles_n;
-  const int first_m = (wg / group) * G_GROUP_M;
-  const int gm = min(tiles_m - first_m, G_GROUP_M);
-  const int tm = first_m + (wg % group) % gm;
-  const int tn = (wg % group) / gm;
-  const int m0 = tm * GB_M, n0 = tn * GB_N;
-
-  f32x4 acc[4][8];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  mainloop_bk64<T>(A, B, M, N, K, lda, ldb, m0, n0, smem, wid, wr, wc, lane, acc);
-  if (wr == 0) bar();  // re-align the groups
-  bar();               // every wave is past its last ds_read: LDS is free for the epilogue
-
   // ---- epilogue ----
   // acc[j][i] holds rows wr*128 + i*16 + lr, cols wc*64 + j*16 + 4*lk .. +3 of the tile. The fp32
   // accumulators are rounded to T and transposed through the wave's own 16 KB LDS region
@@ -291,7 +278,6 @@ __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(const T* __restrict_
   // All LDS reads are issued before the first global access (hipcc drains vmcnt before an LDS access
   // while VMEM ops are pending), and the interior tiles take a branch-free path (a per-element
   // guarded load makes hipcc wait vmcnt(0) per element).
-  char* reg = smem + wid * 16384;
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -319,7 +305,7 @@ __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(const T* __restrict_
 
   const int ncol = n0 + wc * 64 + (lane & 7) * 8;
   const int mrow = m0 + wr * 128 + (lane >> 3);
-  const bool full = m0 + GB_M <= M && n0 + GB_N <= N;
+  const bool full = m0 + TBM <= M && n0 + TBN <= N;
   auto unpack = [&](const u32x4& x, float (&v)[8]) {
     Pack<T, 8> pk = *reinterpret_cast<const Pack<T, 8>*>(&x);
 #pragma unroll
@@ -385,17 +371,24 @@ __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(const T* __restrict_
           else st16(aux_out, m, hraw);
           unpack(hraw, v);  // GELU of the stored pre-activation
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = gelu_f(v[e]);
+          for (int e = 0; e < 8; e += 2) {
+            const f32x2 gv = gelu2(f32x2{v[e], v[e + 1]});
+            v[e] = gv[0];
+            v[e + 1] = gv[1];
+          }
         } else {
           float x[8];
           unpack(ra[it], x);
           const bool ok = F || (m < M && ncol < N);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
+          for (int e = 0; e < 8; e += 2) {
             if constexpr (EPI == EPI_DGELU) {
-              v[e] = ok ? v[e] * gelu_grad_f(x[e]) : 0.f;
+              const f32x2 gg = gelu_grad2(f32x2{x[e], x[e + 1]});
+              v[e] = ok ? v[e] * gg[0] : 0.f;
+              v[e + 1] = ok ? v[e + 1] * gg[1] : 0.f;
             } else {
               v[e] += x[e];
+              v[e + 1] += x[e + 1];
             }
           }
         }
@@ -430,6 +423,45 @@ __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(const T* __restrict_
   };
   if (full) body(std::integral_constant<bool, true>{});
   else body(std::integral_constant<bool, false>{});
+}
+
+template <typename T, int EPI>
+__global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(const T* __restrict__ A, const T* __restrict__ B,
+                                                            T* __restrict__ C, int M, int N, int K, int64_t lda,
+                                                            int64_t ldb, int64_t ldc, const T* __restrict__ bias,
+                                                            const T* __restrict__ aux, int64_t ldaux,
+                                                            T* __restrict__ aux_out, float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) char smem[G_LDS_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+  const int lr = lane & 15, lk = lane >> 4;
+
+  // ---- tile mapping: bijective XCD remap, then GROUP_M panel order ----
+  const int tiles_m = (M + GB_M - 1) / GB_M, tiles_n = (N + GB_N - 1) / GB_N;
+  const int nwg = tiles_m * tiles_n;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
+  const int wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  const int group = G_GROUP_M * tiles_n;
+  const int first_m = (wg / group) * G_GROUP_M;
+  const int gm = min(tiles_m - first_m, G_GROUP_M);
+  const int tm = first_m + (wg % group) % gm;
+  const int tn = (wg % group) / gm;
+  const int m0 = tm * GB_M, n0 = tn * GB_N;
+
+  f32x4 acc[4][8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  mainloop_bk64<T>(A, B, M, N, K, lda, ldb, m0, n0, smem, wid, wr, wc, lane, acc);
+  if (wr == 0) bar();  // re-align the groups
+  bar();               // every wave is past its last ds_read: LDS is free for the epilogue
+
+  epilogue<T, EPI, GB_M, GB_N>(acc, smem + wid * 16384, C, M, N, ldc, bias, aux, ldaux, aux_out, part, m0, n0, tm, wr,
+                                wc, lane);
 }
 
 // 2-D transpose out[C][R] = in[R][C] (16-bit elements). Each lane transposes an 8x8 block in

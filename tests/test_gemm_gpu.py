@@ -28,7 +28,7 @@ SHAPES = [(512, 256, 64), (256, 512, 128), (300, 200, 128), (1000, 1600, 1600), 
 
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("M,N,K", SHAPES + [(512, 512, 64), (512, 512, 128), (768, 256, 192)])
+@pytest.mark.parametrize("M,N,K", SHAPES + [(512, 512, 64), (512, 512, 128), (768, 256, 192), (512, 384, 32 * 3 * 64)])
 def test_gemm_plain(dt, M, N, K):
     C = _C()
     torch.manual_seed(M + N + K)
