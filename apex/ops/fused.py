@@ -74,6 +74,15 @@ def _wgrad(dy2, x2):
     M, N = dy2.shape
     K = x2.shape[1]
     s = _wgrad_splits(M, N, K) if dy2.dtype in (torch.bfloat16, torch.float16) else 1
+    from . import gemm as G
+
+    if G.mode() == "mfma" and dy2.is_cuda:
+        C = _ext.require()
+        st = max(s, 4 if M >= 16384 else 1)
+        if C.gemm_tt_supported(dy2, x2, st):
+            # hand-written transposed-read MFMA GEMM (csrc/gemm.hip, TR main loop); at parity with
+            # the library here (profiles/r1_gemm_policy.jsonl), so only in the all-MFMA mode
+            return C.gemm_tt(dy2, x2, st, dy2.dtype)
     if s == 1 or not (dy2.is_contiguous() and x2.is_contiguous()):
         return torch.mm(dy2.t(), x2)
     slabs = torch.bmm(dy2.view(s, M // s, N).transpose(1, 2), x2.view(s, M // s, K), out_dtype=torch.float32)

@@ -22,7 +22,9 @@ Policy (``APEX_GEMM``):
                     MFMA wins      FFN1 fwd+bias+GELU 299 vs 328 (mm + bias_act), FFN2 dgrad+dGELU
                                    318 vs 402 (mm + bias_act_bwd), QKV dgrad+residual 171 vs 199
                                    (addmm), FFN1 dgrad+residual 221 vs 242
-  mfma            every supported GEMM on the MFMA kernel (A/B and coverage runs)
+  mfma            every supported GEMM on the MFMA kernels, including the weight gradients on
+                  the transposed-read variant (C.gemm_tt: 266-273 us vs the library's 267-272
+                  for the FFN shapes with 4 K-slices; slower for QKV) — A/B and coverage runs
   blas            library GEMM + separate HIP epilogue kernels everywhere
 Each function falls back to the library path when the operands do not fit the MFMA kernel
 (K % 64, N % 8, dtype, alignment). Numerics follow the unfused composition: the GEMM result is
@@ -45,6 +47,10 @@ def _C():
 
 def _2d(x):
     return x.reshape(-1, x.shape[-1])
+
+
+def mode() -> str:
+    return _MODE
 
 
 def use_mfma(a, w, fused=True) -> bool:

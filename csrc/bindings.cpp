@@ -818,6 +818,45 @@ std::vector<Tensor> k_gemm(Tensor a, Tensor b, int64_t epi, const c10::optional<
   return {c, extra};
 }
 
+// weight gradient: out[P, Q] = a^T b for a [R, P], b [R, Q] (contraction over the R rows, split
+// into `splits` slices whose fp32 partials are combined by splitk_reduce)
+bool k_gemm_tt_supported(Tensor a, Tensor b, int64_t splits) {
+  if (!a.is_cuda() || a.dim() != 2 || b.dim() != 2 || a.scalar_type() != b.scalar_type()) return false;
+  if (a.scalar_type() != at::kBFloat16 && a.scalar_type() != at::kHalf) return false;
+  if (!a.is_contiguous() || !b.is_contiguous() || a.size(0) != b.size(0)) return false;
+  auto al = [](const Tensor& t) { return reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0; };
+  return al(a) && al(b) && splits >= 1 &&
+         apex::gemm_tt_supported((int)a.size(1), (int)b.size(1), (int)a.size(0), (int)splits, a.size(1), b.size(1));
+}
+
+Tensor k_gemm_tt(Tensor a, Tensor b, int64_t splits, at::ScalarType out_dtype) {
+  TORCH_CHECK(k_gemm_tt_supported(a, b, splits), "gemm_tt: unsupported operands");
+  const int64_t R = a.size(0), P = a.size(1), Q = b.size(1);
+  apex::GemmArgs g{};
+  g.A = a.data_ptr();
+  g.B = b.data_ptr();
+  g.M = (int)P;
+  g.N = (int)Q;
+  g.K = (int)(R / splits);
+  g.lda = P;
+  g.ldb = Q;
+  g.ldc = Q;
+  g.splits = (int)splits;
+  Tensor out;
+  if (splits == 1 && out_dtype == a.scalar_type()) {
+    out = at::empty({P, Q}, a.options());
+    g.C = out.data_ptr();
+    g.epi = apex::EPI_NONE;
+    check(apex::gemm_tt(g, dt_code(a.scalar_type()), cur_stream()), "gemm_tt");
+    return out;
+  }
+  Tensor slabs = at::empty({splits, P, Q}, a.options().dtype(at::kFloat));
+  g.part = slabs.data_ptr<float>();
+  g.epi = apex::EPI_F32;
+  check(apex::gemm_tt(g, dt_code(a.scalar_type()), cur_stream()), "gemm_tt");
+  return k_splitk_reduce(slabs, out_dtype);
+}
+
 Tensor k_transpose(Tensor x) {
   TORCH_CHECK(x.is_cuda() && x.dim() == 2, "transpose: 2-D device tensor");
   Tensor xc = x.contiguous();
@@ -884,6 +923,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm", &k_gemm, py::arg("a"), py::arg("b"), py::arg("epi") = 0, py::arg("bias") = py::none(),
         py::arg("aux") = py::none(), py::arg("bias_grad_dtype") = py::none());
   m.def("transpose", &k_transpose);
+  m.def("gemm_tt_supported", &k_gemm_tt_supported);
+  m.def("gemm_tt", &k_gemm_tt);
   m.attr("EPI_NONE") = (int)apex::EPI_NONE;
   m.attr("EPI_BIAS") = (int)apex::EPI_BIAS;
   m.attr("EPI_BIAS_GELU") = (int)apex::EPI_BIAS_GELU;

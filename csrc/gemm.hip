@@ -119,19 +119,55 @@ __device__ __forceinline__ void bar() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// One operand K-tile = 32 glds pieces (8 rows x 128 B); wave `wid` owns pieces wid*4 .. wid*4+3.
-// stage_pieces issues pieces [p0, p0+2) of the wave's four.
-template <typename T>
+// One operand K-tile = 32 glds pieces of 1 KB; wave `wid` owns pieces wid*4 .. wid*4+3 and
+// stage_pieces issues pieces [p0, p0+2) of them.
+//  TR = false (operand [rows][K], K contiguous): piece = 8 rows x 128 B of K; image [256 rows][64 K],
+//    chunk c of row r at c ^ ((r >> 1) & 7).
+//  TR = true (operand stored [K][rows], rows contiguous — the weight-gradient GEMM, where the
+//    contraction runs over tokens): piece = 2 K-rows x 512 B; image [64 K][256 rows], chunk c of
+//    K-row r at c ^ ftr(r); fragments are gathered with ds_read_b64_tr_b16 (hardware transpose).
+__device__ __forceinline__ int ftr(int r) { return 2 * (r & 3) + 8 * ((r >> 3) & 1); }
+
+template <typename T, bool TR>
 __device__ __forceinline__ void stage_pieces(const T* __restrict__ g, int64_t ld, int row0, int rows, int k0,
                                              char* lds_tile, int wid, int lane, int p0) {
 #pragma unroll
   for (int j = p0; j < p0 + 2; ++j) {
     const int piece = wid * 4 + j;
-    const int r = piece * 8 + (lane >> 3);
-    const int chunk = (lane & 7) ^ ((r >> 1) & 7);
-    int gr = row0 + r;
-    gr = gr < rows ? gr : rows - 1;
-    glds16(g + (int64_t)gr * ld + k0 + chunk * 8, lds_tile + piece * 1024);
+    if constexpr (TR) {
+      const int r = piece * 2 + (lane >> 5);
+      const int chunk = (lane & 31) ^ ftr(r);
+      glds16(g + (int64_t)(k0 + r) * ld + row0 + chunk * 8, lds_tile + piece * 1024);
+    } else {
+      const int r = piece * 8 + (lane >> 3);
+      const int chunk = (lane & 7) ^ ((r >> 1) & 7);
+      int gr = row0 + r;
+      gr = gr < rows ? gr : rows - 1;
+      glds16(g + (int64_t)gr * ld + k0 + chunk * 8, lds_tile + piece * 1024);
+    }
+  }
+}
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ s16x4 lds_tr16(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
+}
+
+// MFMA fragment for tile rows rb .. rb+15, K step s (32 wide): lane holds rows rb + lr,
+// K = 32s + 8 lk .. +7.
+template <bool TR>
+__device__ __forceinline__ s16x8 frag(const char* tile, int rb, int s, int lr, int lk) {
+  if constexpr (TR) {
+    // two 4(K) x 16(rows) transposed blocks: lane 4q+p of a 16-lane group addresses K-row
+    // 32s + 8lk + 4h + q, rows rb + 4p .. +3; it receives row rb + lr, K 4h .. 4h+3
+    const int q = lr >> 2, pp = lr & 3;
+    const int cl = (rb >> 3) + (pp >> 1);
+    const int r0 = s * 32 + 8 * lk + q, r1 = r0 + 4;
+    const s16x4 lo = lds_tr16(tile + r0 * 512 + ((cl ^ ftr(r0)) << 4) + (pp & 1) * 8);
+    const s16x4 hi = lds_tr16(tile + r1 * 512 + ((cl ^ ftr(r1)) << 4) + (pp & 1) * 8);
+    return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  } else {
+    return lds_frag(tile, rb + lr, s * 4 + lk);
   }
 }
 
@@ -157,20 +193,20 @@ __device__ __forceinline__ void stage_pieces(const T* __restrict__ g, int64_t ld
 // stages, no ping-pong; profiles/r1_gemm_*_2wg_variant.jsonl) — its epilogue does overlap the
 // other workgroup's MFMAs (K = 64: 55 vs 65 us at N = 4096) but the main loop is ~60 % slower. rocprof on the 32768x1024x4096 case: MFMA busy 65 %
 // of SIMD cycles at 1.98 GHz, zero LDS bank conflicts.
-template <typename T>
+template <typename T, bool TR>
 __device__ __forceinline__ void mainloop_bk64(const T* __restrict__ A, const T* __restrict__ B, int M, int N, int K,
                                               int64_t lda, int64_t ldb, int m0, int n0, char* smem, int wid, int wr,
                                               int wc, int lane, f32x4 (&acc)[4][8]) {
   const int nt = K / GB_K;
   const int lr = lane & 15, lk = lane >> 4;
   // prologue: A(0), B(0) -> buf0, B(1) -> buf1; retire tile 0
-  stage_pieces<T>(A, lda, m0, M, 0, smem, wid, lane, 0);
-  stage_pieces<T>(A, lda, m0, M, 0, smem, wid, lane, 2);
-  stage_pieces<T>(B, ldb, n0, N, 0, smem + G_TILE_BYTES, wid, lane, 0);
-  stage_pieces<T>(B, ldb, n0, N, 0, smem + G_TILE_BYTES, wid, lane, 2);
+  stage_pieces<T, TR>(A, lda, m0, M, 0, smem, wid, lane, 0);
+  stage_pieces<T, TR>(A, lda, m0, M, 0, smem, wid, lane, 2);
+  stage_pieces<T, TR>(B, ldb, n0, N, 0, smem + G_TILE_BYTES, wid, lane, 0);
+  stage_pieces<T, TR>(B, ldb, n0, N, 0, smem + G_TILE_BYTES, wid, lane, 2);
   if (nt > 1) {
-    stage_pieces<T>(B, ldb, n0, N, GB_K, smem + G_BUF_BYTES + G_TILE_BYTES, wid, lane, 0);
-    stage_pieces<T>(B, ldb, n0, N, GB_K, smem + G_BUF_BYTES + G_TILE_BYTES, wid, lane, 2);
+    stage_pieces<T, TR>(B, ldb, n0, N, GB_K, smem + G_BUF_BYTES + G_TILE_BYTES, wid, lane, 0);
+    stage_pieces<T, TR>(B, ldb, n0, N, GB_K, smem + G_BUF_BYTES + G_TILE_BYTES, wid, lane, 2);
     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -189,12 +225,12 @@ __device__ __forceinline__ void mainloop_bk64(const T* __restrict__ A, const T* 
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int s = 0; s < 2; ++s) fb0[j][s] = lds_frag(tb, wc * 64 + j * 16 + lr, s * 4 + lk);
+      for (int s = 0; s < 2; ++s) fb0[j][s] = frag<TR>(tb, wc * 64 + j * 16, s, lr, lk);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int s = 0; s < 2; ++s) fa[i][s] = lds_frag(ta, wr * 128 + i * 16 + lr, s * 4 + lk);
-    if (ld_a) stage_pieces<T>(A, lda, m0, M, (t + 1) * GB_K, oth, wid, lane, 0);
+      for (int s = 0; s < 2; ++s) fa[i][s] = frag<TR>(ta, wr * 128 + i * 16, s, lr, lk);
+    if (ld_a) stage_pieces<T, TR>(A, lda, m0, M, (t + 1) * GB_K, oth, wid, lane, 0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     bar();
     __builtin_amdgcn_s_setprio(1);
@@ -210,8 +246,8 @@ __device__ __forceinline__ void mainloop_bk64(const T* __restrict__ A, const T* 
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int s = 0; s < 2; ++s) fb1[j][s] = lds_frag(tb, wc * 64 + 32 + j * 16 + lr, s * 4 + lk);
-    if (ld_a) stage_pieces<T>(A, lda, m0, M, (t + 1) * GB_K, oth, wid, lane, 2);
+      for (int s = 0; s < 2; ++s) fb1[j][s] = frag<TR>(tb, wc * 64 + 32 + j * 16, s, lr, lk);
+    if (ld_a) stage_pieces<T, TR>(A, lda, m0, M, (t + 1) * GB_K, oth, wid, lane, 2);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     bar();
     __builtin_amdgcn_s_setprio(1);
@@ -227,8 +263,8 @@ __device__ __forceinline__ void mainloop_bk64(const T* __restrict__ A, const T* 
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int s = 0; s < 2; ++s) fa[i][s] = lds_frag(ta, wr * 128 + 64 + i * 16 + lr, s * 4 + lk);
-    if (ld_b) stage_pieces<T>(B, ldb, n0, N, (t + 2) * GB_K, cur + G_TILE_BYTES, wid, lane, 0);
+      for (int s = 0; s < 2; ++s) fa[i][s] = frag<TR>(ta, wr * 128 + 64 + i * 16, s, lr, lk);
+    if (ld_b) stage_pieces<T, TR>(B, ldb, n0, N, (t + 2) * GB_K, cur + G_TILE_BYTES, wid, lane, 0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     bar();
     __builtin_amdgcn_s_setprio(1);
@@ -242,7 +278,7 @@ __device__ __forceinline__ void mainloop_bk64(const T* __restrict__ A, const T* 
     bar();
     // ---------------- p4: stage B(t+2) pieces 2,3; retire A(t+1), B(t+1) ----------------
     if (ld_b) {
-      stage_pieces<T>(B, ldb, n0, N, (t + 2) * GB_K, cur + G_TILE_BYTES, wid, lane, 2);
+      stage_pieces<T, TR>(B, ldb, n0, N, (t + 2) * GB_K, cur + G_TILE_BYTES, wid, lane, 2);
       asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -425,7 +461,7 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[4][8], char* reg, T*
   else body(std::integral_constant<bool, false>{});
 }
 
-template <typename T, int EPI>
+template <typename T, int EPI, bool TR>
 __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(const T* __restrict__ A, const T* __restrict__ B,
                                                             T* __restrict__ C, int M, int N, int K, int64_t lda,
                                                             int64_t ldb, int64_t ldc, const T* __restrict__ bias,
@@ -456,9 +492,27 @@ __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(const T* __restrict_
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  mainloop_bk64<T>(A, B, M, N, K, lda, ldb, m0, n0, smem, wid, wr, wc, lane, acc);
+  if constexpr (TR) {  // split-K slice blockIdx.y: K-rows [y*K, (y+1)*K) of both operands
+    A += (int64_t)blockIdx.y * K * lda;
+    B += (int64_t)blockIdx.y * K * ldb;
+  }
+  mainloop_bk64<T, TR>(A, B, M, N, K, lda, ldb, m0, n0, smem, wid, wr, wc, lane, acc);
   if (wr == 0) bar();  // re-align the groups
   bar();               // every wave is past its last ds_read: LDS is free for the epilogue
+  if constexpr (EPI == EPI_F32) {
+    // fp32 slab (split-K partials): each lane stores its 4 consecutive columns per fragment
+    float* out = part + (int64_t)blockIdx.y * M * ldc;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wc * 64 + j * 16 + 4 * lk;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int m = m0 + wr * 128 + i * 16 + lr;
+        if (m < M && n < N) *reinterpret_cast<f32x4*>(out + (int64_t)m * ldc + n) = acc[j][i];
+      }
+    }
+    return;
+  }
 
   epilogue<T, EPI, GB_M, GB_N>(acc, smem + wid * 16384, C, M, N, ldc, bias, aux, ldaux, aux_out, part, m0, n0, tm, wr,
                                 wc, lane);
@@ -493,10 +547,10 @@ __global__ void __launch_bounds__(256) transpose_kernel(const T* __restrict__ in
   }
 }
 
-template <typename T, int EPI>
+template <typename T, int EPI, bool TR = false>
 void launch_gemm(const GemmArgs& g, hipStream_t s) {
   const int tiles = ((g.M + GB_M - 1) / GB_M) * ((g.N + GB_N - 1) / GB_N);
-  hipLaunchKernelGGL((gemm_nt_kernel<T, EPI>), dim3(tiles), dim3(G_THREADS), 0, s, (const T*)g.A, (const T*)g.B,
+  hipLaunchKernelGGL((gemm_nt_kernel<T, EPI, TR>), dim3(tiles, TR ? g.splits : 1), dim3(G_THREADS), 0, s, (const T*)g.A, (const T*)g.B,
                      (T*)g.C, g.M, g.N, g.K, g.lda, g.ldb, g.ldc, (const T*)g.bias, (const T*)g.aux, g.ldaux,
                      (T*)g.aux_out, g.part);
 }
@@ -528,6 +582,28 @@ int gemm_nt(const GemmArgs& g, int dt, hipStream_t s) {
   if (dt == kBF16Code) return gemm_dispatch<bf16>(g, s);
   if (dt == kF16Code) return gemm_dispatch<f16>(g, s);
   return -1;
+}
+
+bool gemm_tt_supported(int P, int Q, int R, int splits, int64_t lda, int64_t ldb) {
+  return P > 0 && Q > 0 && splits > 0 && P % GB_M == 0 && Q % GB_N == 0 && R % (splits * GB_K) == 0 &&
+         lda % 8 == 0 && ldb % 8 == 0;
+}
+
+int gemm_tt(const GemmArgs& g, int dt, hipStream_t s) {
+  // C[P=M, Q=N] (+)= sum_r A[r, p] B[r, q]; g.K = contraction rows per split; g.part = fp32 slabs
+  // [splits, M, N] when g.epi == EPI_F32, else g.C in the operand dtype (splits must be 1)
+  if (!gemm_tt_supported(g.M, g.N, g.K * g.splits, g.splits, g.lda, g.ldb)) return -2;
+  if (g.epi != EPI_F32 && (g.epi != EPI_NONE || g.splits != 1)) return -3;
+  if (dt == kBF16Code) {
+    if (g.epi == EPI_F32) launch_gemm<bf16, EPI_F32, true>(g, s);
+    else launch_gemm<bf16, EPI_NONE, true>(g, s);
+  } else if (dt == kF16Code) {
+    if (g.epi == EPI_F32) launch_gemm<f16, EPI_F32, true>(g, s);
+    else launch_gemm<f16, EPI_NONE, true>(g, s);
+  } else {
+    return -1;
+  }
+  return (int)hipGetLastError();
 }
 
 int gemm_bias_grad(const float* part, int parts, int N, void* out, int odt, hipStream_t s) {

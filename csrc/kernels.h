@@ -167,7 +167,7 @@ int xentropy_bwd(const void* dloss, int64_t dloss_stride, int dloss_dt, const vo
                  float smoothing, int64_t ignore_index, int dt, hipStream_t s);
 
 // ----------------------------- MFMA GEMM (gemm.hip) ------------------------
-enum GemmEpi : int { EPI_NONE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_DGELU = 3, EPI_RESID = 4 };
+enum GemmEpi : int { EPI_NONE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_DGELU = 3, EPI_RESID = 4, EPI_F32 = 5 };
 struct GemmArgs {
   const void* A;  // [M, K] row-major, lda
   const void* B;  // [N, K] row-major, ldb
@@ -180,10 +180,14 @@ struct GemmArgs {
   void* aux_out;     // [M, N], ldc    EPI_BIAS_GELU (pre-activation H)
   float* part;       // [gemm_part_rows(M), N] fp32  EPI_DGELU (bias-grad partials)
   int epi;
+  int splits;        // gemm_tt: split-K slices (blockIdx.y)
 };
 bool gemm_supported(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc);
 int64_t gemm_part_rows(int M);
 int gemm_nt(const GemmArgs& g, int dt, hipStream_t s);
+// weight-gradient form: C[P, Q] = A^T B with A [R, P], B [R, Q] row-major (contraction over rows)
+bool gemm_tt_supported(int P, int Q, int R, int splits, int64_t lda, int64_t ldb);
+int gemm_tt(const GemmArgs& g, int dt, hipStream_t s);
 int gemm_bias_grad(const float* part, int parts, int N, void* out, int odt, hipStream_t s);
 int transpose_2d(const void* in, void* out, int R, int C, int dt, hipStream_t s);
 

@@ -121,3 +121,29 @@ def test_gemm_supported_rejects():
                                 torch.randn(16, 96, device=DEV).bfloat16())  # K % 64
     assert not C.gemm_supported(a.float(), torch.randn(16, 128, device=DEV))  # fp32
     assert C.gemm_supported(a, torch.randn(16, 128, device=DEV).bfloat16())
+
+
+@pytest.mark.parametrize("R,P,Q,splits", [(256, 256, 256, 1), (1024, 256, 512, 2), (2048, 512, 256, 4),
+                                          (8192, 1024, 1024, 8)])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_gemm_tt_weight_grad(R, P, Q, splits, dt):
+    """dW = dY^T X through the transposed-read (ds_read_b64_tr_b16) main loop, split-K slabs."""
+    C = _C()
+    torch.manual_seed(R + P + Q)
+    dy = torch.randn(R, P, device=DEV).to(dt)
+    x = torch.randn(R, Q, device=DEV).to(dt)
+    assert C.gemm_tt_supported(dy, x, splits)
+    ref = dy.float().t() @ x.float()
+    out = C.gemm_tt(dy, x, splits, dt)
+    assert out.shape == (P, Q) and out.dtype == dt
+    _close(out, ref, 1e-2)
+    out32 = C.gemm_tt(dy, x, splits, torch.float32)
+    _close(out32, ref, 1e-4)
+
+
+def test_gemm_tt_asymmetric_identity():
+    C = _C()
+    n = 256
+    a = torch.eye(n, device=DEV, dtype=torch.bfloat16)  # [R=n, P=n]
+    b = (torch.arange(n * n, device=DEV).reshape(n, n) % 89).to(torch.bfloat16)  # [R, Q]
+    torch.testing.assert_close(C.gemm_tt(a, b, 1, torch.bfloat16).float(), b.float(), rtol=0, atol=0)

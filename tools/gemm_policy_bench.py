@@ -20,6 +20,7 @@ def r(*s):
 
 def main():
     import apex._ext as e
+    from apex.ops.fused import _wgrad
 
     C = e.require()
     M = int(os.environ.get("PB_M", 32768))
@@ -43,6 +44,15 @@ def main():
         "ffn1_dgrad_resid": {"lib": lambda: torch.addmm(dres, dh, w1), "mfma": lambda: C.gemm(dh, w1T, 4, None, dres),
                              "lib_mm_add": lambda: torch.mm(dh, w1).add_(dres)},
         "transpose_w1": {"mfma": lambda: C.transpose(w1)},
+        "wgrad_qkv": {"lib": lambda: _wgrad(dqkv, x), "mfma_s2": lambda: C.gemm_tt(dqkv, x, 2, torch.bfloat16),
+                      "mfma_s4": lambda: C.gemm_tt(dqkv, x, 4, torch.bfloat16)},
+        "wgrad_o": {"lib": lambda: _wgrad(dt, o), "mfma_s4": lambda: C.gemm_tt(dt, o, 4, torch.bfloat16),
+                    "mfma_s8": lambda: C.gemm_tt(dt, o, 8, torch.bfloat16),
+                    "mfma_s16": lambda: C.gemm_tt(dt, o, 16, torch.bfloat16)},
+        "wgrad_1": {"lib": lambda: _wgrad(dh, x), "mfma_s2": lambda: C.gemm_tt(dh, x, 2, torch.bfloat16),
+                    "mfma_s4": lambda: C.gemm_tt(dh, x, 4, torch.bfloat16)},
+        "wgrad_2": {"lib": lambda: _wgrad(dt, g), "mfma_s2": lambda: C.gemm_tt(dt, g, 2, torch.bfloat16),
+                    "mfma_s4": lambda: C.gemm_tt(dt, g, 4, torch.bfloat16)},
     }
     for name, vs in cases.items():
         best = {k: 1e30 for k in vs}
