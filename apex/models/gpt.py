@@ -18,6 +18,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from ..normalization import FusedLayerNorm
+from ..ops import blocks as fblocks
 from ..ops import fused as fops
 
 
@@ -69,8 +70,12 @@ class GPTBlock(nn.Module):
         qkv = fops.fused_dense(self.ln_1(x), self.c_attn.weight, self.c_attn.bias).view(B, S, 3, self.h, self.d)
         ctx = fops.attention_qkv_packed(qkv, None, p, causal=True).reshape(B, S, E)
         x = fops.bias_dropout_add(fops.fused_dense(ctx, self.c_proj.weight, None), self.c_proj.bias, x, p)
-        h = fops.dense_act(self.ln_2(x), self.c_fc.weight, self.c_fc.bias, fops.ACT_GELU_TANH)
-        return fops.bias_dropout_add(fops.fused_dense(h, self.mlp_proj.weight, None), self.mlp_proj.bias, x, p)
+        xn = self.ln_2(x)
+        t = fblocks.mlp(xn, self.c_fc.weight, self.c_fc.bias, self.mlp_proj.weight, fops.ACT_GELU_TANH)
+        if t is None:
+            h = fops.dense_act(xn, self.c_fc.weight, self.c_fc.bias, fops.ACT_GELU_TANH)
+            t = fops.fused_dense(h, self.mlp_proj.weight, None)
+        return fops.bias_dropout_add(t, self.mlp_proj.bias, x, p)
 
 
 class GPTModel(nn.Module):

@@ -20,6 +20,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from ..normalization import FusedLayerNorm
+from ..ops import blocks as fblocks
 from ..ops import fused as fops
 from ..transformer import parallel_state as ps
 from ..transformer import tensor_parallel as tp
@@ -84,9 +85,17 @@ class ParallelTransformerLayer(nn.Module):
         ctx = fops.attention_qkv_packed(qkv, None, pa, causal=True)
         out, bias = self.dense(ctx.reshape(B, S, -1))
         x = fops.bias_dropout_add(out, bias, x, ph)
-        h, b1 = self.dense_h_to_4h(self.post_attention_layernorm(x))
+        xn = self.post_attention_layernorm(x)
+        f1, f2 = self.dense_h_to_4h, self.dense_4h_to_h
+        if not (f1.sequence_parallel_enabled or f2.sequence_parallel_enabled) and f1.bias is not None:
+            # whole MLP shard as one Function (GEMM+bias+GELU epilogue, dGELU epilogue in backward)
+            # between the same TP mappings the two parallel linears apply
+            t = fblocks.mlp(tp.copy_to_tensor_model_parallel_region(xn), f1.weight, f1.bias, f2.weight)
+            if t is not None:
+                return fops.bias_dropout_add(tp.reduce_from_tensor_model_parallel_region(t), f2.bias, x, ph)
+        h, b1 = f1(xn)
         h = fops.bias_gelu(h, b1) if b1 is not None else F.gelu(h)
-        out, bias = self.dense_4h_to_h(h)
+        out, bias = f2(h)
         return fops.bias_dropout_add(out, bias, x, ph)
 
 

@@ -106,6 +106,42 @@ class _FFNSublayer(torch.autograd.Function):
                 dbeta, None, None, None)
 
 
+class _MLP(torch.autograd.Function):
+    """gelu(x W1^T + b1) W2^T (the second bias is left to the caller's bias+dropout+residual
+    kernel): one MFMA GEMM with bias+GELU in its epilogue, then the output GEMM; backward is
+    the output-gradient GEMM with the dGELU + bias-grad epilogue, the input-gradient GEMM and
+    the two weight gradients."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, act):
+        x2 = _2d(x)
+        g, h = G.linear_gelu(x2, w1, b1, act)
+        t = G.linear(g, w2)
+        ctx.save_for_backward(x2, w1, h, g, w2)
+        ctx.act = act
+        ctx.b1dt = b1.dtype
+        return t.view(*x.shape[:-1], w2.shape[0])
+
+    @staticmethod
+    def backward(ctx, dt):
+        x2, w1, h, g, w2 = ctx.saved_tensors
+        dt2 = _2d(dt).contiguous()
+        dh, db1 = G.dgrad_dgelu(dt2, w2, h, ctx.b1dt, act=ctx.act)
+        dw2 = _wgrad(dt2, g)
+        dx = G.dgrad(dh, w1).view(*dt.shape[:-1], w1.shape[1])
+        dw1 = _wgrad(dh, x2)
+        return dx, dw1, db1, dw2, None
+
+
+def mlp(x, w1, b1, w2, act=ACT_GELU):
+    """gelu(x W1^T + b1) W2^T for GELU (act 0) / tanh-GELU (act 1) MLPs; None when the fused
+    path does not apply (caller composes the ops)."""
+    if not (_ext.use_native(x) and x.dtype in (torch.float16, torch.bfloat16) and b1 is not None and
+            act in (0, 1) and w1.dtype == x.dtype and w2.dtype == x.dtype and b1.dtype == x.dtype):
+        return None
+    return _MLP.apply(x, w1, b1, w2, int(act))
+
+
 def _ok(x, *dims):
     return _ext.use_native(x) and x.dtype in (torch.float16, torch.bfloat16) and x.is_contiguous() and \
         all(d % 8 == 0 for d in dims) and _ext.require().bdaln_supported(x.shape[-1])

@@ -146,9 +146,9 @@ class _DenseAct(torch.autograd.Function):
 
         C = _ext.require()
         x2 = _2d(x)
-        if act == ACT_GELU and b is not None and G.use_mfma(x2, w) and b.dtype == x2.dtype:
+        if act in (ACT_GELU, ACT_GELU_TANH) and b is not None and G.use_mfma(x2, w) and b.dtype == x2.dtype:
             # one MFMA GEMM with bias+GELU in the epilogue; h (with bias) kept for backward
-            y, h = G.linear_gelu(x2, w, b)
+            y, h = G.linear_gelu(x2, w, b, act)
             ctx.save_for_backward(x2, w, h, None)
             ctx.bdtype = b.dtype
         else:

@@ -78,16 +78,18 @@ def linear(x, w, b=None):
     return y.view(*x.shape[:-1], w.shape[0])
 
 
-def linear_gelu(x, w, b):
-    """(gelu(h), h) with h = x w^T + b (erf GELU); h is kept for the backward."""
+ACT_GELU, ACT_GELU_TANH = 0, 1  # apex.ops.fused activation codes
+
+
+def linear_gelu(x, w, b, act=ACT_GELU):
+    """(gelu(h), h) with h = x w^T + b (erf GELU, or tanh GELU for act=1); h kept for backward."""
     a = _2d(x)
+    C = _C()
     if use_mfma(a, w) and b is not None and b.dtype == x.dtype:
-        C = _C()
-        y, h = C.gemm(a, w, C.EPI_BIAS_GELU, b)
+        y, h = C.gemm(a, w, C.EPI_BIAS_GELU_TANH if act == ACT_GELU_TANH else C.EPI_BIAS_GELU, b)
     else:
-        C = _C()
         h = torch.mm(a, w.t())
-        y = C.bias_act_fwd(h, b, 0)
+        y = C.bias_act_fwd(h, b, act)
         h = h + b if b is not None else h  # the pre-activation as the fused path stores it
     shp = (*x.shape[:-1], w.shape[0])
     return y.view(shp), h.view(shp)
@@ -118,18 +120,18 @@ def dgrad_resid(dy, w, r, wT=None):
     return torch.addmm(r2, a, w).view(*dy.shape[:-1], w.shape[1])
 
 
-def dgrad_dgelu(dy, w, h, bias_dtype, wT=None):
+def dgrad_dgelu(dy, w, h, bias_dtype, wT=None, act=ACT_GELU):
     """(dh, db): dh = (dy @ w) * gelu'(h), db = column sums of dh (in bias_dtype)."""
     a = _2d(dy)
     h2 = _2d(h)
+    C = _C()
     if _MODE != "blas" and a.is_cuda and h2.is_contiguous() and h2.dtype == a.dtype:
         wT = transpose(w) if wT is None else wT
         if use_mfma(a, wT):
-            C = _C()
-            dh, db = C.gemm(a, wT, C.EPI_DGELU, None, h2, bias_dtype)
+            epi = C.EPI_DGELU_TANH if act == ACT_GELU_TANH else C.EPI_DGELU
+            dh, db = C.gemm(a, wT, epi, None, h2, bias_dtype)
             return dh, db
-    C = _C()
     dg = torch.mm(a, w)
-    dh, _ = C.bias_act_bwd(dg, h2, None, 0)
+    dh, _ = C.bias_act_bwd(dg, h2, None, act)
     db = C.colsum(dh, bias_dtype) if bias_dtype is not None else None
     return dh, db

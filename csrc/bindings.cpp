@@ -786,30 +786,33 @@ std::vector<Tensor> k_gemm(Tensor a, Tensor b, int64_t epi, const c10::optional<
   g.ldc = N;
   g.epi = (int)epi;
   Tensor extra;
-  if (epi == apex::EPI_BIAS || epi == apex::EPI_BIAS_GELU) {
+  const bool gelu_fwd = epi == apex::EPI_BIAS_GELU || epi == apex::EPI_BIAS_GELU_TANH;
+  const bool dgelu = epi == apex::EPI_DGELU || epi == apex::EPI_DGELU_TANH;
+  TORCH_CHECK(epi >= 0 && epi <= apex::EPI_DGELU_TANH && epi != apex::EPI_F32, "gemm: bad epilogue ", epi);
+  if (epi == apex::EPI_BIAS || gelu_fwd) {
     TORCH_CHECK(bias.has_value() && bias->defined() && bias->is_contiguous() && bias->numel() == N &&
                     bias->scalar_type() == a.scalar_type(),
                 "gemm: bias must be a contiguous [N] tensor of the operand dtype");
     g.bias = bias->data_ptr();
   }
-  if (epi == apex::EPI_BIAS_GELU) {
+  if (gelu_fwd) {
     extra = at::empty(osz, a.options());
     g.aux_out = extra.data_ptr();
   }
   Tensor part;
-  if (epi == apex::EPI_DGELU || epi == apex::EPI_RESID) {
+  if (dgelu || epi == apex::EPI_RESID) {
     TORCH_CHECK(aux.has_value() && aux->defined() && aux->scalar_type() == a.scalar_type() &&
                     aux->numel() == M * N && aux->stride(-1) == 1 && aux->is_contiguous(),
                 "gemm: aux must be a contiguous [M, N] tensor of the operand dtype");
     g.aux = aux->data_ptr();
     g.ldaux = N;
   }
-  if (epi == apex::EPI_DGELU) {
+  if (dgelu) {
     part = at::empty({apex::gemm_part_rows((int)M), N}, a.options().dtype(at::kFloat));
     g.part = part.data_ptr<float>();
   }
   check(apex::gemm_nt(g, dt_code(a.scalar_type()), cur_stream()), "gemm");
-  if (epi == apex::EPI_DGELU && bias_grad_dtype.has_value()) {
+  if (dgelu && bias_grad_dtype.has_value()) {
     extra = at::empty({N}, a.options().dtype(*bias_grad_dtype));
     check(apex::gemm_bias_grad(part.data_ptr<float>(), (int)part.size(0), (int)N, extra.data_ptr(),
                                dt_code(*bias_grad_dtype), cur_stream()),
@@ -930,4 +933,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.attr("EPI_BIAS_GELU") = (int)apex::EPI_BIAS_GELU;
   m.attr("EPI_DGELU") = (int)apex::EPI_DGELU;
   m.attr("EPI_RESID") = (int)apex::EPI_RESID;
+  m.attr("EPI_BIAS_GELU_TANH") = (int)apex::EPI_BIAS_GELU_TANH;
+  m.attr("EPI_DGELU_TANH") = (int)apex::EPI_DGELU_TANH;
 }

@@ -14,6 +14,7 @@
 //   EPI_DGELU     C = acc * gelu'(H[m,n])   and per-(256-row tile, wave row) column partial sums
 //                 of C written to `part` (the bias gradient, finished by partial_colsum)
 //   EPI_RESID     C = acc + R[m,n]          (residual-gradient accumulation)
+//   EPI_BIAS_GELU_TANH / EPI_DGELU_TANH: the same with the tanh-approximated GELU (GPT-2)
 //
 // Tiling (CDNA4, cdna_hip_programming.md §5):
 //  * 256x256 output tile, BK = 64, 512 threads = 8 waves as 2 (M) x 4 (N); each wave owns a
@@ -88,6 +89,18 @@ __device__ __forceinline__ f32x2 exp_neg_half_sq2(f32x2 x) {
 __device__ __forceinline__ f32x2 gelu2(f32x2 x) {
   const f32x2 c = erf2(x * splat(0.70710678118654752f), exp_neg_half_sq2(x));
   return splat(0.5f) * x * (splat(1.f) + c);
+}
+// tanh-approximated GELU (GPT-2): x * sigmoid(2u), u = sqrt(2/pi) (x + 0.044715 x^3)
+__device__ __forceinline__ f32x2 sig2u(f32x2 x) {
+  const f32x2 u = splat(-2.f * 0.7978845608028654f * 1.4426950408889634f) * pk_fma(splat(0.044715f) * x, x * x, x);
+  const f32x2 d = splat(1.f) + f32x2{__builtin_amdgcn_exp2f(u[0]), __builtin_amdgcn_exp2f(u[1])};
+  return f32x2{__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+}
+__device__ __forceinline__ f32x2 gelu_tanh2(f32x2 x) { return x * sig2u(x); }
+__device__ __forceinline__ f32x2 gelu_tanh_grad2(f32x2 x) {
+  const f32x2 sg = sig2u(x);
+  const f32x2 du = splat(2.f * 0.7978845608028654f) * pk_fma(splat(3.f * 0.044715f) * x, x, splat(1.f));
+  return pk_fma(x * sg * (splat(1.f) - sg), du, sg);
 }
 __device__ __forceinline__ f32x2 gelu_grad2(f32x2 x) {
   const f32x2 e = exp_neg_half_sq2(x);
@@ -373,14 +386,17 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[4][8], char* reg, T*
   auto body = [&](auto full_tag) {
     constexpr bool F = decltype(full_tag)::value;
     float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
+    constexpr bool GELU_FWD = EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_TANH;
+    constexpr bool DGELU = EPI == EPI_DGELU || EPI == EPI_DGELU_TANH;
+    constexpr bool TANH = EPI == EPI_BIAS_GELU_TANH || EPI == EPI_DGELU_TANH;
+    if constexpr (EPI == EPI_BIAS || GELU_FWD) {
       u32x4 braw;
       if constexpr (F) braw = *reinterpret_cast<const u32x4*>(bias + ncol);
       else braw = ld16(bias, 0, 0);  // (bias is [N]: row 0 of a 1-row tensor)
       unpack(braw, bv);
     }
     u32x4 ra[16];
-    if constexpr (EPI == EPI_DGELU || EPI == EPI_RESID) {
+    if constexpr (DGELU || EPI == EPI_RESID) {
 #pragma unroll
       for (int it = 0; it < 16; ++it) {
         const int m = mrow + it * 8;
@@ -399,7 +415,7 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[4][8], char* reg, T*
         if constexpr (EPI == EPI_BIAS) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += bv[e];
-        } else if constexpr (EPI == EPI_BIAS_GELU) {
+        } else if constexpr (GELU_FWD) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += bv[e];
           const u32x4 hraw = pack(v);
@@ -408,7 +424,7 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[4][8], char* reg, T*
           unpack(hraw, v);  // GELU of the stored pre-activation
 #pragma unroll
           for (int e = 0; e < 8; e += 2) {
-            const f32x2 gv = gelu2(f32x2{v[e], v[e + 1]});
+            const f32x2 gv = TANH ? gelu_tanh2(f32x2{v[e], v[e + 1]}) : gelu2(f32x2{v[e], v[e + 1]});
             v[e] = gv[0];
             v[e + 1] = gv[1];
           }
@@ -418,8 +434,8 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[4][8], char* reg, T*
           const bool ok = F || (m < M && ncol < N);
 #pragma unroll
           for (int e = 0; e < 8; e += 2) {
-            if constexpr (EPI == EPI_DGELU) {
-              const f32x2 gg = gelu_grad2(f32x2{x[e], x[e + 1]});
+            if constexpr (DGELU) {
+              const f32x2 gg = TANH ? gelu_tanh_grad2(f32x2{x[e], x[e + 1]}) : gelu_grad2(f32x2{x[e], x[e + 1]});
               v[e] = ok ? v[e] * gg[0] : 0.f;
               v[e + 1] = ok ? v[e + 1] * gg[1] : 0.f;
             } else {
@@ -429,7 +445,7 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[4][8], char* reg, T*
           }
         }
         out = pack(v);
-        if constexpr (EPI == EPI_DGELU) {
+        if constexpr (DGELU) {
           float r[8];
           unpack(out, r);  // the bias grad sums the stored (rounded) values
 #pragma unroll
@@ -439,7 +455,7 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[4][8], char* reg, T*
       if constexpr (F) *reinterpret_cast<u32x4*>(C + (int64_t)m * ldc + ncol) = out;
       else st16(C, m, out);
     }
-    if constexpr (EPI == EPI_DGELU) {
+    if constexpr (DGELU) {
       // lanes l, l^8, l^16, ... share the column chunk: reduce over the wave's 8 row slots
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -562,6 +578,8 @@ int gemm_dispatch(const GemmArgs& g, hipStream_t s) {
     case EPI_BIAS: launch_gemm<T, EPI_BIAS>(g, s); break;
     case EPI_BIAS_GELU: launch_gemm<T, EPI_BIAS_GELU>(g, s); break;
     case EPI_DGELU: launch_gemm<T, EPI_DGELU>(g, s); break;
+    case EPI_BIAS_GELU_TANH: launch_gemm<T, EPI_BIAS_GELU_TANH>(g, s); break;
+    case EPI_DGELU_TANH: launch_gemm<T, EPI_DGELU_TANH>(g, s); break;
     case EPI_RESID: launch_gemm<T, EPI_RESID>(g, s); break;
     default: return -3;
   }

@@ -167,7 +167,8 @@ int xentropy_bwd(const void* dloss, int64_t dloss_stride, int dloss_dt, const vo
                  float smoothing, int64_t ignore_index, int dt, hipStream_t s);
 
 // ----------------------------- MFMA GEMM (gemm.hip) ------------------------
-enum GemmEpi : int { EPI_NONE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_DGELU = 3, EPI_RESID = 4, EPI_F32 = 5 };
+enum GemmEpi : int { EPI_NONE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_DGELU = 3, EPI_RESID = 4, EPI_F32 = 5,
+                     EPI_BIAS_GELU_TANH = 6, EPI_DGELU_TANH = 7 };
 struct GemmArgs {
   const void* A;  // [M, K] row-major, lda
   const void* B;  // [N, K] row-major, ldb

@@ -147,3 +147,43 @@ def test_gemm_tt_asymmetric_identity():
     a = torch.eye(n, device=DEV, dtype=torch.bfloat16)  # [R=n, P=n]
     b = (torch.arange(n * n, device=DEV).reshape(n, n) % 89).to(torch.bfloat16)  # [R, Q]
     torch.testing.assert_close(C.gemm_tt(a, b, 1, torch.bfloat16).float(), b.float(), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 1600, 1600), (2048, 4096, 1024)])
+def test_gemm_tanh_gelu_epilogues(M, N, K):
+    C = _C()
+    a = (torch.randn(M, K, device=DEV) / K ** 0.5).bfloat16()
+    b = torch.randn(N, K, device=DEV).bfloat16()
+    bias = torch.randn(N, device=DEV).bfloat16()
+    y, h = C.gemm(a, b, C.EPI_BIAS_GELU_TANH, bias)
+    href = _ref_mm(a, b) + bias.float()
+    _close(h, href, 1e-2)
+    _close(y, F.gelu(href, approximate="tanh"), 1.5e-2)
+    hh = torch.randn(M, N, device=DEV).bfloat16()
+    bt = (torch.randn(N, K, device=DEV) / K ** 0.5).bfloat16()
+    dh, db = C.gemm(a, bt, C.EPI_DGELU_TANH, None, hh, torch.float32)
+    hr = hh.float().requires_grad_(True)
+    F.gelu(hr, approximate="tanh").backward(_ref_mm(a, bt))
+    _close(dh, hr.grad, 1.5e-2)
+    torch.testing.assert_close(db, dh.float().sum(0), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("act", [0, 1])
+def test_mlp_block_matches_composition(act):
+    """apex.ops.blocks.mlp (fused epilogues) vs F.linear / F.gelu in fp32 on the same bf16 inputs."""
+    from apex.ops import blocks
+
+    torch.manual_seed(act)
+    x = torch.randn(4, 256, 512, device=DEV).bfloat16().requires_grad_(True)
+    w1 = (torch.randn(2048, 512, device=DEV) * 0.03).bfloat16().requires_grad_(True)
+    b1 = (torch.randn(2048, device=DEV) * 0.1).bfloat16().requires_grad_(True)
+    w2 = (torch.randn(512, 2048, device=DEV) * 0.03).bfloat16().requires_grad_(True)
+    y = blocks.mlp(x, w1, b1, w2, act)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    ref = [t.detach().float().requires_grad_(True) for t in (x, w1, b1, w2)]
+    yr = F.linear(F.gelu(F.linear(ref[0], ref[1], ref[2]), approximate="tanh" if act else "none"), ref[3])
+    yr.backward(dy.float())
+    _close(y, yr, 2e-2)
+    for got, r in zip((x, w1, b1, w2), ref):
+        _close(got.grad, r.grad, 3e-2)
