@@ -206,7 +206,11 @@ __device__ __forceinline__ s16x8 frag(const char* tile, int rb, int s, int lr, i
 // stages, no ping-pong; profiles/r1_gemm_*_2wg_variant.jsonl) — its epilogue does overlap the
 // other workgroup's MFMAs (K = 64: 55 vs 65 us at N = 4096) but the main loop is ~60 % slower;
 // two phases per K-tile with the whole tile read in the first R section (half the barriers, next
-// loads 4 sections ahead, 256 VGPRs; profiles/r1_gemm_ksweep_2phase.jsonl) — within 1 %. rocprof on the 32768x1024x4096 case: MFMA busy 65 %
+// loads 4 sections ahead, 256 VGPRs; profiles/r1_gemm_ksweep_2phase.jsonl) — within 1 %.
+// hipBLASLt's kernel on the same shape (rocprof): one wave per SIMD with 128x128 wave tiles (256
+// AGPR accumulators), 74 % MFMA busy vs 64 % here. That geometry in HIP source (fragments
+// software-pipelined under 64-MFMA halves) makes hipcc shuffle ~220 accumulator copies
+// (v_accvgpr_read/write) per K-tile through the loop-carried phis, so it is not used. rocprof on the 32768x1024x4096 case: MFMA busy 65 %
 // of SIMD cycles at 1.98 GHz, zero LDS bank conflicts.
 template <typename T, bool TR>
 __device__ __forceinline__ void mainloop_bk64(const T* __restrict__ A, const T* __restrict__ B, int M, int N, int K,
