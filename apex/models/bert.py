@@ -73,6 +73,9 @@ class BertEmbeddings(nn.Module):
 
     def forward(self, input_ids, token_type_ids):
         S = input_ids.shape[1]
+        if S > self.position_embeddings.num_embeddings:  # host-side check (a bad gather faults the GPU)
+            raise ValueError(f"sequence length {S} exceeds max_position_embeddings="
+                             f"{self.position_embeddings.num_embeddings}")
         pos = torch.arange(S, device=input_ids.device)
         x = self.word_embeddings(input_ids) + self.position_embeddings(pos)[None] + \
             self.token_type_embeddings(token_type_ids)

@@ -101,6 +101,8 @@ class GPTModel(nn.Module):
 
     def forward(self, input_ids, labels=None):
         B, S = input_ids.shape
+        if S > self.config.n_positions:  # host-side check: an out-of-range gather faults the GPU
+            raise ValueError(f"sequence length {S} exceeds n_positions={self.config.n_positions}")
         pos = torch.arange(S, device=input_ids.device)
         x = self.wte(input_ids) + self.wpe(pos)[None]
         x = F.dropout(x, self.config.dropout, self.training)

@@ -131,6 +131,9 @@ class MegatronGPT(nn.Module):
     def forward(self, input_ids, labels=None):
         if self.pre_process:
             S = input_ids.shape[1]
+            if S > self.config.max_position_embeddings:  # host-side check (a bad gather faults the GPU)
+                raise ValueError(f"sequence length {S} exceeds max_position_embeddings="
+                                 f"{self.config.max_position_embeddings}")
             pos = torch.arange(S, device=input_ids.device)
             x = self.word_embeddings(input_ids) + self.position_embeddings(pos)[None]
             x = F.dropout(x, self.config.hidden_dropout, self.training)

@@ -51,6 +51,17 @@ def _is_rccl(group=None) -> bool:
         return False
 
 
+def _dense_non_overlapping(t) -> bool:
+    """True when t's elements exactly fill numel() slots in some dimension order (e.g. a
+    channels_last conv weight), so a bucket slice can carry t's own strides."""
+    expected = 1
+    for stride, size in sorted((st, sz) for st, sz in zip(t.stride(), t.shape) if sz != 1):
+        if stride != expected:
+            return False
+        expected *= size
+    return True
+
+
 def _flatten(tensors):
     return torch.cat([t.contiguous().view(-1) for t in tensors]) if len(tensors) > 1 else \
         tensors[0].contiguous().view(-1).clone()
@@ -390,7 +401,7 @@ class DistributedDataParallel(Module):
             for i in idxs:
                 p = self._params[i]
                 n = p.numel()
-                if p.is_contiguous() or not p.is_non_overlapping_and_dense():
+                if p.is_contiguous() or not _dense_non_overlapping(p):
                     v = flat[off:off + n].view_as(p)
                 else:  # e.g. channels_last conv weight: the grad view keeps the param's strides
                     v = flat[off:off + n].as_strided(p.shape, p.stride())

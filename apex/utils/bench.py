@@ -52,20 +52,26 @@ class DistEnv:
 
 
 def init_distributed(backend=None, device="cuda"):
-    """Read RANK/WORLD_SIZE/LOCAL_RANK (torchrun), bind the GPU, init the process group."""
+    """Read RANK/WORLD_SIZE/LOCAL_RANK (torchrun), bind the GPU, init the process group.
+
+    Rehearsal knobs (not for measurements): ``APEX_DIST_BACKEND`` overrides the backend
+    (e.g. ``gloo``), ``APEX_DIST_SHARE_GPU=1`` binds every rank to device 0, so the multi-rank
+    path (DDP hooks, bucket all-reduces, metric reductions) runs on a one-GPU box."""
     protect_stdout()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("APEX_DIST_BACKEND") or backend
     if device == "cuda":
-        torch.cuda.set_device(local_rank)
-        dev = torch.device("cuda", local_rank)
+        dev_index = 0 if os.environ.get("APEX_DIST_SHARE_GPU", "0") == "1" else local_rank
+        torch.cuda.set_device(dev_index)
+        dev = torch.device("cuda", dev_index)
     else:
         dev = torch.device("cpu")
     if world > 1 and not dist.is_initialized():
         if backend is None:
             backend = "nccl" if dev.type == "cuda" else "gloo"
-        kw = {"device_id": dev} if dev.type == "cuda" else {}
+        kw = {"device_id": dev} if (dev.type == "cuda" and backend == "nccl") else {}
         dist.init_process_group(backend, **kw)
     return DistEnv(rank, world, local_rank, dev)
 

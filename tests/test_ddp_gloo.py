@@ -184,3 +184,45 @@ def test_fused_optimizer_zero_grad_on_ddp_buckets():
     for p in procs:
         p.join(timeout=60)
     assert all(r[1] == "ok" for r in res), res
+
+
+def _channels_last_worker(rank, world, port, q):
+    try:
+        _init(rank, world, port)
+        from apex.parallel import DistributedDataParallel as DDP
+
+        torch.manual_seed(0)
+        net = torch.nn.Sequential(torch.nn.Conv2d(3, 8, 3), torch.nn.ReLU(), torch.nn.Conv2d(8, 4, 1))
+        net = net.to(memory_format=torch.channels_last)
+        model = DDP(net, message_size=100)
+        for i in range(2):
+            model.zero_grad(set_to_none=False)
+            x = torch.randn(2, 3, 6, 6).to(memory_format=torch.channels_last) + rank
+            model(x).sum().backward()
+        w = net[0].weight
+        # the grad is a bucket view that keeps the channels_last strides of its parameter
+        assert w.grad.stride() == w.stride(), (w.grad.stride(), w.stride())
+        ref = [torch.empty_like(w.grad) for _ in range(world)]
+        dist.all_gather(ref, w.grad.contiguous())
+        assert all(torch.equal(ref[0], r) for r in ref)
+        q.put((rank, "ok"))
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ddp_channels_last_params():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_channels_last_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[1] == "ok" for r in res), res
