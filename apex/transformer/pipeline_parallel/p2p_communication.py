@@ -25,6 +25,12 @@ def _communicate(tensor_send_next, tensor_send_prev, recv_prev, recv_next, tenso
     t_next = torch.empty(tensor_shape, dtype=dtype, device=dev, requires_grad=True) if recv_next else None
     ops = []
     group = ps.get_pipeline_model_parallel_group()
+    # the wire format is the agreed (shape, dtype): a stage whose output is wider (amp O2 casts
+    # model outputs to fp32) sends it in the agreed dtype, or the peer's receive size mismatches
+    if tensor_send_prev is not None and tensor_send_prev.dtype != dtype:
+        tensor_send_prev = tensor_send_prev.to(dtype)
+    if tensor_send_next is not None and tensor_send_next.dtype != dtype:
+        tensor_send_next = tensor_send_next.to(dtype)
     if tensor_send_prev is not None:
         ops.append(dist.P2POp(dist.isend, tensor_send_prev.contiguous(), ps.get_pipeline_model_parallel_prev_rank(),
                               group))

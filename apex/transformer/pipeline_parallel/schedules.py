@@ -64,6 +64,8 @@ def backward_step(input_tensor, output_tensor, output_tensor_grad, grad_scaler=N
         input_tensor.retain_grad()
     if output_tensor_grad is None and grad_scaler is not None:
         output_tensor = grad_scaler(output_tensor)
+    if output_tensor_grad is not None and output_tensor_grad.dtype != output_tensor.dtype:
+        output_tensor_grad = output_tensor_grad.to(output_tensor.dtype)  # wire dtype -> output dtype
     torch.autograd.backward(output_tensor, grad_tensors=output_tensor_grad)
     return input_tensor.grad if input_tensor is not None else None
 

@@ -108,6 +108,8 @@ def test_tensor_parallel_layers(world):
 
 
 class _Stage(torch.nn.Module):
+    wide = False  # emit fp64 (wider than the fp32 wire dtype), as amp O2 does with fp32 outputs
+
     def __init__(self, w):
         super().__init__()
         self.lin = torch.nn.Linear(6, 6)
@@ -121,10 +123,11 @@ class _Stage(torch.nn.Module):
 
     def forward(self, x):
         inp = x if self.input_tensor is None else self.input_tensor
-        return torch.tanh(self.lin(inp))
+        out = torch.tanh(self.lin(inp))
+        return out.double() if self.wide else out
 
 
-def _pipeline(rank, world, n_micro):
+def _pipeline(rank, world, n_micro, wide=False):
     from apex.transformer import parallel_state as ps
     from apex.transformer.pipeline_parallel import get_forward_backward_func, setup_microbatch_calculator
 
@@ -136,6 +139,7 @@ def _pipeline(rank, world, n_micro):
     target = torch.randn(n_micro * 2, 6)
     stage = ps.get_pipeline_model_parallel_rank()
     model = _Stage(weights[stage])
+    model.wide = wide
     tgt_chunks = list(target.chunk(n_micro))
     state = {"i": 0}
 
@@ -146,6 +150,7 @@ def _pipeline(rank, world, n_micro):
             state["i"] += 1
 
         def loss_fn(o):
+            o = o.float()
             return F.mse_loss(o, t), {"loss": F.mse_loss(o, t).detach()}
 
         return out, loss_fn
@@ -172,6 +177,11 @@ def _pipeline(rank, world, n_micro):
 @pytest.mark.parametrize("world,n_micro", [(2, 4), (4, 6), (4, 2)])
 def test_pipeline_1f1b_matches_serial(world, n_micro):
     _spawn(_pipeline, world, n_micro)
+
+
+def test_pipeline_stage_output_wider_than_wire_dtype():
+    """A stage whose output dtype differs from the agreed p2p dtype still exchanges correctly."""
+    _spawn(_pipeline, 2, 4, True)
 
 
 def _groups(rank, world):
