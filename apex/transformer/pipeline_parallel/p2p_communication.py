@@ -13,24 +13,32 @@ import torch.distributed as dist
 from .. import parallel_state as ps
 
 
-def _device():
-    if torch.cuda.is_available() and dist.get_backend() == "nccl":
-        return torch.device("cuda", torch.cuda.current_device())
-    return torch.device("cpu")
+def _devices(sent):
+    """(wire device, compute device). RCCL moves device buffers; gloo only host buffers, so a
+    gloo run with GPU activations stages through the host (rehearsals, CPU tests)."""
+    if sent is not None:
+        compute = sent.device
+    elif torch.cuda.is_available() and torch.cuda.is_initialized():
+        compute = torch.device("cuda", torch.cuda.current_device())
+    else:
+        compute = torch.device("cpu")
+    wire = compute if dist.get_backend() == "nccl" else torch.device("cpu")
+    return wire, compute
 
 
 def _communicate(tensor_send_next, tensor_send_prev, recv_prev, recv_next, tensor_shape, dtype):
-    dev = _device()
-    t_prev = torch.empty(tensor_shape, dtype=dtype, device=dev, requires_grad=True) if recv_prev else None
-    t_next = torch.empty(tensor_shape, dtype=dtype, device=dev, requires_grad=True) if recv_next else None
+    sent = tensor_send_next if tensor_send_next is not None else tensor_send_prev
+    dev, compute = _devices(sent)
+    t_prev = torch.empty(tensor_shape, dtype=dtype, device=dev) if recv_prev else None
+    t_next = torch.empty(tensor_shape, dtype=dtype, device=dev) if recv_next else None
     ops = []
     group = ps.get_pipeline_model_parallel_group()
     # the wire format is the agreed (shape, dtype): a stage whose output is wider (amp O2 casts
     # model outputs to fp32) sends it in the agreed dtype, or the peer's receive size mismatches
-    if tensor_send_prev is not None and tensor_send_prev.dtype != dtype:
-        tensor_send_prev = tensor_send_prev.to(dtype)
-    if tensor_send_next is not None and tensor_send_next.dtype != dtype:
-        tensor_send_next = tensor_send_next.to(dtype)
+    if tensor_send_prev is not None:
+        tensor_send_prev = tensor_send_prev.detach().to(device=dev, dtype=dtype)
+    if tensor_send_next is not None:
+        tensor_send_next = tensor_send_next.detach().to(device=dev, dtype=dtype)
     if tensor_send_prev is not None:
         ops.append(dist.P2POp(dist.isend, tensor_send_prev.contiguous(), ps.get_pipeline_model_parallel_prev_rank(),
                               group))
@@ -46,9 +54,9 @@ def _communicate(tensor_send_next, tensor_send_prev, recv_prev, recv_next, tenso
         for r in dist.batch_isend_irecv(ops):
             r.wait()
     if t_prev is not None:
-        t_prev = t_prev.detach().requires_grad_(True)
+        t_prev = t_prev.to(compute).requires_grad_(True)
     if t_next is not None:
-        t_next = t_next.detach()
+        t_next = t_next.to(compute)
     return t_prev, t_next
 
 
