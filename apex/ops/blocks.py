@@ -61,9 +61,12 @@ class _AttnSublayer(torch.autograd.Function):
         q, k, v = qkv.view(B, S, 3, heads, d).unbind(2)
         dqkv = torch.empty_like(qkv)
         dq, dk, dv = dqkv.view(B, S, 3, heads, d).unbind(2)
+        # the attention backward also emits per-sequence column sums of dq/dk/dv (the QKV bias
+        # gradient before the sum over the batch) — no separate pass over dqkv
+        dsum = torch.zeros(B, 3 * E, device=dqkv.device, dtype=torch.float32) if has_bqkv else None
         C.flash_attn_bwd(dctx, q, k, v, o, lse, dq, dk, dv, bool(causal), scale, float(p_attn), sa, oa, k_lens,
-                         dmask)
-        dbqkv = C.colsum(dqkv, bdt) if has_bqkv else None
+                         dmask, dsum)
+        dbqkv = C.partial_colsum(dsum, bdt) if has_bqkv else None
         dx = G.dgrad_resid(dqkv, wqkv, dres)  # residual grad accumulated in the GEMM epilogue
         dwqkv = _wgrad(dqkv, x2)
         return (dx.view(B, S, E), dwqkv, dbqkv, dwo, dbo if has_bo else None, dgamma, dbeta,

@@ -309,7 +309,7 @@ constexpr int kBwdWaves = 4;
 constexpr int kBwdBK = 32 * kBwdWaves;  // 128 keys per workgroup
 constexpr int kBwdBQ = 32;              // queries per inner step
 
-template <typename T, int D, bool CAUSAL, bool DROPOUT>
+template <typename T, int D, bool CAUSAL, bool DROPOUT, bool DSUM>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 64 ? 2 : 1, D == 64 ? 2 : 1))) attn_bwd_kernel(AttnArgs a, const void* dout, float* dq_acc,
                                                          void* dk_out, void* dv_out) {
   using M = MfmaT<T>;
@@ -412,6 +412,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 6
   };
   if (qstart < nq) fetch(qstart);
 
+  float dq_colsum = 0.f;  // DSUM: this lane's dq column (32cb + r) summed over its query rows
   for (int qb = qstart; qb < nq; qb += kBwdBQ) {
     lds_barrier();
     // stage the prefetched tiles; delta = rowsum(dO * O) is computed here from O
@@ -534,26 +535,48 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 6
           const int q = qb + (i & 3) + 8 * (i >> 2) + 4 * hl;
           if (q < nq) {
             if (single_kblock) {  // sole writer of this (b, h) query block: final dtype, strided
-              ((T*)a.dq)[b * a.dq_bs + h * a.dq_hs + (int64_t)q * a.dq_ss + 32 * cb + r] = (T)dq[i];
+              const T v = (T)dq[i];
+              ((T*)a.dq)[b * a.dq_bs + h * a.dq_hs + (int64_t)q * a.dq_ss + 32 * cb + r] = v;
+              if constexpr (DSUM) dq_colsum += (float)v;
             } else {
               atomicAdd(dq_acc + ((int64_t)bh * a.Sq + q) * D + 32 * cb + r, dq[i]);
+              if constexpr (DSUM) dq_colsum += dq[i];
             }
           }
         }
+
       }
     }
   }
   // write dK, dV: element i of block db -> key = k0 + 32wid + (i&3)+8(i>>2)+4hl, dim = 32db + r
   T* dkp = (T*)dk_out + b * a.dk_bs + h * a.dk_hs;
   T* dvp = (T*)dv_out + b * a.dv_bs + h * a.dv_hs;
+  // optional bias-gradient partials: column sums of the stored dq / dk / dv over positions
+  float* dsum = DSUM ? a.dsum + ((int64_t)b * 3 * a.H + h) * D : nullptr;
+  if (DSUM && wid < (D / 32)) {  // the ks == 0 waves own dq column block cb == wid
+    const float t = dq_colsum + __shfl_xor(dq_colsum, 32, 64);
+    if (hl == 0) atomicAdd(dsum + 32 * wid + r, t);
+  }
 #pragma unroll
   for (int db = 0; db < D / 32; ++db) {
+    float sk = 0.f, sv = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int key = k0 + 32 * wid + (i & 3) + 8 * (i >> 2) + 4 * hl;
       if (key < a.Sk) {
-        dkp[(int64_t)key * a.dk_ss + 32 * db + r] = (T)dk[db][i];
-        dvp[(int64_t)key * a.dv_ss + 32 * db + r] = (T)dv[db][i];
+        const T vk = (T)dk[db][i], vv = (T)dv[db][i];
+        dkp[(int64_t)key * a.dk_ss + 32 * db + r] = vk;
+        dvp[(int64_t)key * a.dv_ss + 32 * db + r] = vv;
+        sk += (float)vk;
+        sv += (float)vv;
+      }
+    }
+    if constexpr (DSUM) {
+      sk += __shfl_xor(sk, 32, 64);
+      sv += __shfl_xor(sv, 32, 64);
+      if (hl == 0) {
+        atomicAdd(dsum + (int64_t)a.H * D + 32 * db + r, sk);
+        atomicAdd(dsum + (int64_t)2 * a.H * D + 32 * db + r, sv);
       }
     }
   }
@@ -638,9 +661,9 @@ int attn_bwd(const AttnArgs& a, const void* dout, float* dq_acc, void* dk, void*
   if (multi) hipMemsetAsync(dq_acc, 0, rows * a.D * sizeof(float), s);
   ATTN_DISPATCH(dt, T, ATTN_DISPATCH_D(a.D, D, {
     dim3 grid((a.Sk + kBwdBK - 1) / kBwdBK, a.B * a.H);
-    ATTN_DISPATCH_B(a.causal, C, ATTN_DISPATCH_B(drop, DR,
-        hipLaunchKernelGGL((attn_bwd_kernel<T, D, C, DR>), grid, dim3(256), 0, s, a, dout, dq_acc, dk,
-                           dv)));
+    ATTN_DISPATCH_B(a.causal, C, ATTN_DISPATCH_B(drop, DR, ATTN_DISPATCH_B(a.dsum != nullptr, DS,
+        hipLaunchKernelGGL((attn_bwd_kernel<T, D, C, DR, DS>), grid, dim3(256), 0, s, a, dout, dq_acc, dk,
+                           dv))));
     if (multi) {
       const int64_t tot = rows * (D / 8);
       hipLaunchKernelGGL((attn_dq_convert<T, D>), dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s,

@@ -351,8 +351,14 @@ std::vector<Tensor> flash_attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, do
 void flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor dq,
                     Tensor dk, Tensor dv, bool causal, double scale, double p_drop, int64_t seed,
                     int64_t offset, const c10::optional<Tensor>& k_lens,
-                    const c10::optional<Tensor>& dmask) {
+                    const c10::optional<Tensor>& dmask, const c10::optional<Tensor>& dsum) {
   apex::AttnArgs a = attn_common(q, k, v, causal, scale, p_drop, seed, offset, k_lens);
+  if (dsum.has_value() && dsum->defined()) {
+    TORCH_CHECK(dsum->is_cuda() && dsum->scalar_type() == at::kFloat && dsum->is_contiguous() &&
+                    dsum->numel() == (int64_t)a.B * 3 * a.H * a.D,
+                "flash_attn_bwd: dsum must be a zeroed fp32 [B, 3, H, D] tensor");
+    a.dsum = dsum->data_ptr<float>();
+  }
   a.o = o.data_ptr();
   attn_set(a, o, a.o_bs, a.o_ss, a.o_hs);
   a.lse = lse.data_ptr<float>();
@@ -860,6 +866,17 @@ Tensor k_gemm_tt(Tensor a, Tensor b, int64_t splits, at::ScalarType out_dtype) {
   return k_splitk_reduce(slabs, out_dtype);
 }
 
+// sum the rows of an fp32 [P, N] partials tensor -> [N] in out_dtype
+Tensor k_partial_colsum(Tensor part, at::ScalarType out_dtype) {
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.dim() == 2 && part.is_contiguous(),
+              "partial_colsum: contiguous fp32 [P, N]");
+  Tensor out = at::empty({part.size(1)}, part.options().dtype(out_dtype));
+  check(apex::gemm_bias_grad(part.data_ptr<float>(), (int)part.size(0), (int)part.size(1), out.data_ptr(),
+                             dt_code(out_dtype), cur_stream()),
+        "partial_colsum");
+  return out;
+}
+
 Tensor k_transpose(Tensor x) {
   TORCH_CHECK(x.is_cuda() && x.dim() == 2, "transpose: 2-D device tensor");
   Tensor xc = x.contiguous();
@@ -896,7 +913,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd", &xent_bwd);
   m.def("flash_attn_fwd", &flash_attn_fwd);
-  m.def("flash_attn_bwd", &flash_attn_bwd);
+  m.def("flash_attn_bwd", &flash_attn_bwd, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"),
+        py::arg("o"), py::arg("lse"), py::arg("dq"), py::arg("dk"), py::arg("dv"), py::arg("causal"),
+        py::arg("scale"), py::arg("p_drop"), py::arg("seed"), py::arg("offset"), py::arg("k_lens"),
+        py::arg("dmask"), py::arg("dsum") = py::none());
+  m.def("partial_colsum", &k_partial_colsum);
   m.def("flash_dropout_mask", &flash_dropout_mask);
   m.def("weight_norm_fwd", &k_wn_fwd);
   m.def("weight_norm_bwd", &k_wn_bwd);

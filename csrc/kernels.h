@@ -91,6 +91,8 @@ struct AttnArgs {
   const int* k_lens;     // optional per-batch valid key length
   uint16_t* dmask;       // dropout keep bits [B*H, Sq, mask_words] (fwd writes, bwd reads)
   int64_t mask_words;    // 2 * ceil(Sk / 32)
+  float* dsum;           // optional, zeroed [B][3][H][D]: bwd adds the column sums (over positions)
+                         // of dq, dk, dv — the packed-QKV projection's bias gradient, per batch
 };
 int attn_fwd(const AttnArgs& a, int dt, hipStream_t s);
 bool attn_bwd_needs_dq_acc(const AttnArgs& a);

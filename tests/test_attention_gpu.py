@@ -107,3 +107,26 @@ def test_flash_dropout_matches_masked_reference(causal):
     torch.testing.assert_close(dv, v.grad, rtol=5e-2, atol=5e-2)
     torch.testing.assert_close(dk, k.grad, rtol=5e-2, atol=5e-2)
     torch.testing.assert_close(dq, q.grad, rtol=5e-2, atol=5e-2)
+
+
+@pytest.mark.parametrize("S,causal", [(128, False), (200, False), (256, True)])
+def test_attention_bwd_bias_colsums(S, causal):
+    """flash_attn_bwd's optional dsum output = per-sequence column sums of dq, dk, dv."""
+    import apex._ext as e
+
+    C = e.require()
+    torch.manual_seed(S)
+    B, H, D = 3, 4, 64
+    qkv = torch.randn(B, S, 3, H, D, device="cuda").bfloat16()
+    q, k, v = qkv.unbind(2)
+    scale = D ** -0.5
+    o, lse, dmask = C.flash_attn_fwd(q, k, v, causal, scale, 0.0, 0, 0, None)
+    do = torch.randn_like(o)
+    dqkv = torch.empty_like(qkv)
+    dq, dk, dv = dqkv.unbind(2)
+    dsum = torch.zeros(B, 3 * H * D, device="cuda")
+    C.flash_attn_bwd(do, q, k, v, o, lse, dq, dk, dv, causal, scale, 0.0, 0, 0, None, dmask, dsum)
+    ref = dqkv.float().sum(1).reshape(B, 3 * H * D)
+    torch.testing.assert_close(dsum, ref, rtol=2e-3, atol=2e-2)
+    db = C.partial_colsum(dsum, torch.float32)
+    torch.testing.assert_close(db, ref.sum(0), rtol=2e-3, atol=5e-2)

@@ -59,7 +59,12 @@ def main():
             dq, dk, dv = dqkv.unbind(2)
             t_b = bench(lambda: C.flash_attn_bwd(do, q, k, v, o, lse, dq, dk, dv, causal, scale, p, 1, 2, None,
                                                  dmask))
-            for pas, t, f in (("fwd", t_f, flops), ("bwd", t_b, 2.5 * flops)):
+            dsum = torch.zeros(B, 3 * H * D, device="cuda")
+            t_bs = bench(lambda: C.flash_attn_bwd(do, q, k, v, o, lse, dq, dk, dv, causal, scale, p, 1, 2, None,
+                                                  dmask, dsum))
+            t_cs = bench(lambda: C.colsum(dqkv.view(B * S, 3 * H * D), torch.bfloat16))
+            for pas, t, f in (("fwd", t_f, flops), ("bwd", t_b, 2.5 * flops), ("bwd+dsum", t_bs, 2.5 * flops),
+                              ("separate colsum", t_cs, 0.0)):
                 print(json.dumps({"shape": name, "p": p, "pass": pas, "us": round(t, 1),
                                   "tflops": round(f / t / 1e6, 1)}), flush=True)
 
