@@ -11,7 +11,7 @@ timeout -k 10 300 python __graft_entry__.py smoke > $O/smoke.log 2>&1 || exit 5
 tail -1 $O/smoke.log
 timeout -k 10 400 python bench.py --steps 20 --warmup 5 > $O/bench_mfma.json 2> $O/bench_mfma.err || exit 7
 cat $O/bench_mfma.json
-APEX_GEMM=${AB_MODE:-blas} timeout -k 10 400 python bench.py --steps 20 --warmup 5 > $O/bench_blas.json 2> $O/bench_blas.err || exit 8
+env ${AB_ENV:-APEX_GEMM=blas} timeout -k 10 400 python bench.py --steps 20 --warmup 5 > $O/bench_blas.json 2> $O/bench_blas.err || exit 8
 cat $O/bench_blas.json
 if [ -n "$PROF" ]; then
   cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
