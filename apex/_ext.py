@@ -24,7 +24,17 @@ def _load():
     try:
         import torch  # noqa: F401  (torch must load its HIP runtime first)
 
-        _C = importlib.import_module("apex._C")
+        so = os.environ.get("APEX_EXT_SO")  # A/B runs: load another build of the same module
+        if so:
+            import importlib.util as ilu
+            import sys
+
+            spec = ilu.spec_from_file_location("apex._C", so)
+            _C = ilu.module_from_spec(spec)
+            spec.loader.exec_module(_C)
+            sys.modules["apex._C"] = _C
+        else:
+            _C = importlib.import_module("apex._C")
     except Exception as e:  # pragma: no cover - depends on build state
         _err = e
     return _C

@@ -78,17 +78,34 @@ __device__ __forceinline__ V8 pack8(const float* x) {
   return __builtin_bit_cast(V8, r);
 }
 
-// dropout keep-test for element (row, col) of head `bh`: 16-bit uniforms, 8 per Philox call
+// Attention dropout keep bits: 8-bit uniforms (keep iff u8 >= thresh), 16 per Philox4x32-7
+// call. One call per (row, 16-key half of a 32-key block); the four 32-bit outputs are compared
+// against the threshold four bytes at a time (SWAR: the carry out of u + (256 - thresh) in each
+// byte is the keep bit — u & 0x7f.. plus the low 7 bits of the addend, then the majority of the
+// three top bits), and the carries are shifted into the natural bit order: the returned 16 bits
+// land at positions 4 hl + {0..3, 8..11, 16..19, 24..27}, i.e. bit k of the OR of both halves is
+// key k of the block (random word j = k & 3 of half hl = (k >> 2) & 1, byte k >> 3).
 struct DropGen {
   uint64_t seed, offset;
-  uint32_t thresh;  // keep if r16 >= thresh
-  __device__ __forceinline__ uint4 block(int64_t bh, int64_t row, int64_t col8, int64_t Sq) const {
-    Philox ph(seed, (uint64_t)(bh * Sq + row), offset + (uint64_t)col8);
-    return ph.next();
+  uint32_t thresh;
+  __device__ __forceinline__ uint32_t half_bits(int64_t bh, int64_t row, int64_t blk, int hl, int64_t Sq) const {
+    Philox ph(seed, (uint64_t)(bh * Sq + row), offset + (uint64_t)(2 * blk + hl));
+    const uint4 r = ph.next();
+    const uint32_t C = (256u - thresh) * 0x01010101u;
+    const uint32_t C7 = C & 0x7f7f7f7fu;
+    const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+    uint32_t out = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t u = w[j];
+      const uint32_t s7 = (u & 0x7f7f7f7fu) + C7;
+      const uint32_t carry = ((u & C) | ((u | C) & s7)) & 0x80808080u;  // bit 8b+7: keep of byte b
+      out |= carry >> (7 - j);                                           // -> bit 8b + j
+    }
+    return out << (4 * hl);
   }
-  __device__ __forceinline__ static uint32_t r16(const uint4& r, int idx) {
-    const uint32_t w = idx < 2 ? r.x : idx < 4 ? r.y : idx < 6 ? r.z : r.w;
-    return (idx & 1) ? (w >> 16) : (w & 0xffffu);
+  __device__ __forceinline__ uint32_t block_bits(int64_t bh, int64_t row, int64_t blk, int64_t Sq) const {
+    return half_bits(bh, row, blk, 0, Sq) | half_bits(bh, row, blk, 1, Sq);
   }
 };
 
@@ -104,7 +121,8 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) T lds_k[kFwdKB * LDR];
   __shared__ __attribute__((aligned(16))) T lds_v[kFwdKB * LDR];
 
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  // wid through readfirstlane: wave-uniform in SGPRs, so tile-level conditions become scalar branches
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 31, hl = lane >> 5;
   const int bh = blockIdx.y;
   const int b = bh / a.H, h = bh % a.H;
@@ -136,8 +154,23 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
   // tile loader: 64 x D elements, 16B chunks, CH chunks per thread
   constexpr int CPR = D / 8;               // chunks per row
   constexpr int CH = kFwdKB * CPR / 256;   // chunks per thread per tensor
-  uint4 kreg[CH], vreg[CH];
-  auto gload = [&](int kt) {
+  // K/V tiles of the tile TWO ahead are loaded into registers while the current tile computes
+  // (two register sets, loop unrolled by two) at D = 64; one ahead at D = 128 (register budget)
+  constexpr bool KV2 = D == 64;
+  constexpr int AHEAD = KV2 ? 2 : 1;
+  struct KV {
+    uint4 k[CH], v[CH];
+  };
+  KV kva, kvb;
+  // dropout: each lane draws the keep bits of its own 16 keys of every 32-key block in the
+  // loop (one Philox call per block, DropGen::half_bits), and the two lane halves' words are
+  // combined and stored for the backward kernels
+  uint32_t* mrow =
+      DROPOUT && qrow < a.Sq ? (uint32_t*)(a.dmask + ((int64_t)bh * a.Sq + qrow) * a.mask_words) : nullptr;
+  const DropGen dg{a.seed, a.offset, a.drop_thresh};
+  auto gload = [&](KV& R, int kt) {
+    uint4 (&kreg)[CH] = R.k;
+    uint4 (&vreg)[CH] = R.v;
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
       const int idx = threadIdx.x + 256 * c;
@@ -152,7 +185,9 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
       }
     }
   };
-  auto lstore = [&]() {
+  auto lstore = [&](KV& R) {
+    uint4 (&kreg)[CH] = R.k;
+    uint4 (&vreg)[CH] = R.v;
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
       const int idx = threadIdx.x + 256 * c;
@@ -162,51 +197,80 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
     }
   };
 
-  DropGen dg{a.seed, a.offset, a.drop_thresh};
-  const float rkeep = a.drop_scale;
-
-  if (ntiles > 0) gload(0);
-  for (int kt = 0; kt < ntiles; ++kt) {
+  if (ntiles > 0) gload(kva, 0);
+  if (KV2 && ntiles > 1) gload(kvb, 1);
+  auto tile = [&](KV& R, const int kt) {
     lds_barrier();  // previous tile fully consumed
-    lstore();
+    lstore(R);
     lds_barrier();
-    if (kt + 1 < ntiles) gload(kt + 1);
+    uint32_t mcur[2] = {0u, 0u};
+    if (DROPOUT) {
+#pragma unroll
+      for (int sb = 0; sb < 2; ++sb) {
+        const int blk = (kt * kFwdKB >> 5) + sb;
+        const uint32_t hb = dg.half_bits(bh, qrow, blk, hl, a.Sq);  // bits at 4 hl + {0-3, 8-11, ..}
+        const uint32_t word = hb | __shfl_xor(hb, 32, 64);
+        if (hl == 0 && mrow && blk * 32 < a.Sk) mrow[blk] = word;
+        mcur[sb] = hb >> (4 * hl);
+      }
+    }
+    if (kt + AHEAD < ntiles) gload(R, kt + AHEAD);
     const int kb = kt * kFwdKB;
 
     // ---- S^T for two 32-key sub-blocks
+    // all K fragments of the tile are read before the MFMA chain (one LDS latency per tile
+    // instead of one per MFMA)
     f32x16 st[2];
+    V8 kf[2][D / 16];
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+      for (int s = 0; s < D / 16; ++s) kf[sb][s] = *(const V8*)(lds_k + (32 * sb + r) * LDR + 16 * s + 8 * hl);
+    __builtin_amdgcn_sched_group_barrier(0x100, 2 * (D / 16), 0);  // DS reads first
+    __builtin_amdgcn_sched_group_barrier(0x008, 2 * (D / 16), 0);  // then the MFMAs
 #pragma unroll
     for (int sb = 0; sb < 2; ++sb) {
       st[sb] = f32x16{};
 #pragma unroll
-      for (int s = 0; s < D / 16; ++s) {
-        const V8 kf = *(const V8*)(lds_k + (32 * sb + r) * LDR + 16 * s + 8 * hl);
-        st[sb] = M::mma(kf, qf[s], st[sb]);
-      }
+      for (int s = 0; s < D / 16; ++s) st[sb] = M::mma(kf[sb][s], qf[s], st[sb]);
+    }
+    // D = 64: the V^T fragments of the PV product are read now, their LDS latency hidden
+    // behind the softmax (D = 128 would not fit in the register budget of 2 workgroups/CU)
+    constexpr bool HOIST_V = D == 64;
+    V8 vt[2][2][HOIST_V ? D / 32 : 1];
+    if constexpr (HOIST_V) {
+#pragma unroll
+      for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int db = 0; db < D / 32; ++db) {
+            const int k0 = 32 * sb + 16 * s2 + 4 * hl + ((lane & 15) >> 2);
+            const int c0 = 32 * db + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+            vt[sb][s2][db] = join4<V8>(lds_tr16(lds_v + k0 * LDR + c0), lds_tr16(lds_v + (k0 + 8) * LDR + c0));
+          }
     }
     // ---- mask (boundary tiles only) + running max on the RAW scores; the softmax scale is
     // folded into the exp2 argument (one FMA per element) and exp2 is the bare v_exp_f32
     // (no denormal range reduction: underflow to 0 is what softmax wants).
     const bool interior = (kb + kFwdKB <= Sk) && (!CAUSAL || kb + kFwdKB - 1 <= q0 + 32 * wid);
-    float tmax = -INFINITY;
-    if (interior) {
-#pragma unroll
-      for (int sb = 0; sb < 2; ++sb)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) tmax = fmaxf(tmax, st[sb][i]);
-    } else {
+    if (!interior) {
+      // keys valid for this lane's query: key < lim (one compare + select per element)
+      const int lim = CAUSAL ? min(Sk, qrow + 1) : Sk;
 #pragma unroll
       for (int sb = 0; sb < 2; ++sb) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int key = kb + 32 * sb + (i & 3) + 8 * (i >> 2) + 4 * hl;
-          float t = st[sb][i];
-          if (key >= Sk || (CAUSAL && key > qrow)) t = -INFINITY;
-          st[sb][i] = t;
-          tmax = fmaxf(tmax, t);
+          if (key >= lim) st[sb][i] = -INFINITY;
         }
       }
     }
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) tmax = fmaxf(tmax, st[sb][i]);
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
     const float mnew = fmaxf(m, tmax);
     const float muse = mnew == -INFINITY ? 0.f : mnew;
@@ -216,45 +280,17 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
     float psum = 0.f;
 #pragma unroll
     for (int sb = 0; sb < 2; ++sb) {
-      // dropout: this lane's 16 keys are 4 groups g of 4 (keys 8g + 4hl + e). Each 8-key
-      // group is one Philox block shared by the two lane halves, so each half generates
-      // two of the four blocks and swaps the other half's chunks over lane^32.
-      uint32_t wlo[2][2], whi[2][2];
-      if (DROPOUT) {
 #pragma unroll
-        for (int gg = 0; gg < 2; ++gg) {
-          const int gme = hl ? gg + 2 : gg;
-          const uint4 rr = dg.block(bh, qrow, (kb + 32 * sb + 8 * gme) >> 3, a.Sq);
-          const uint32_t m0 = hl ? rr.z : rr.x, m1 = hl ? rr.w : rr.y;
-          const uint32_t s0 = hl ? rr.x : rr.z, s1 = hl ? rr.y : rr.w;
-          const uint32_t r0 = __shfl_xor(s0, 32, 64), r1 = __shfl_xor(s1, 32, 64);
-          wlo[gg][0] = hl ? r0 : m0;
-          wlo[gg][1] = hl ? r1 : m1;
-          whi[gg][0] = hl ? m0 : r0;
-          whi[gg][1] = hl ? m1 : r1;
-        }
+      for (int i = 0; i < 16; ++i) {
+        const float p = __builtin_amdgcn_exp2f(fmaf(st[sb][i], a.scale_log2, mscaled));
+        psum += p;
+        // dropped: keep bit i selects p or +0 (bfe sign-extends the bit to an all-ones mask);
+        // the 1/(1-p) rescale is applied once in the epilogue
+        // element i = key (i & 3) + 8 (i >> 2) + 4 hl: bit (i & 3) + 8 (i >> 2) of the shifted word
+        st[sb][i] = DROPOUT ? __builtin_bit_cast(float, __builtin_bit_cast(int, p) &
+                                                            __builtin_amdgcn_sbfe((int)mcur[sb], (i & 3) + 8 * (i >> 2), 1))
+                            : p;
       }
-      uint32_t bits = 0;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int i = 4 * g + e;
-          const float p = __builtin_amdgcn_exp2f(fmaf(st[sb][i], a.scale_log2, mscaled));
-          psum += p;
-          float pd = p;
-          if (DROPOUT) {
-            const uint32_t w = g < 2 ? wlo[g & 1][e >> 1] : whi[g & 1][e >> 1];
-            const uint32_t r16 = (e & 1) ? (w >> 16) : (w & 0xffffu);
-            const bool keep = r16 >= dg.thresh;
-            bits |= (uint32_t)keep << i;
-            pd = keep ? p * rkeep : 0.f;
-          }
-          st[sb][i] = pd;
-        }
-      }
-      if (DROPOUT && a.dmask && qrow < a.Sq && kb + 32 * sb < a.Sk)
-        a.dmask[((int64_t)bh * a.Sq + qrow) * a.mask_words + ((kb >> 5) + sb) * 2 + hl] = (uint16_t)bits;
     }
     l = l * alpha + psum;
 #pragma unroll
@@ -273,18 +309,30 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
         const int k0 = 32 * sb + 16 * s2 + 4 * hl + ((lane & 15) >> 2);
 #pragma unroll
         for (int db = 0; db < D / 32; ++db) {
-          const int c0 = 32 * db + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-          const s16x4 lo = lds_tr16(lds_v + k0 * LDR + c0);
-          const s16x4 hi = lds_tr16(lds_v + (k0 + 8) * LDR + c0);
-          o[db] = M::mma(join4<V8>(lo, hi), pf, o[db]);
+          if constexpr (HOIST_V) {
+            o[db] = M::mma(vt[sb][s2][db], pf, o[db]);
+          } else {
+            const int c0 = 32 * db + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+            const s16x4 lo = lds_tr16(lds_v + k0 * LDR + c0);
+            const s16x4 hi = lds_tr16(lds_v + (k0 + 8) * LDR + c0);
+            o[db] = M::mma(join4<V8>(lo, hi), pf, o[db]);
+          }
         }
       }
     }
+  };
+  if constexpr (KV2) {
+    for (int kt = 0; kt < ntiles; kt += 2) {
+      tile(kva, kt);
+      if (kt + 1 < ntiles) tile(kvb, kt + 1);
+    }
+  } else {
+    for (int kt = 0; kt < ntiles; ++kt) tile(kva, kt);
   }
   // ---- epilogue
   const float ltot = l + __shfl_xor(l, 32, 64);
   if (qrow < a.Sq) {
-    const float inv = ltot > 0.f ? 1.f / ltot : 0.f;
+    const float inv = ltot > 0.f ? (DROPOUT ? a.drop_scale : 1.f) / ltot : 0.f;
     T* op = (T*)a.o + b * a.o_bs + h * a.o_hs + (int64_t)qrow * a.o_ss;
 #pragma unroll
     for (int db = 0; db < D / 32; ++db) {
@@ -309,8 +357,12 @@ constexpr int kBwdWaves = 4;
 constexpr int kBwdBK = 32 * kBwdWaves;  // 128 keys per workgroup
 constexpr int kBwdBQ = 32;              // queries per inner step
 
-template <typename T, int D, bool CAUSAL, bool DROPOUT, bool DSUM>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 64 ? 2 : 1, D == 64 ? 2 : 1))) attn_bwd_kernel(AttnArgs a, const void* dout, float* dq_acc,
+// DQ = true (Sk <= 128: the workgroup holds every key, so it is the sole owner of dQ for its
+// query rows and writes it directly). DQ = false (longer key ranges): dK/dV only; the key-block-0
+// workgroups also store delta = rowsum(dO * O) into delta_out, and attn_bwd_dq_kernel computes dQ
+// from a query-stationary loop (no cross-workgroup fp32 atomics; see the kernel below).
+template <typename T, int D, bool CAUSAL, bool DROPOUT, bool DSUM, bool DQ>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 64 ? 2 : 1, D == 64 ? 2 : 1))) attn_bwd_kernel(AttnArgs a, const void* dout, float* delta_out,
                                                          void* dk_out, void* dv_out) {
   using M = MfmaT<T>;
   using V8 = typename M::V8;
@@ -322,9 +374,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 6
   __shared__ __attribute__((aligned(16))) T lds_ds[kBwdBQ * LDS_S];
   __shared__ float lds_lse[kBwdBQ], lds_delta[kBwdBQ];
   __shared__ float lds_dqred[(D == 64) ? 2048 : 1];
-  __shared__ uint16_t lds_mask[kBwdBQ * 8];  // [q][4 key blocks][2 halves]
+  __shared__ uint32_t lds_mask[4 * kBwdBQ];  // [wave's 32-key block][q]: bit k <-> key 32 wid + k
 
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  // wid through readfirstlane: wave-uniform in SGPRs, so tile-level conditions become scalar branches
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 31, hl = lane >> 5;
   const int bh = blockIdx.y;
   const int b = bh / a.H, h = bh % a.H;
@@ -352,6 +405,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 6
     }
   }
   // whole K block to LDS (needed as the B operand of dQ = dS.K via tr reads)
+  if (DQ)
   for (int idx = threadIdx.x; idx < kBwdBK * (D / 8); idx += 256) {
     const int row = idx / (D / 8), col = (idx % (D / 8)) * 8;
     const int key = k0 + row;
@@ -371,19 +425,32 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 6
   int qstart = 0;
   if (CAUSAL) qstart = (k0 / kBwdBQ) * kBwdBQ;
   const int nq = a.Sq;
-  DropGen dg{a.seed, a.offset, a.drop_thresh};
   const float rkeep = a.drop_scale;
-  const bool single_kblock = (a.Sk <= kBwdBK);
 
-  // Q / dO / O tiles (32 x D), lse and the dropout words of the NEXT query block are loaded
-  // into registers while the current block computes (software pipelining); the barriers
+  // Q / dO / O tiles (32 x D), lse and the dropout words of the query block TWO steps ahead
+  // are loaded into registers while the current block computes (two register sets, the loop
+  // unrolled by two, so every global load has two steps of compute to land in); the barriers
   // below only wait for LDS traffic so these global loads stay in flight across them.
   constexpr int CPR = D / 8;
   constexpr int NLD = kBwdBQ * CPR / 256;
-  uint4 pf_q[NLD], pf_do[NLD], pf_o[NLD];
-  float pf_lse = INFINITY;
-  uint16_t pf_mask = 0;
-  auto fetch = [&](int qb) {
+  struct Pf {
+    uint4 q[NLD], d[NLD], o[NLD];
+    float lse;
+    uint32_t mask;
+  };
+  // two register sets where they fit (dK/dV-only kernel at D = 64); one set (prefetch one step
+  // ahead) for the fused single-key-block kernel and D = 128, which would spill
+  constexpr bool DEPTH2 = !DQ && D == 64;
+  constexpr int AHEAD = DEPTH2 ? 2 : 1;
+  Pf pfa, pfb;
+  auto fetch = [&](Pf& P, int qb) {
+    uint4 (&pf_q)[NLD] = P.q;
+    uint4 (&pf_do)[NLD] = P.d;
+    uint4 (&pf_o)[NLD] = P.o;
+    float& pf_lse = P.lse;
+    uint32_t& pf_mask = P.mask;
+    pf_lse = INFINITY;
+    pf_mask = 0u;
 #pragma unroll
     for (int c = 0; c < NLD; ++c) {
       const int idx = threadIdx.x + 256 * c;
@@ -401,19 +468,23 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 6
       const int q = qb + threadIdx.x;
       pf_lse = q < nq ? lsep[q] * kLog2e : INFINITY;
     }
-    if (DROPOUT) {
-      // dropout bits written by the forward pass: [q][32-key block][half] uint16 words
-      const int qi = threadIdx.x >> 3, w = threadIdx.x & 7;
-      const int q = qb + qi, blk = (k0 >> 5) + (w >> 1);
+    if (DROPOUT && threadIdx.x < 4 * kBwdBQ) {
+      // dropout words written by the forward: one per (query, 32-key block), bit k <-> key k
+      const int qi = threadIdx.x & (kBwdBQ - 1), w = threadIdx.x / kBwdBQ;
+      const int q = qb + qi, blk = (k0 >> 5) + w;
       pf_mask = (q < nq && blk * 32 < a.Sk)
-                    ? a.dmask[((int64_t)bh * a.Sq + q) * a.mask_words + blk * 2 + (w & 1)]
-                    : (uint16_t)0;
+                    ? ((const uint32_t*)(a.dmask + ((int64_t)bh * a.Sq + q) * a.mask_words))[blk]
+                    : 0u;
     }
   };
-  if (qstart < nq) fetch(qstart);
+  if (qstart < nq) fetch(pfa, qstart);
+  if (DEPTH2 && qstart + kBwdBQ < nq) fetch(pfb, qstart + kBwdBQ);
 
   float dq_colsum = 0.f;  // DSUM: this lane's dq column (32cb + r) summed over its query rows
-  for (int qb = qstart; qb < nq; qb += kBwdBQ) {
+  auto body = [&](Pf& P, const int qb) {
+    uint4 (&pf_q)[NLD] = P.q;
+    uint4 (&pf_do)[NLD] = P.d;
+    uint4 (&pf_o)[NLD] = P.o;
     lds_barrier();
     // stage the prefetched tiles; delta = rowsum(dO * O) is computed here from O
     // (CPR consecutive threads own one row -> xor-shuffle reduce), no separate pass.
@@ -429,13 +500,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 6
       for (int e = 0; e < 8; ++e) part += ov[e] * dov[e];
 #pragma unroll
       for (int o = CPR / 2; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
-      if ((idx % CPR) == 0) lds_delta[row] = part;
+      if ((idx % CPR) == 0) {
+        lds_delta[row] = part;
+        if (!DQ && blockIdx.x == 0 && qb + row < nq) delta_out[(int64_t)bh * a.Sq + qb + row] = part;
+      }
       *(uint4*)(lds_q + row * LDR + col) = pf_q[c];
       *(uint4*)(lds_do + row * LDR + col) = pf_do[c];
     }
-    if (threadIdx.x < kBwdBQ) lds_lse[threadIdx.x] = pf_lse;
-    if (DROPOUT) lds_mask[threadIdx.x] = pf_mask;
-    if (qb + kBwdBQ < nq) fetch(qb + kBwdBQ);
+    if (threadIdx.x < kBwdBQ) lds_lse[threadIdx.x] = P.lse;
+    if (DROPOUT && threadIdx.x < 4 * kBwdBQ) lds_mask[threadIdx.x] = P.mask;
+    if (qb + AHEAD * kBwdBQ < nq) fetch(P, qb + AHEAD * kBwdBQ);
     lds_barrier();
 
     // S = Q . K^T  [32 q x 32 keys]: A = Q rows (LDS), B = K rows (regs)
@@ -447,10 +521,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 6
       sacc = M::mma(qa, kf[s], sacc);
       dpacc = M::mma(da, vf[s], dpacc);
     }
-    // element i: q = qb + (i&3) + 8(i>>2) + 4hl, key = mykey
+    // element i: q = qb + (i&3) + 8(i>>2) + 4hl, key = mykey.
+    // pd = P * keep (the 1/(1-p) factor of dV is applied once, in the epilogue),
+    // ds = P * (dP * keep / (1-p) - delta) (the softmax scale of dK / dQ likewise).
     float pd[16], ds[16];
-    // this lane's key within its 32-key block: forward stored it as bit kbit of half khalf
-    const int khalf = (r >> 2) & 1, kbit = (r & 3) + 4 * (r >> 3);
+    const bool interior = (k0 + 32 * wid + 31 < Sk) && (qb + kBwdBQ <= nq) && (!CAUSAL || k0 + 32 * wid + 31 <= qb);
     // exp2 is the bare v_exp_f32 (no denormal range reduction)
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
@@ -459,15 +534,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 6
       for (int e = 0; e < 4; ++e) {
         const int i = 4 * g + e;
         const int qi = qr0 + e;
-        const int q = qb + qi;
-        const float t = sacc[i] * a.scale_log2 - lds_lse[qi];
-        const bool valid = (mykey < Sk) && (q < nq) && !(CAUSAL && mykey > q);
-        const float p = valid ? __builtin_amdgcn_exp2f(t) : 0.f;
-        float keep = 1.f;
-        if (DROPOUT) keep = ((lds_mask[qi * 8 + wid * 2 + khalf] >> kbit) & 1) ? rkeep : 0.f;
-        pd[i] = p * keep;                                   // dropped P (for dV)
-        const float dpv = dpacc[i] * keep;                  // dP through dropout
-        ds[i] = p * (dpv - lds_delta[qi]) * a.scale;        // dS (includes softmax scale)
+        float p = __builtin_amdgcn_exp2f(fmaf(sacc[i], a.scale_log2, -lds_lse[qi]));
+        if (!interior) {
+          const int q = qb + qi;
+          const bool valid = (mykey < Sk) && (q < nq) && !(CAUSAL && mykey > q);
+          p = valid ? p : 0.f;
+        }
+        float dpv = dpacc[i];
+        float pk = p;
+        if (DROPOUT) {
+          const int m = __builtin_amdgcn_sbfe((int)lds_mask[wid * kBwdBQ + qi], r, 1);
+          pk = __builtin_bit_cast(float, __builtin_bit_cast(int, p) & m);
+          dpv = __builtin_bit_cast(float, __builtin_bit_cast(int, dpv) & m);
+        }
+        pd[i] = pk;
+        ds[i] = p * fmaf(dpv, rkeep, -lds_delta[qi]);
       }
     }
     // dV += P^T . dO : accumulator-as-A (contraction over q = rows), B = dO via tr reads
@@ -486,6 +567,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 6
         dk[db] = M::mma(sa, qbf, dk[db]);
       }
     }
+    if constexpr (DQ) {
     // dS to LDS as [q][key] (bf16) for dQ = dS . K
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -528,49 +610,63 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 6
             for (int i = 0; i < 16; ++i) dq[i] += lds_dqred[((k2 - 1) * NCB + cb) * 1024 + i * 64 + lane];
         }
       }
-      // dq element i: row q = (i&3)+8(i>>2)+4hl, col dim = 32cb + r
+      // dq element i: row q = (i&3)+8(i>>2)+4hl, col dim = 32cb + r; this workgroup is the sole
+      // writer of these query rows (DQ only with a single key block): final dtype, strided
       if (ks == 0) {
+        T* dqp = (T*)a.dq + b * a.dq_bs + h * a.dq_hs + 32 * cb + r;
+        auto store = [&](auto guarded) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int q = qb + (i & 3) + 8 * (i >> 2) + 4 * hl;
-          if (q < nq) {
-            if (single_kblock) {  // sole writer of this (b, h) query block: final dtype, strided
-              const T v = (T)dq[i];
-              ((T*)a.dq)[b * a.dq_bs + h * a.dq_hs + (int64_t)q * a.dq_ss + 32 * cb + r] = v;
+          for (int i = 0; i < 16; ++i) {
+            const int q = qb + (i & 3) + 8 * (i >> 2) + 4 * hl;
+            if (!decltype(guarded)::value || q < nq) {
+              const T v = (T)(dq[i] * a.scale);
+              dqp[(int64_t)q * a.dq_ss] = v;
               if constexpr (DSUM) dq_colsum += (float)v;
-            } else {
-              atomicAdd(dq_acc + ((int64_t)bh * a.Sq + q) * D + 32 * cb + r, dq[i]);
-              if constexpr (DSUM) dq_colsum += dq[i];
             }
           }
-        }
-
+        };
+        if (qb + kBwdBQ <= nq) store(std::false_type{});  // uniform: no per-element guards
+        else store(std::true_type{});
       }
     }
+    }  // DQ
+  };
+  if constexpr (DEPTH2) {
+    for (int qb = qstart; qb < nq; qb += 2 * kBwdBQ) {
+      body(pfa, qb);
+      if (qb + kBwdBQ < nq) body(pfb, qb + kBwdBQ);
+    }
+  } else {
+    for (int qb = qstart; qb < nq; qb += kBwdBQ) body(pfa, qb);
   }
   // write dK, dV: element i of block db -> key = k0 + 32wid + (i&3)+8(i>>2)+4hl, dim = 32db + r
   T* dkp = (T*)dk_out + b * a.dk_bs + h * a.dk_hs;
   T* dvp = (T*)dv_out + b * a.dv_bs + h * a.dv_hs;
   // optional bias-gradient partials: column sums of the stored dq / dk / dv over positions
   float* dsum = DSUM ? a.dsum + ((int64_t)b * 3 * a.H + h) * D : nullptr;
-  if (DSUM && wid < (D / 32)) {  // the ks == 0 waves own dq column block cb == wid
+  if (DSUM && DQ && wid < (D / 32)) {  // the ks == 0 waves own dq column block cb == wid
     const float t = dq_colsum + __shfl_xor(dq_colsum, 32, 64);
     if (hl == 0) atomicAdd(dsum + 32 * wid + r, t);
   }
+  const bool kfull = k0 + 32 * wid + 32 <= a.Sk;
 #pragma unroll
   for (int db = 0; db < D / 32; ++db) {
     float sk = 0.f, sv = 0.f;
+    auto store = [&](auto guarded) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int key = k0 + 32 * wid + (i & 3) + 8 * (i >> 2) + 4 * hl;
-      if (key < a.Sk) {
-        const T vk = (T)dk[db][i], vv = (T)dv[db][i];
-        dkp[(int64_t)key * a.dk_ss + 32 * db + r] = vk;
-        dvp[(int64_t)key * a.dv_ss + 32 * db + r] = vv;
-        sk += (float)vk;
-        sv += (float)vv;
+      for (int i = 0; i < 16; ++i) {
+        const int key = k0 + 32 * wid + (i & 3) + 8 * (i >> 2) + 4 * hl;
+        if (!decltype(guarded)::value || key < a.Sk) {
+          const T vk = (T)(dk[db][i] * a.scale), vv = (T)(dv[db][i] * rkeep);
+          dkp[(int64_t)key * a.dk_ss + 32 * db + r] = vk;
+          dvp[(int64_t)key * a.dv_ss + 32 * db + r] = vv;
+          sk += (float)vk;
+          sv += (float)vv;
+        }
       }
-    }
+    };
+    if (kfull) store(std::false_type{});  // uniform: no per-element guards
+    else store(std::true_type{});
     if constexpr (DSUM) {
       sk += __shfl_xor(sk, 32, 64);
       sv += __shfl_xor(sv, 32, 64);
@@ -582,43 +678,232 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 6
   }
 }
 
-// dQ fp32 accumulator [B*H, Sq, D] -> output dtype with strides
-template <typename T, int D>
-__global__ void __launch_bounds__(256) attn_dq_convert(AttnArgs a, const float* dq_acc) {
-  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;  // one thread per 8 elements
-  const int64_t total = (int64_t)a.B * a.H * a.Sq * (D / 8);
-  if (idx >= total) return;
-  const int c8 = (int)(idx % (D / 8));
-  const int64_t row = idx / (D / 8);
-  const int q = (int)(row % a.Sq);
-  const int64_t bh = row / a.Sq;
-  const int b = (int)(bh / a.H), h = (int)(bh % a.H);
-  float v[8];
-  load_f<float, 8>(dq_acc + row * D + c8 * 8, v);
-  T* dst = (T*)a.dq + b * a.dq_bs + h * a.dq_hs + (int64_t)q * a.dq_ss + c8 * 8;
-  store_f<T, 8>(dst, v);
+// dQ for key ranges longer than one backward key block: query-stationary, the forward's
+// structure (one workgroup = 4 waves x 32 query rows, K/V streamed in 64-key tiles):
+//   S^T = K . Q^T and dP^T = V . dO^T (32x32x16, one query per lane, so lse and delta are
+//   lane-local scalars), dS^T = P^T * (dP^T * keep - delta) in registers, and
+//   dQ^T += K^T . dS^T with the dS^T accumulators reused directly as the B operand (the same
+//   register reuse as O^T += V^T . P^T in the forward). Every dQ row has exactly one writer:
+//   no fp32 atomics, no accumulator buffer, no conversion pass. The extra S / dP products (vs
+//   the fused single-kernel backward) cost less than the fp32 atomic traffic they replace.
+template <typename T, int D, bool CAUSAL, bool DROPOUT, bool DSUM>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 64 ? 2 : 1, D == 64 ? 2 : 1))) attn_bwd_dq_kernel(AttnArgs a, const void* dout, const float* delta_in) {
+  using M = MfmaT<T>;
+  using V8 = typename M::V8;
+  constexpr int LDR = D + 8;
+  __shared__ __attribute__((aligned(16))) T lds_k[kFwdKB * LDR];
+  __shared__ __attribute__((aligned(16))) T lds_v[kFwdKB * LDR];
+
+  // wid through readfirstlane: wave-uniform in SGPRs, so tile-level conditions become scalar branches
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 31, hl = lane >> 5;
+  const int bh = blockIdx.y;
+  const int b = bh / a.H, h = bh % a.H;
+  const int q0 = blockIdx.x * kFwdBQ;
+  const int qrow = q0 + 32 * wid + r;
+  const int Sk = a.k_lens ? min(a.k_lens[b], a.Sk) : a.Sk;
+
+  const T* qp = (const T*)a.q + b * a.q_bs + h * a.q_hs;
+  const T* dop = (const T*)dout + b * a.do_bs + h * a.do_hs;
+  const T* kp = (const T*)a.k + b * a.k_bs + h * a.k_hs;
+  const T* vp = (const T*)a.v + b * a.v_bs + h * a.v_hs;
+
+  // Q^T and dO^T fragments (B operands): lane (q=r, hl) holds X[q][16s + 8hl .. +7]
+  V8 qf[D / 16], df[D / 16];
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) {
+    if (qrow < a.Sq) {
+      qf[s] = *(const V8*)(qp + (int64_t)qrow * a.q_ss + 16 * s + 8 * hl);
+      df[s] = *(const V8*)(dop + (int64_t)qrow * a.do_ss + 16 * s + 8 * hl);
+    } else {
+      qf[s] = V8{};
+      df[s] = V8{};
+    }
+  }
+  // log2-domain lse (+inf for padding rows and fully masked rows: P = 0) and delta
+  const float lse2 = qrow < a.Sq ? a.lse[(int64_t)bh * a.Sq + qrow] * kLog2e : INFINITY;
+  const float delta = qrow < a.Sq ? delta_in[(int64_t)bh * a.Sq + qrow] : 0.f;
+
+  f32x16 dq[D / 32];
+#pragma unroll
+  for (int i = 0; i < D / 32; ++i) dq[i] = f32x16{};
+
+  int kend = Sk;
+  if (CAUSAL) kend = min(kend, q0 + kFwdBQ);
+  const int ntiles = (kend + kFwdKB - 1) / kFwdKB;
+
+  constexpr int CPR = D / 8;
+  constexpr int CH = kFwdKB * CPR / 256;
+  // K/V tiles of the tile TWO ahead are loaded into registers while the current tile computes
+  // (two register sets, loop unrolled by two) at D = 64; one ahead at D = 128 (register budget)
+  constexpr bool KV2 = D == 64;
+  constexpr int AHEAD = KV2 ? 2 : 1;
+  struct KV {
+    uint4 k[CH], v[CH];
+    uint32_t m[2];
+  };
+  KV kva, kvb;
+  const uint32_t* mrow =
+      DROPOUT && qrow < a.Sq ? (const uint32_t*)(a.dmask + ((int64_t)bh * a.Sq + qrow) * a.mask_words) : nullptr;
+  auto gload = [&](KV& R, int kt) {
+    uint4 (&kreg)[CH] = R.k;
+    uint4 (&vreg)[CH] = R.v;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int idx = threadIdx.x + 256 * c;
+      const int row = idx / CPR, col = (idx % CPR) * 8;
+      const int key = kt * kFwdKB + row;
+      if (key < Sk) {
+        kreg[c] = *(const uint4*)(kp + (int64_t)key * a.k_ss + col);
+        vreg[c] = *(const uint4*)(vp + (int64_t)key * a.v_ss + col);
+      } else {
+        kreg[c] = make_uint4(0, 0, 0, 0);
+        vreg[c] = make_uint4(0, 0, 0, 0);
+      }
+    }
+    if (DROPOUT) {
+      // the forward's keep bits for this lane's 16 keys of each 32-key block (same layout)
+#pragma unroll
+      for (int sb = 0; sb < 2; ++sb) {
+        const int blk = (kt * kFwdKB >> 5) + sb;
+        R.m[sb] = (mrow && blk * 32 < a.Sk) ? mrow[blk] >> (4 * hl) : 0u;
+      }
+    }
+  };
+  auto lstore = [&](KV& R) {
+    uint4 (&kreg)[CH] = R.k;
+    uint4 (&vreg)[CH] = R.v;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int idx = threadIdx.x + 256 * c;
+      const int row = idx / CPR, col = (idx % CPR) * 8;
+      *(uint4*)(lds_k + row * LDR + col) = kreg[c];
+      *(uint4*)(lds_v + row * LDR + col) = vreg[c];
+    }
+  };
+
+  const float rkeep = a.drop_scale;
+  if (ntiles > 0) gload(kva, 0);
+  if (KV2 && ntiles > 1) gload(kvb, 1);
+  auto tile = [&](KV& R, const int kt) {
+    lds_barrier();  // previous tile fully consumed
+    lstore(R);
+    const uint32_t mcur[2] = {R.m[0], R.m[1]};
+    lds_barrier();
+    if (kt + AHEAD < ntiles) gload(R, kt + AHEAD);
+    const int kb = kt * kFwdKB;
+
+    f32x16 st[2], dpt[2];
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb) {
+      V8 kf[D / 16], vf[D / 16];
+#pragma unroll
+      for (int s = 0; s < D / 16; ++s) {
+        kf[s] = *(const V8*)(lds_k + (32 * sb + r) * LDR + 16 * s + 8 * hl);
+        vf[s] = *(const V8*)(lds_v + (32 * sb + r) * LDR + 16 * s + 8 * hl);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x100, 2 * (D / 16), 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 2 * (D / 16), 0);
+      st[sb] = f32x16{};
+      dpt[sb] = f32x16{};
+#pragma unroll
+      for (int s = 0; s < D / 16; ++s) {
+        st[sb] = M::mma(kf[s], qf[s], st[sb]);
+        dpt[sb] = M::mma(vf[s], df[s], dpt[sb]);
+      }
+    }
+    const bool interior = (kb + kFwdKB <= Sk) && (!CAUSAL || kb + kFwdKB - 1 <= q0 + 32 * wid);
+    const int lim = CAUSAL ? min(Sk, qrow + 1) : Sk;
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float p = __builtin_amdgcn_exp2f(fmaf(st[sb][i], a.scale_log2, -lse2));
+        if (!interior) {
+          const int key = kb + 32 * sb + (i & 3) + 8 * (i >> 2) + 4 * hl;
+          if (key >= lim) p = 0.f;
+        }
+        float dp = dpt[sb][i];
+        if (DROPOUT)
+          dp = __builtin_bit_cast(float, __builtin_bit_cast(int, dp) & __builtin_amdgcn_sbfe((int)mcur[sb], (i & 3) + 8 * (i >> 2), 1));
+        st[sb][i] = p * fmaf(dp, rkeep, -delta);  // dS^T (the softmax scale is applied once, at the end)
+      }
+    }
+    // dQ^T += K^T . dS^T
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb) {
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        float sv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sv[j] = st[sb][8 * s2 + j];
+        const V8 sf = pack8<T, V8>(sv);
+        const int k0 = 32 * sb + 16 * s2 + 4 * hl + ((lane & 15) >> 2);
+#pragma unroll
+        for (int db = 0; db < D / 32; ++db) {
+          const int c0 = 32 * db + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+          const s16x4 lo = lds_tr16(lds_k + k0 * LDR + c0);
+          const s16x4 hi = lds_tr16(lds_k + (k0 + 8) * LDR + c0);
+          dq[db] = M::mma(join4<V8>(lo, hi), sf, dq[db]);
+        }
+      }
+    }
+  };
+  if constexpr (KV2) {
+    for (int kt = 0; kt < ntiles; kt += 2) {
+      tile(kva, kt);
+      if (kt + 1 < ntiles) tile(kvb, kt + 1);
+    }
+  } else {
+    for (int kt = 0; kt < ntiles; ++kt) tile(kva, kt);
+  }
+  // ---- epilogue: element 4g+e of block db -> dim 32db + 8g + 4hl + e of query qrow
+  float* dsum = DSUM ? a.dsum + ((int64_t)b * 3 * a.H + h) * D : nullptr;
+#pragma unroll
+  for (int db = 0; db < D / 32; ++db) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      typedef T t4 __attribute__((ext_vector_type(4)));
+      t4 w;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) w[e] = (T)(dq[db][4 * g + e] * a.scale);
+      if (qrow < a.Sq)
+        *(t4*)((T*)a.dq + b * a.dq_bs + h * a.dq_hs + (int64_t)qrow * a.dq_ss + 32 * db + 8 * g + 4 * hl) = w;
+      if constexpr (DSUM) {
+        // column sums of the stored values over this wave's 32 query rows (lanes r), then one
+        // atomic per dim per wave
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float t = qrow < a.Sq ? (float)w[e] : 0.f;
+#pragma unroll
+          for (int o = 16; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+          if (r == 0) atomicAdd(dsum + 32 * db + 8 * g + 4 * hl + e, t);
+        }
+      }
+    }
+  }
 }
 
 // debug / test: materialise the keep-mask the kernels use (uint8 [B*H, Sq, Sk])
 __global__ void attn_dropout_mask_kernel(uint8_t* out, int64_t BH, int Sq, int Sk, uint64_t seed,
                                          uint64_t offset, uint32_t thresh) {
-  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;  // one thread per 8 keys
-  const int64_t n8 = (Sk + 7) / 8;
-  if (idx >= BH * Sq * n8) return;
-  const int64_t c8 = idx % n8, row = idx / n8;
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;  // one thread per 32 keys
+  const int64_t nblk = (Sk + 31) / 32;
+  if (idx >= BH * Sq * nblk) return;
+  const int64_t blk = idx % nblk, row = idx / nblk;
   const int q = (int)(row % Sq);
   const int64_t bh = row / Sq;
   DropGen dg{seed, offset, thresh};
-  const uint4 rnd = dg.block(bh, q, c8, Sq);
-  for (int e = 0; e < 8; ++e) {
-    const int64_t key = c8 * 8 + e;
-    if (key < Sk) out[row * Sk + key] = DropGen::r16(rnd, e) >= thresh ? 1 : 0;
+  const uint32_t w = dg.block_bits(bh, q, blk, Sq);
+  for (int k = 0; k < 32; ++k) {
+    const int64_t key = blk * 32 + k;
+    if (key < Sk) out[row * Sk + key] = (w >> k) & 1;
   }
 }
 
 int attn_dropout_mask(uint8_t* out, int64_t BH, int Sq, int Sk, uint64_t seed, uint64_t offset,
                       uint32_t thresh, hipStream_t s) {
-  const int64_t n = BH * Sq * ((Sk + 7) / 8);
+  const int64_t n = BH * Sq * ((Sk + 31) / 32);
   hipLaunchKernelGGL(attn_dropout_mask_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
                      out, BH, Sq, Sk, seed, offset, thresh);
   return (int)hipGetLastError();
@@ -644,6 +929,7 @@ int attn_fwd(const AttnArgs& a, int dt, hipStream_t s) {
   if (a.B * a.H == 0 || a.Sq == 0) return 0;
   dim3 grid((a.Sq + kFwdBQ - 1) / kFwdBQ, a.B * a.H);
   const bool drop = a.drop_thresh > 0;
+  if (drop && !a.dmask) return -3;
   ATTN_DISPATCH(dt, T, ATTN_DISPATCH_D(a.D, D, ATTN_DISPATCH_B(a.causal, C, ATTN_DISPATCH_B(drop, DR,
       hipLaunchKernelGGL((attn_fwd_kernel<T, D, C, DR>), grid, dim3(256), 0, s, a)))));
   return (int)hipGetLastError();
@@ -651,24 +937,27 @@ int attn_fwd(const AttnArgs& a, int dt, hipStream_t s) {
 
 bool attn_bwd_needs_dq_acc(const AttnArgs& a) { return a.Sk > kBwdBK; }
 
-int attn_bwd(const AttnArgs& a, const void* dout, float* dq_acc, void* dk, void* dv, int dt,
+int attn_bwd(const AttnArgs& a, const void* dout, float* delta_ws, void* dk, void* dv, int dt,
              hipStream_t s) {
   if (a.B * a.H == 0 || a.Sq == 0) return 0;
   const bool drop = a.drop_thresh > 0;
   if (drop && !a.dmask) return -3;  // backward needs the forward's dropout bits
-  const int64_t rows = (int64_t)a.B * a.H * a.Sq;
   const bool multi = attn_bwd_needs_dq_acc(a);
-  if (multi) hipMemsetAsync(dq_acc, 0, rows * a.D * sizeof(float), s);
+  if (multi && !delta_ws) return -4;
   ATTN_DISPATCH(dt, T, ATTN_DISPATCH_D(a.D, D, {
     dim3 grid((a.Sk + kBwdBK - 1) / kBwdBK, a.B * a.H);
-    ATTN_DISPATCH_B(a.causal, C, ATTN_DISPATCH_B(drop, DR, ATTN_DISPATCH_B(a.dsum != nullptr, DS,
-        hipLaunchKernelGGL((attn_bwd_kernel<T, D, C, DR, DS>), grid, dim3(256), 0, s, a, dout, dq_acc, dk,
-                           dv))));
-    if (multi) {
-      const int64_t tot = rows * (D / 8);
-      hipLaunchKernelGGL((attn_dq_convert<T, D>), dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s,
-                         a, dq_acc);
-    }
+    ATTN_DISPATCH_B(a.causal, C, ATTN_DISPATCH_B(drop, DR, ATTN_DISPATCH_B(a.dsum != nullptr, DS, {
+      if (multi) {
+        hipLaunchKernelGGL((attn_bwd_kernel<T, D, C, DR, DS, false>), grid, dim3(256), 0, s, a, dout, delta_ws, dk,
+                           dv);
+        dim3 qgrid((a.Sq + kFwdBQ - 1) / kFwdBQ, a.B * a.H);
+        hipLaunchKernelGGL((attn_bwd_dq_kernel<T, D, C, DR, DS>), qgrid, dim3(256), 0, s, a, dout,
+                           (const float*)delta_ws);
+      } else {
+        hipLaunchKernelGGL((attn_bwd_kernel<T, D, C, DR, DS, true>), grid, dim3(256), 0, s, a, dout, nullptr, dk,
+                           dv);
+      }
+    })));
   }));
   return (int)hipGetLastError();
 }

@@ -315,9 +315,10 @@ apex::AttnArgs attn_common(const Tensor& q, const Tensor& k, const Tensor& v, bo
   a.scale = (float)scale;
   a.scale_log2 = (float)(scale * 1.4426950408889634);
   TORCH_CHECK(p_drop >= 0.0 && p_drop < 1.0, "dropout p must be in [0, 1)");
-  a.drop_thresh = p_drop > 0.0 ? (uint32_t)std::lround(p_drop * 65536.0) : 0u;
-  if (p_drop > 0.0 && a.drop_thresh == 0) a.drop_thresh = 1;
-  a.drop_scale = p_drop > 0.0 ? (float)(1.0 / (1.0 - a.drop_thresh / 65536.0)) : 1.f;
+  // attention dropout draws 8-bit uniforms (keep iff u8 >= thresh, p quantised to 1/256 as in
+  // FlashAttention-2); the rescale uses the quantised keep probability, so E[output] is exact
+  a.drop_thresh = apex::attn_drop_thresh(p_drop);
+  a.drop_scale = p_drop > 0.0 ? (float)(256.0 / (256.0 - a.drop_thresh)) : 1.f;
   a.seed = (uint64_t)seed;
   a.offset = (uint64_t)offset;
   if (k_lens.has_value() && k_lens->defined()) {
@@ -374,9 +375,9 @@ void flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor 
     a.dmask = (uint16_t*)dmask->data_ptr();
   }
   const int64_t rows = (int64_t)a.B * a.H * a.Sq;
-  Tensor dq_acc;
-  if (apex::attn_bwd_needs_dq_acc(a)) dq_acc = at::empty({rows * a.D}, q.options().dtype(at::kFloat));
-  check(apex::attn_bwd(a, dout.data_ptr(), dq_acc.defined() ? dq_acc.data_ptr<float>() : nullptr,
+  Tensor delta_ws;  // rowsum(dO * O) handed from the dK/dV kernel to the dQ kernel
+  if (apex::attn_bwd_needs_dq_acc(a)) delta_ws = at::empty({rows}, q.options().dtype(at::kFloat));
+  check(apex::attn_bwd(a, dout.data_ptr(), delta_ws.defined() ? delta_ws.data_ptr<float>() : nullptr,
                        dk.data_ptr(), dv.data_ptr(), dt_code(q.scalar_type()), cur_stream()),
         "attn_bwd");
 }
@@ -715,8 +716,7 @@ Tensor k_smx_bwd(Tensor dy, Tensor y, double scale) {
 Tensor flash_dropout_mask(int64_t B, int64_t H, int64_t Sq, int64_t Sk, double p_drop, int64_t seed,
                           int64_t offset, at::Device dev) {
   Tensor out = at::empty({B, H, Sq, Sk}, at::TensorOptions().dtype(at::kByte).device(dev));
-  uint32_t th = p_drop > 0.0 ? (uint32_t)std::lround(p_drop * 65536.0) : 0u;
-  if (p_drop > 0.0 && th == 0) th = 1;
+  const uint32_t th = apex::attn_drop_thresh(p_drop);
   check(apex::attn_dropout_mask(out.data_ptr<uint8_t>(), B * H, (int)Sq, (int)Sk, (uint64_t)seed,
                                 (uint64_t)offset, th, cur_stream()),
         "attn_dropout_mask");

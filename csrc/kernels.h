@@ -85,18 +85,25 @@ struct AttnArgs {
   int B, H, Sq, Sk, D;
   int causal;
   float scale, scale_log2;
-  uint32_t drop_thresh;  // keep iff 16-bit uniform >= drop_thresh (0 = no dropout)
-  float drop_scale;      // 1 / (1 - p)
+  uint32_t drop_thresh;  // keep iff 8-bit uniform >= drop_thresh (0 = no dropout)
+  float drop_scale;      // 256 / (256 - drop_thresh)
   uint64_t seed, offset;
   const int* k_lens;     // optional per-batch valid key length
-  uint16_t* dmask;       // dropout keep bits [B*H, Sq, mask_words] (fwd writes, bwd reads)
-  int64_t mask_words;    // 2 * ceil(Sk / 32)
+  uint16_t* dmask;       // dropout keep bits [B*H, Sq, mask_words] (fwd writes, bwd reads): one
+                         // 32-bit word per (row, 32-key block), bit k <-> key 32 blk + k
+  int64_t mask_words;    // 2 * ceil(Sk / 32) (uint16 units)
   float* dsum;           // optional, zeroed [B][3][H][D]: bwd adds the column sums (over positions)
                          // of dq, dk, dv — the packed-QKV projection's bias gradient, per batch
 };
+inline uint32_t attn_drop_thresh(double p) {  // 8-bit keep threshold in [1, 255], 0 = off
+  if (p <= 0.0) return 0u;
+  long t = (long)(p * 256.0 + 0.5);
+  return (uint32_t)(t < 1 ? 1 : t > 255 ? 255 : t);
+}
 int attn_fwd(const AttnArgs& a, int dt, hipStream_t s);
 bool attn_bwd_needs_dq_acc(const AttnArgs& a);
-int attn_bwd(const AttnArgs& a, const void* dout, float* dq_acc, void* dk, void* dv, int dt,
+// delta_ws: [B*H*Sq] fp32 workspace when attn_bwd_needs_dq_acc (two-kernel backward)
+int attn_bwd(const AttnArgs& a, const void* dout, float* delta_ws, void* dk, void* dv, int dt,
              hipStream_t s);
 int attn_dropout_mask(uint8_t* out, int64_t BH, int Sq, int Sk, uint64_t seed, uint64_t offset,
                       uint32_t thresh, hipStream_t s);
