@@ -464,17 +464,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 6
         pf_q[c] = pf_do[c] = pf_o[c] = make_uint4(0, 0, 0, 0);
       }
     }
+    // raw values only: any arithmetic on a loaded value here would make the compiler wait for
+    // the whole prefetch (s_waitcnt vmcnt(0)) instead of letting it land during the next step
     if (threadIdx.x < kBwdBQ) {
       const int q = qb + threadIdx.x;
-      pf_lse = q < nq ? lsep[q] * kLog2e : INFINITY;
+      if (q < nq) pf_lse = lsep[q];  // natural log; x log2(e) at staging
     }
     if (DROPOUT && threadIdx.x < 4 * kBwdBQ) {
       // dropout words written by the forward: one per (query, 32-key block), bit k <-> key k
       const int qi = threadIdx.x & (kBwdBQ - 1), w = threadIdx.x / kBwdBQ;
       const int q = qb + qi, blk = (k0 >> 5) + w;
-      pf_mask = (q < nq && blk * 32 < a.Sk)
-                    ? ((const uint32_t*)(a.dmask + ((int64_t)bh * a.Sq + q) * a.mask_words))[blk]
-                    : 0u;
+      if (q < nq && blk * 32 < a.Sk) pf_mask = ((const uint32_t*)(a.dmask + ((int64_t)bh * a.Sq + q) * a.mask_words))[blk];
     }
   };
   if (qstart < nq) fetch(pfa, qstart);
@@ -507,9 +507,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 6
       *(uint4*)(lds_q + row * LDR + col) = pf_q[c];
       *(uint4*)(lds_do + row * LDR + col) = pf_do[c];
     }
-    if (threadIdx.x < kBwdBQ) lds_lse[threadIdx.x] = P.lse;
+    if (threadIdx.x < kBwdBQ) lds_lse[threadIdx.x] = P.lse * kLog2e;  // +inf stays +inf
     if (DROPOUT && threadIdx.x < 4 * kBwdBQ) lds_mask[threadIdx.x] = P.mask;
-    if (qb + AHEAD * kBwdBQ < nq) fetch(P, qb + AHEAD * kBwdBQ);
+    if (qb + AHEAD * kBwdBQ < nq && !(a.dbg & 8)) fetch(P, qb + AHEAD * kBwdBQ);
     lds_barrier();
 
     // S = Q . K^T  [32 q x 32 keys]: A = Q rows (LDS), B = K rows (regs)
@@ -554,7 +554,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 6
     // dV += P^T . dO : accumulator-as-A (contraction over q = rows), B = dO via tr reads
     // dK += dS^T . Q : same with Q
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
+    for (int s2 = 0; s2 < 2 && !(a.dbg & 2); ++s2) {
       const V8 pa = pack8<T, V8>(pd + 8 * s2);
       const V8 sa = pack8<T, V8>(ds + 8 * s2);
       const int kq = 16 * s2 + 4 * hl + ((lane & 15) >> 2);
@@ -567,7 +567,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 6
         dk[db] = M::mma(sa, qbf, dk[db]);
       }
     }
-    if constexpr (DQ) {
+    if (DQ && !(a.dbg & 1)) {
     // dS to LDS as [q][key] (bf16) for dQ = dS . K
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -766,7 +766,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 6
 #pragma unroll
       for (int sb = 0; sb < 2; ++sb) {
         const int blk = (kt * kFwdKB >> 5) + sb;
-        R.m[sb] = (mrow && blk * 32 < a.Sk) ? mrow[blk] >> (4 * hl) : 0u;
+        R.m[sb] = 0u;
+        if (mrow && blk * 32 < a.Sk) R.m[sb] = mrow[blk];  // raw: shifted at use (no wait here)
       }
     }
   };
@@ -788,7 +789,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 6
   auto tile = [&](KV& R, const int kt) {
     lds_barrier();  // previous tile fully consumed
     lstore(R);
-    const uint32_t mcur[2] = {R.m[0], R.m[1]};
+    const uint32_t mcur[2] = {R.m[0] >> (4 * hl), R.m[1] >> (4 * hl)};
     lds_barrier();
     if (kt + AHEAD < ntiles) gload(R, kt + AHEAD);
     const int kb = kt * kFwdKB;

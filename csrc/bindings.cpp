@@ -352,8 +352,9 @@ std::vector<Tensor> flash_attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, do
 void flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor dq,
                     Tensor dk, Tensor dv, bool causal, double scale, double p_drop, int64_t seed,
                     int64_t offset, const c10::optional<Tensor>& k_lens,
-                    const c10::optional<Tensor>& dmask, const c10::optional<Tensor>& dsum) {
+                    const c10::optional<Tensor>& dmask, const c10::optional<Tensor>& dsum, int64_t dbg) {
   apex::AttnArgs a = attn_common(q, k, v, causal, scale, p_drop, seed, offset, k_lens);
+  a.dbg = (int)dbg;
   if (dsum.has_value() && dsum->defined()) {
     TORCH_CHECK(dsum->is_cuda() && dsum->scalar_type() == at::kFloat && dsum->is_contiguous() &&
                     dsum->numel() == (int64_t)a.B * 3 * a.H * a.D,
@@ -916,7 +917,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("flash_attn_bwd", &flash_attn_bwd, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"),
         py::arg("o"), py::arg("lse"), py::arg("dq"), py::arg("dk"), py::arg("dv"), py::arg("causal"),
         py::arg("scale"), py::arg("p_drop"), py::arg("seed"), py::arg("offset"), py::arg("k_lens"),
-        py::arg("dmask"), py::arg("dsum") = py::none());
+        py::arg("dmask"), py::arg("dsum") = py::none(), py::arg("dbg") = 0);
   m.def("partial_colsum", &k_partial_colsum);
   m.def("flash_dropout_mask", &flash_dropout_mask);
   m.def("weight_norm_fwd", &k_wn_fwd);
