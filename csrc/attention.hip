@@ -392,28 +392,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 6
   const T* op = (const T*)a.o + b * a.o_bs + h * a.o_hs;
   const float* lsep = a.lse + (int64_t)bh * a.Sq;
 
-  // K and V rows for this wave's 32 keys as B operands: lane (key=r, hl) holds X[key][16s+8hl..]
-  V8 kf[D / 16], vf[D / 16];
-#pragma unroll
-  for (int s = 0; s < D / 16; ++s) {
-    if (mykey < Sk) {
-      kf[s] = *(const V8*)(kp + (int64_t)mykey * a.k_ss + 16 * s + 8 * hl);
-      vf[s] = *(const V8*)(vp + (int64_t)mykey * a.v_ss + 16 * s + 8 * hl);
-    } else {
-      kf[s] = V8{};
-      vf[s] = V8{};
-    }
-  }
-  // whole K block to LDS (needed as the B operand of dQ = dS.K via tr reads)
-  if (DQ)
-  for (int idx = threadIdx.x; idx < kBwdBK * (D / 8); idx += 256) {
-    const int row = idx / (D / 8), col = (idx % (D / 8)) * 8;
-    const int key = k0 + row;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (key < Sk) v = *(const uint4*)(kp + (int64_t)key * a.k_ss + col);
-    *(uint4*)(lds_k + row * LDR + col) = v;
-  }
-
   // accumulators: dK, dV  [key x dim]: C rows = keys (regs), cols = dim (lanes)
   f32x16 dk[D / 32], dv[D / 32];
 #pragma unroll
@@ -477,8 +455,35 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 6
       if (q < nq && blk * 32 < a.Sk) pf_mask = ((const uint32_t*)(a.dmask + ((int64_t)bh * a.Sq + q) * a.mask_words))[blk];
     }
   };
+  V8 kf[D / 16], vf[D / 16];
+  auto load_kv = [&]() {
+  // K and V rows for this wave's 32 keys as B operands: lane (key=r, hl) holds X[key][16s+8hl..]
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) {
+    if (mykey < Sk) {
+      kf[s] = *(const V8*)(kp + (int64_t)mykey * a.k_ss + 16 * s + 8 * hl);
+      vf[s] = *(const V8*)(vp + (int64_t)mykey * a.v_ss + 16 * s + 8 * hl);
+    } else {
+      kf[s] = V8{};
+      vf[s] = V8{};
+    }
+  }
+  // whole K block to LDS (needed as the B operand of dQ = dS.K via tr reads)
+  if (DQ)
+  for (int idx = threadIdx.x; idx < kBwdBK * (D / 8); idx += 256) {
+    const int row = idx / (D / 8), col = (idx % (D / 8)) * 8;
+    const int key = k0 + row;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (key < Sk) v = *(const uint4*)(kp + (int64_t)key * a.k_ss + col);
+    *(uint4*)(lds_k + row * LDR + col) = v;
+  }
+  };
+  // D = 64: the K/V loads are issued after the first query-block fetch, so both latencies
+  // overlap (at D = 128 that order spills registers)
+  if (D == 128) load_kv();
   if (qstart < nq) fetch(pfa, qstart);
   if (DEPTH2 && qstart + kBwdBQ < nq) fetch(pfb, qstart + kBwdBQ);
+  if (D == 64) load_kv();
 
   float dq_colsum = 0.f;  // DSUM: this lane's dq column (32cb + r) summed over its query rows
   auto body = [&](Pf& P, const int qb) {
@@ -648,34 +653,34 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 6
     const float t = dq_colsum + __shfl_xor(dq_colsum, 32, 64);
     if (hl == 0) atomicAdd(dsum + 32 * wid + r, t);
   }
-  const bool kfull = k0 + 32 * wid + 32 <= a.Sk;
+  // dK then dV staged through LDS ([key][D] rows in lds_k) so the global stores are 16-byte
+  // row chunks (4 per thread at D = 64) instead of 2-byte column scatters (32 per lane)
+  lds_barrier();  // every wave is done reading lds_k (dQ products)
+  auto emit = [&](const f32x16 (&acc)[D / 32], const float mul, T* dst, const int64_t ss, float* dsum_t) {
 #pragma unroll
-  for (int db = 0; db < D / 32; ++db) {
-    float sk = 0.f, sv = 0.f;
-    auto store = [&](auto guarded) {
+    for (int db = 0; db < D / 32; ++db) {
+      float sum = 0.f;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const int key = k0 + 32 * wid + (i & 3) + 8 * (i >> 2) + 4 * hl;
-        if (!decltype(guarded)::value || key < a.Sk) {
-          const T vk = (T)(dk[db][i] * a.scale), vv = (T)(dv[db][i] * rkeep);
-          dkp[(int64_t)key * a.dk_ss + 32 * db + r] = vk;
-          dvp[(int64_t)key * a.dv_ss + 32 * db + r] = vv;
-          sk += (float)vk;
-          sv += (float)vv;
-        }
+        const int kl = 32 * wid + (i & 3) + 8 * (i >> 2) + 4 * hl;
+        const T v = (T)(acc[db][i] * mul);
+        lds_k[kl * LDR + 32 * db + r] = v;
+        if constexpr (DSUM) sum += (k0 + kl < a.Sk) ? (float)v : 0.f;
       }
-    };
-    if (kfull) store(std::false_type{});  // uniform: no per-element guards
-    else store(std::true_type{});
-    if constexpr (DSUM) {
-      sk += __shfl_xor(sk, 32, 64);
-      sv += __shfl_xor(sv, 32, 64);
-      if (hl == 0) {
-        atomicAdd(dsum + (int64_t)a.H * D + 32 * db + r, sk);
-        atomicAdd(dsum + (int64_t)2 * a.H * D + 32 * db + r, sv);
+      if constexpr (DSUM) {
+        sum += __shfl_xor(sum, 32, 64);
+        if (hl == 0) atomicAdd(dsum_t + 32 * db + r, sum);
       }
     }
-  }
+    lds_barrier();
+    for (int idx = threadIdx.x; idx < kBwdBK * (D / 8); idx += 256) {
+      const int row = idx / (D / 8), col = (idx % (D / 8)) * 8;
+      if (k0 + row < a.Sk) *(uint4*)(dst + (int64_t)(k0 + row) * ss + col) = *(const uint4*)(lds_k + row * LDR + col);
+    }
+    lds_barrier();
+  };
+  emit(dk, a.scale, dkp, a.dk_ss, DSUM ? dsum + (int64_t)a.H * D : nullptr);
+  emit(dv, rkeep, dvp, a.dv_ss, DSUM ? dsum + (int64_t)2 * a.H * D : nullptr);
 }
 
 // dQ for key ranges longer than one backward key block: query-stationary, the forward's
