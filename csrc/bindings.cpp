@@ -914,6 +914,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd", &xent_bwd);
   m.def("flash_attn_fwd", &flash_attn_fwd);
+  m.def("gemm_set_dbg", [](int64_t v) { check(apex::gemm_set_dbg((int)v), "gemm_set_dbg"); });
   m.def("flash_attn_bwd", &flash_attn_bwd, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"),
         py::arg("o"), py::arg("lse"), py::arg("dq"), py::arg("dk"), py::arg("dv"), py::arg("causal"),
         py::arg("scale"), py::arg("p_drop"), py::arg("seed"), py::arg("offset"), py::arg("k_lens"),

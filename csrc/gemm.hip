@@ -483,12 +483,23 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[4][8], char* reg, T*
   else body(std::integral_constant<bool, false>{});
 }
 
+// diagnostics only (tools/gemm_epi_cost.py): 2 = skip the epilogue (main-loop-only timing)
+__device__ int g_gemm_dbg = 0;
+// First-round stagger (experiment, off by default): half of the first round's workgroups
+// (bid & 8) sleep g_gemm_stagger x s_sleep(127) before starting, offsetting every later tile on
+// those CUs so their epilogues (HBM + VALU, MFMA idle) run beside the other half's main loops.
+// Isolated GEMMs (tools/gemm_stagger.py, M = 32768, N = 4096, K = 1024): bias+GELU 362 -> 312 us,
+// dGELU 429 -> 405 at 2 units; the whole BERT-Large step was 2.4 % SLOWER with it (same-box A/B,
+// profiles/r1_gemm_stagger.json), so the launchers pass 0.
+__device__ int g_gemm_stagger = 0;
+
 template <typename T, int EPI, bool TR>
 __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(const T* __restrict__ A, const T* __restrict__ B,
                                                             T* __restrict__ C, int M, int N, int K, int64_t lda,
                                                             int64_t ldb, int64_t ldc, const T* __restrict__ bias,
                                                             const T* __restrict__ aux, int64_t ldaux,
-                                                            T* __restrict__ aux_out, float* __restrict__ part) {
+                                                            T* __restrict__ aux_out, float* __restrict__ part,
+                                                            int stagger) {
   __shared__ __attribute__((aligned(16))) char smem[G_LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -514,6 +525,12 @@ __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(const T* __restrict_
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  {
+    const int st = g_gemm_stagger > 0 ? g_gemm_stagger : g_gemm_stagger < 0 ? 0 : stagger;
+    if (st > 0 && bid < 256 && (bid & 8)) {
+      for (int i = 0; i < st; ++i) __builtin_amdgcn_s_sleep(127);
+    }
+  }
   if constexpr (TR) {  // split-K slice blockIdx.y: K-rows [y*K, (y+1)*K) of both operands
     A += (int64_t)blockIdx.y * K * lda;
     B += (int64_t)blockIdx.y * K * ldb;
@@ -536,9 +553,19 @@ __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(const T* __restrict_
     return;
   }
 
+  if (__builtin_expect(g_gemm_dbg == 2, 0)) {  // keep the accumulators live, store nothing
+    float t = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) t += acc[j][i][0] + acc[j][i][1] + acc[j][i][2] + acc[j][i][3];
+    if (t == 1.2345e-30f) C[0] = from_f<T>(t);
+    return;
+  }
   epilogue<T, EPI, GB_M, GB_N>(acc, smem + wid * 16384, C, M, N, ldc, bias, aux, ldaux, aux_out, part, m0, n0, tm, wr,
                                 wc, lane);
 }
+
 
 // 2-D transpose out[C][R] = in[R][C] (16-bit elements). Each lane transposes an 8x8 block in
 // registers: 8 x 16-B row loads, 8 x 16-B row stores. A wave is 8 (along C) x 8 (along R) blocks,
@@ -572,9 +599,10 @@ __global__ void __launch_bounds__(256) transpose_kernel(const T* __restrict__ in
 template <typename T, int EPI, bool TR = false>
 void launch_gemm(const GemmArgs& g, hipStream_t s) {
   const int tiles = ((g.M + GB_M - 1) / GB_M) * ((g.N + GB_N - 1) / GB_N);
+  const int stagger = 0;  // see g_gemm_stagger
   hipLaunchKernelGGL((gemm_nt_kernel<T, EPI, TR>), dim3(tiles, TR ? g.splits : 1), dim3(G_THREADS), 0, s, (const T*)g.A, (const T*)g.B,
                      (T*)g.C, g.M, g.N, g.K, g.lda, g.ldb, g.ldc, (const T*)g.bias, (const T*)g.aux, g.ldaux,
-                     (T*)g.aux_out, g.part);
+                     (T*)g.aux_out, g.part, stagger);
 }
 
 template <typename T>
@@ -600,6 +628,15 @@ bool gemm_supported(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc) 
 }
 
 int64_t gemm_part_rows(int M) { return (int64_t)((M + GB_M - 1) / GB_M) * 2; }
+
+int gemm_set_dbg(int v) {
+  // v < 0: -v = stagger units (experiment); v >= 0: diagnostics mode
+  if (v < 0) {  // -100: force no stagger; -200: launcher's choice; -k: k units
+    const int st = v == -100 ? -1 : v == -200 ? 0 : -v;
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_gemm_stagger), &st, sizeof(int));
+  }
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_gemm_dbg), &v, sizeof(int));
+}
 
 int gemm_nt(const GemmArgs& g, int dt, hipStream_t s) {
   if (!gemm_supported(g.M, g.N, g.K, g.lda, g.ldb, g.ldc)) return -2;

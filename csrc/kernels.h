@@ -196,6 +196,7 @@ struct GemmArgs {
 bool gemm_supported(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc);
 int64_t gemm_part_rows(int M);
 int gemm_nt(const GemmArgs& g, int dt, hipStream_t s);
+int gemm_set_dbg(int v);  // diagnostics: 2 = skip the epilogue
 // weight-gradient form: C[P, Q] = A^T B with A [R, P], B [R, Q] row-major (contraction over rows)
 bool gemm_tt_supported(int P, int Q, int R, int splits, int64_t lda, int64_t ldb);
 int gemm_tt(const GemmArgs& g, int dt, hipStream_t s);
