@@ -20,6 +20,8 @@ The numerics are those of the unfused composition in apex.ops.fused (tests compa
 """
 from __future__ import annotations
 
+import os
+
 import math
 
 import torch
@@ -28,6 +30,10 @@ from .. import _ext
 from . import gemm as G
 from .fused import ACT_GELU, _2d, _seed, _wgrad
 
+
+# MLP forward keeps gelu'(h) for the backward (EPI_BIAS_GELU_D + EPI_MUL) by default;
+# APEX_MLP_STORE=h keeps the pre-activation and re-evaluates erf/exp in the backward epilogue
+_STORE_DERIV = os.environ.get("APEX_MLP_STORE", "deriv") != "h"
 
 class _AttnSublayer(torch.autograd.Function):
     @staticmethod
@@ -79,7 +85,9 @@ class _FFNSublayer(torch.autograd.Function):
         C = _ext.require()
         x2 = _2d(x)
         if act == ACT_GELU and b1 is not None:
-            g, h = G.linear_gelu(x2, w1, b1)  # h = x W1^T + b1 (pre-activation), g = gelu(h)
+            # g = gelu(h), h = x W1^T + b1; the backward keeps gelu'(h) (computed in this epilogue
+            # from the same exp/erf) rather than h
+            g, h = G.linear_gelu_d(x2, w1, b1) if _STORE_DERIV else G.linear_gelu(x2, w1, b1)
             hb = None
         else:
             h = torch.mm(x2, w1.t())
@@ -99,7 +107,10 @@ class _FFNSublayer(torch.autograd.Function):
         p, seed, off, act, has_b2, b1dt = ctx.cfg
         dres, dt, dgamma, dbeta, db2 = C.bdaln_bwd(_2d(dy), s, gamma, mean, rstd, float(p), seed, off, has_b2)
         if hb is None and act == ACT_GELU and b1dt is not None:
-            dh, db1 = G.dgrad_dgelu(dt, w2, h, b1dt)  # (dt W2) * gelu'(h) and its column sums
+            if _STORE_DERIV:
+                dh, db1 = G.dgrad_mul(dt, w2, h, b1dt)  # (dt W2) * gelu'(h) (stored) and its column sums
+            else:
+                dh, db1 = G.dgrad_dgelu(dt, w2, h, b1dt)  # (dt W2) * gelu'(h) from h
         else:
             dh, db1 = C.bias_act_bwd(G.dgrad(dt, w2), h, hb, act)
         dw2 = _wgrad(dt, g)
@@ -118,18 +129,24 @@ class _MLP(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w1, b1, w2, act):
         x2 = _2d(x)
-        g, h = G.linear_gelu(x2, w1, b1, act)
+        if _STORE_DERIV:
+            g, gd = G.linear_gelu_d(x2, w1, b1, act)  # gelu(h) and gelu'(h)
+        else:
+            g, gd = G.linear_gelu(x2, w1, b1, act)  # gelu(h) and h
         t = G.linear(g, w2)
-        ctx.save_for_backward(x2, w1, h, g, w2)
+        ctx.save_for_backward(x2, w1, gd, g, w2)
         ctx.act = act
         ctx.b1dt = b1.dtype
         return t.view(*x.shape[:-1], w2.shape[0])
 
     @staticmethod
     def backward(ctx, dt):
-        x2, w1, h, g, w2 = ctx.saved_tensors
+        x2, w1, gd, g, w2 = ctx.saved_tensors
         dt2 = _2d(dt).contiguous()
-        dh, db1 = G.dgrad_dgelu(dt2, w2, h, ctx.b1dt, act=ctx.act)
+        if _STORE_DERIV:
+            dh, db1 = G.dgrad_mul(dt2, w2, gd, ctx.b1dt)
+        else:
+            dh, db1 = G.dgrad_dgelu(dt2, w2, gd, ctx.b1dt, act=ctx.act)
         dw2 = _wgrad(dt2, g)
         dx = G.dgrad(dh, w1).view(*dt.shape[:-1], w1.shape[1])
         dw1 = _wgrad(dh, x2)

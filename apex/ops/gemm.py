@@ -5,6 +5,8 @@
   dgrad(dy, W)                 dx = dy W        (via W^T, K-contiguous)
   dgrad_resid(dy, W, r)        dx = dy W + r                         EPI_RESID
   dgrad_dgelu(dy, W, h)        dh = (dy W) * gelu'(h), db = sum(dh)  EPI_DGELU
+  linear_gelu_d(x, W, b)       y = gelu(h), g = gelu'(h) -> (y, g)   EPI_BIAS_GELU_D
+  dgrad_mul(dy, W, g)          dh = (dy W) * g, db = sum(dh)          EPI_MUL
 
 The kernel takes both operands K-contiguous (A[M,K], B[N,K]); the input-gradient GEMMs use a
 transposed copy of W made by a HIP transpose kernel (cheap next to the GEMM: 2 bytes/weight
@@ -93,6 +95,37 @@ def linear_gelu(x, w, b, act=ACT_GELU):
         h = h + b if b is not None else h  # the pre-activation as the fused path stores it
     shp = (*x.shape[:-1], w.shape[0])
     return y.view(shp), h.view(shp)
+
+
+def linear_gelu_d(x, w, b, act=ACT_GELU):
+    """(gelu(h), gelu'(h)) with h = x w^T + b: the forward of an MLP whose backward multiplies by
+    the stored derivative (dgrad_mul) instead of re-evaluating erf/exp from h. The derivative
+    is taken at the rounded h, as the unfused composition's backward would."""
+    a = _2d(x)
+    C = _C()
+    if use_mfma(a, w) and b is not None and b.dtype == x.dtype:
+        y, gd = C.gemm(a, w, C.EPI_BIAS_GELU_TANH_D if act == ACT_GELU_TANH else C.EPI_BIAS_GELU_D, b)
+    else:
+        h = torch.mm(a, w.t())
+        y = C.bias_act_fwd(h, b, act)
+        gd, _ = C.bias_act_bwd(torch.ones_like(h), h, b, act)  # gelu'(h + b)
+    shp = (*x.shape[:-1], w.shape[0])
+    return y.view(shp), gd.view(shp)
+
+
+def dgrad_mul(dy, w, gd, bias_dtype, wT=None):
+    """(dh, db): dh = (dy @ w) * gd (gd = the stored activation derivative), db = column sums of dh."""
+    a = _2d(dy)
+    g2 = _2d(gd)
+    C = _C()
+    if _MODE != "blas" and a.is_cuda and g2.is_contiguous() and g2.dtype == a.dtype:
+        wT = transpose(w) if wT is None else wT
+        if use_mfma(a, wT):
+            dh, db = C.gemm(a, wT, C.EPI_MUL, None, g2, bias_dtype)
+            return dh, db
+    dh = torch.mm(a, w) * g2
+    db = C.colsum(dh, bias_dtype) if bias_dtype is not None else None
+    return dh, db
 
 
 def dgrad(dy, w, wT=None):

@@ -756,7 +756,7 @@ Tensor k_input_normalize(Tensor x, std::vector<double> mean, std::vector<double>
 
 // ---------------------------------------------------------------------------
 // MFMA GEMM (gemm.hip): C = epi(A[M,K] . B[N,K]^T). Returns [C, H] (H: pre-activation for
-// EPI_BIAS_GELU) or [C, dbias] (EPI_DGELU). A may be any [..., K] view with a unit inner stride.
+// EPI_BIAS_GELU, gelu'(H) for EPI_BIAS_GELU_D) or [C, dbias] (EPI_DGELU, EPI_MUL). A may be any [..., K] view with a unit inner stride.
 // ---------------------------------------------------------------------------
 bool k_gemm_supported(Tensor a, Tensor b) {
   if (!a.is_cuda() || a.dim() < 2 || b.dim() != 2 || a.scalar_type() != b.scalar_type()) return false;
@@ -793,9 +793,10 @@ std::vector<Tensor> k_gemm(Tensor a, Tensor b, int64_t epi, const c10::optional<
   g.ldc = N;
   g.epi = (int)epi;
   Tensor extra;
-  const bool gelu_fwd = epi == apex::EPI_BIAS_GELU || epi == apex::EPI_BIAS_GELU_TANH;
-  const bool dgelu = epi == apex::EPI_DGELU || epi == apex::EPI_DGELU_TANH;
-  TORCH_CHECK(epi >= 0 && epi <= apex::EPI_DGELU_TANH && epi != apex::EPI_F32, "gemm: bad epilogue ", epi);
+  const bool gelu_fwd = epi == apex::EPI_BIAS_GELU || epi == apex::EPI_BIAS_GELU_TANH ||
+                        epi == apex::EPI_BIAS_GELU_D || epi == apex::EPI_BIAS_GELU_TANH_D;
+  const bool dgelu = epi == apex::EPI_DGELU || epi == apex::EPI_DGELU_TANH || epi == apex::EPI_MUL;
+  TORCH_CHECK(epi >= 0 && epi <= apex::EPI_MUL && epi != apex::EPI_F32, "gemm: bad epilogue ", epi);
   if (epi == apex::EPI_BIAS || gelu_fwd) {
     TORCH_CHECK(bias.has_value() && bias->defined() && bias->is_contiguous() && bias->numel() == N &&
                     bias->scalar_type() == a.scalar_type(),
@@ -958,4 +959,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.attr("EPI_RESID") = (int)apex::EPI_RESID;
   m.attr("EPI_BIAS_GELU_TANH") = (int)apex::EPI_BIAS_GELU_TANH;
   m.attr("EPI_DGELU_TANH") = (int)apex::EPI_DGELU_TANH;
+  m.attr("EPI_BIAS_GELU_D") = (int)apex::EPI_BIAS_GELU_D;
+  m.attr("EPI_BIAS_GELU_TANH_D") = (int)apex::EPI_BIAS_GELU_TANH_D;
+  m.attr("EPI_MUL") = (int)apex::EPI_MUL;
 }

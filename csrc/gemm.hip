@@ -15,6 +15,12 @@
 //                 of C written to `part` (the bias gradient, finished by partial_colsum)
 //   EPI_RESID     C = acc + R[m,n]          (residual-gradient accumulation)
 //   EPI_BIAS_GELU_TANH / EPI_DGELU_TANH: the same with the tanh-approximated GELU (GPT-2)
+//   EPI_BIAS_GELU_D / _TANH_D  C = gelu(H) and gelu'(H) stored instead of H: the derivative shares
+//                 the exp / erf (or sigmoid) of the GELU, so it is a few FMAs here, and the backward
+//                 epilogue becomes
+//   EPI_MUL       C = acc * G[m,n] with the bias-gradient partials of EPI_DGELU — a multiply
+//                 instead of the erf/exp evaluation that made the dGELU epilogue VALU-bound
+//                 (404 vs 201 us main loop at M=32768 N=4096 K=1024, profiles/r1_gemm_stagger.json)
 //
 // Tiling (CDNA4, cdna_hip_programming.md §5):
 //  * 256x256 output tile, BK = 64, 512 threads = 8 waves as 2 (M) x 4 (N); each wave owns a
@@ -101,6 +107,20 @@ __device__ __forceinline__ f32x2 gelu_tanh_grad2(f32x2 x) {
   const f32x2 sg = sig2u(x);
   const f32x2 du = splat(2.f * 0.7978845608028654f) * pk_fma(splat(3.f * 0.044715f) * x, x, splat(1.f));
   return pk_fma(x * sg * (splat(1.f) - sg), du, sg);
+}
+// gelu(x) and gelu'(x) from one exp / erf (or one sigmoid for the tanh form)
+__device__ __forceinline__ void gelu_and_grad2(f32x2 x, bool tanh_form, f32x2& y, f32x2& g) {
+  if (tanh_form) {
+    const f32x2 sg = sig2u(x);
+    y = x * sg;
+    const f32x2 du = splat(2.f * 0.7978845608028654f) * pk_fma(splat(3.f * 0.044715f) * x, x, splat(1.f));
+    g = pk_fma(y * (splat(1.f) - sg), du, sg);
+  } else {
+    const f32x2 e = exp_neg_half_sq2(x);
+    const f32x2 cdf = splat(0.5f) * (splat(1.f) + erf2(x * splat(0.70710678118654752f), e));
+    y = x * cdf;
+    g = pk_fma(x * splat(0.39894228040143268f), e, cdf);
+  }
 }
 __device__ __forceinline__ f32x2 gelu_grad2(f32x2 x) {
   const f32x2 e = exp_neg_half_sq2(x);
@@ -392,9 +412,12 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[4][8], char* reg, T*
   auto body = [&](auto full_tag) {
     constexpr bool F = decltype(full_tag)::value;
     float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    constexpr bool GELU_FWD = EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_TANH;
+    constexpr bool GELU_D = EPI == EPI_BIAS_GELU_D || EPI == EPI_BIAS_GELU_TANH_D;
+    constexpr bool GELU_FWD = EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_TANH || GELU_D;
     constexpr bool DGELU = EPI == EPI_DGELU || EPI == EPI_DGELU_TANH;
-    constexpr bool TANH = EPI == EPI_BIAS_GELU_TANH || EPI == EPI_DGELU_TANH;
+    constexpr bool MUL = EPI == EPI_MUL;
+    constexpr bool COLSUM = DGELU || MUL;
+    constexpr bool TANH = EPI == EPI_BIAS_GELU_TANH || EPI == EPI_DGELU_TANH || EPI == EPI_BIAS_GELU_TANH_D;
     if constexpr (EPI == EPI_BIAS || GELU_FWD) {
       u32x4 braw;
       if constexpr (F) braw = *reinterpret_cast<const u32x4*>(bias + ncol);
@@ -402,7 +425,7 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[4][8], char* reg, T*
       unpack(braw, bv);
     }
     u32x4 ra[16];
-    if constexpr (DGELU || EPI == EPI_RESID) {
+    if constexpr (DGELU || MUL || EPI == EPI_RESID) {
 #pragma unroll
       for (int it = 0; it < 16; ++it) {
         const int m = mrow + it * 8;
@@ -425,14 +448,31 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[4][8], char* reg, T*
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += bv[e];
           const u32x4 hraw = pack(v);
-          if constexpr (F) *reinterpret_cast<u32x4*>(aux_out + (int64_t)m * ldc + ncol) = hraw;
-          else st16(aux_out, m, hraw);
-          unpack(hraw, v);  // GELU of the stored pre-activation
+          if constexpr (!GELU_D) {
+            if constexpr (F) *reinterpret_cast<u32x4*>(aux_out + (int64_t)m * ldc + ncol) = hraw;
+            else st16(aux_out, m, hraw);
+          }
+          unpack(hraw, v);  // GELU of the (rounded) pre-activation, as the unfused composition
+          float gd[8];
 #pragma unroll
           for (int e = 0; e < 8; e += 2) {
-            const f32x2 gv = TANH ? gelu_tanh2(f32x2{v[e], v[e + 1]}) : gelu2(f32x2{v[e], v[e + 1]});
-            v[e] = gv[0];
-            v[e + 1] = gv[1];
+            if constexpr (GELU_D) {
+              f32x2 gv, gg;
+              gelu_and_grad2(f32x2{v[e], v[e + 1]}, TANH, gv, gg);
+              v[e] = gv[0];
+              v[e + 1] = gv[1];
+              gd[e] = gg[0];
+              gd[e + 1] = gg[1];
+            } else {
+              const f32x2 gv = TANH ? gelu_tanh2(f32x2{v[e], v[e + 1]}) : gelu2(f32x2{v[e], v[e + 1]});
+              v[e] = gv[0];
+              v[e + 1] = gv[1];
+            }
+          }
+          if constexpr (GELU_D) {
+            const u32x4 graw = pack(gd);
+            if constexpr (F) *reinterpret_cast<u32x4*>(aux_out + (int64_t)m * ldc + ncol) = graw;
+            else st16(aux_out, m, graw);
           }
         } else {
           float x[8];
@@ -444,6 +484,9 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[4][8], char* reg, T*
               const f32x2 gg = TANH ? gelu_tanh_grad2(f32x2{x[e], x[e + 1]}) : gelu_grad2(f32x2{x[e], x[e + 1]});
               v[e] = ok ? v[e] * gg[0] : 0.f;
               v[e + 1] = ok ? v[e + 1] * gg[1] : 0.f;
+            } else if constexpr (MUL) {
+              v[e] = ok ? v[e] * x[e] : 0.f;
+              v[e + 1] = ok ? v[e + 1] * x[e + 1] : 0.f;
             } else {
               v[e] += x[e];
               v[e + 1] += x[e + 1];
@@ -451,7 +494,7 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[4][8], char* reg, T*
           }
         }
         out = pack(v);
-        if constexpr (DGELU) {
+        if constexpr (COLSUM) {
           float r[8];
           unpack(out, r);  // the bias grad sums the stored (rounded) values
 #pragma unroll
@@ -461,7 +504,7 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[4][8], char* reg, T*
       if constexpr (F) *reinterpret_cast<u32x4*>(C + (int64_t)m * ldc + ncol) = out;
       else st16(C, m, out);
     }
-    if constexpr (DGELU) {
+    if constexpr (COLSUM) {
       // lanes l, l^8, l^16, ... share the column chunk: reduce over the wave's 8 row slots
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -615,6 +658,9 @@ int gemm_dispatch(const GemmArgs& g, hipStream_t s) {
     case EPI_BIAS_GELU_TANH: launch_gemm<T, EPI_BIAS_GELU_TANH>(g, s); break;
     case EPI_DGELU_TANH: launch_gemm<T, EPI_DGELU_TANH>(g, s); break;
     case EPI_RESID: launch_gemm<T, EPI_RESID>(g, s); break;
+    case EPI_BIAS_GELU_D: launch_gemm<T, EPI_BIAS_GELU_D>(g, s); break;
+    case EPI_BIAS_GELU_TANH_D: launch_gemm<T, EPI_BIAS_GELU_TANH_D>(g, s); break;
+    case EPI_MUL: launch_gemm<T, EPI_MUL>(g, s); break;
     default: return -3;
   }
   return (int)hipGetLastError();

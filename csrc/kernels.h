@@ -178,7 +178,9 @@ int xentropy_bwd(const void* dloss, int64_t dloss_stride, int dloss_dt, const vo
 
 // ----------------------------- MFMA GEMM (gemm.hip) ------------------------
 enum GemmEpi : int { EPI_NONE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_DGELU = 3, EPI_RESID = 4, EPI_F32 = 5,
-                     EPI_BIAS_GELU_TANH = 6, EPI_DGELU_TANH = 7 };
+                     EPI_BIAS_GELU_TANH = 6, EPI_DGELU_TANH = 7,
+                     // forward GELU that stores gelu'(h) instead of h, and its backward: C = acc * aux
+                     EPI_BIAS_GELU_D = 8, EPI_BIAS_GELU_TANH_D = 9, EPI_MUL = 10 };
 struct GemmArgs {
   const void* A;  // [M, K] row-major, lda
   const void* B;  // [N, K] row-major, ldb
@@ -186,10 +188,10 @@ struct GemmArgs {
   int M, N, K;
   int64_t lda, ldb, ldc;
   const void* bias;  // [N]            EPI_BIAS, EPI_BIAS_GELU
-  const void* aux;   // [M, N], ldaux  EPI_DGELU (pre-activation H), EPI_RESID (residual)
+  const void* aux;   // [M, N], ldaux  EPI_DGELU (pre-activation H), EPI_RESID (residual), EPI_MUL (gelu'(H))
   int64_t ldaux;
-  void* aux_out;     // [M, N], ldc    EPI_BIAS_GELU (pre-activation H)
-  float* part;       // [gemm_part_rows(M), N] fp32  EPI_DGELU (bias-grad partials)
+  void* aux_out;     // [M, N], ldc    EPI_BIAS_GELU (pre-activation H), EPI_BIAS_GELU_D (gelu'(H))
+  float* part;       // [gemm_part_rows(M), N] fp32  EPI_DGELU / EPI_MUL (bias-grad partials)
   int epi;
   int splits;        // gemm_tt: split-K slices (blockIdx.y)
 };

@@ -83,6 +83,59 @@ def test_gemm_dgelu_bias_grad(M, N, K):
     torch.testing.assert_close(db, dh.float().sum(0), rtol=1e-4, atol=1e-3)
 
 
+def _gelu_grad_ref(h, tanh):
+    hr = h.float().requires_grad_(True)
+    F.gelu(hr, approximate="tanh" if tanh else "none").backward(torch.ones_like(hr))
+    return hr.grad
+
+
+@pytest.mark.parametrize("tanh", [False, True])
+@pytest.mark.parametrize("M,N,K", [(1000, 1600, 1600), (4096, 4096, 1024), (300, 200, 128)])
+def test_gemm_bias_gelu_stores_derivative(M, N, K, tanh):
+    """EPI_BIAS_GELU_D: y = gelu(h), aux = gelu'(h) at the rounded h (fp32 reference)."""
+    C = _C()
+    a = (torch.randn(M, K, device=DEV) / K ** 0.5).bfloat16()
+    b = torch.randn(N, K, device=DEV).bfloat16()
+    bias = torch.randn(N, device=DEV).bfloat16()
+    y, gd = C.gemm(a, b, C.EPI_BIAS_GELU_TANH_D if tanh else C.EPI_BIAS_GELU_D, bias)
+    href = (_ref_mm(a, b) + bias.float()).bfloat16().float()  # the kernel rounds h first
+    _close(y, F.gelu(href, approximate="tanh" if tanh else "none"), 1.5e-2)
+    _close(gd, _gelu_grad_ref(href, tanh), 1.5e-2)
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 1600, 1600), (4096, 4096, 1024), (300, 200, 128)])
+def test_gemm_mul_bias_grad(M, N, K):
+    """EPI_MUL: dh = (A B^T) * G and the bias gradient from the stored dh."""
+    C = _C()
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    b = (torch.randn(N, K, device=DEV) / K ** 0.5).bfloat16()
+    g = torch.rand(M, N, device=DEV).bfloat16()
+    dh, db = C.gemm(a, b, C.EPI_MUL, None, g, torch.float32)
+    _close(dh, _ref_mm(a, b) * g.float(), 1.5e-2)
+    torch.testing.assert_close(db, dh.float().sum(0), rtol=1e-4, atol=1e-3)
+
+
+def test_mlp_stored_derivative_matches_reference():
+    """apex.ops.blocks.mlp (GELU-derivative-storing forward + multiply backward) vs fp32 autograd."""
+    from apex.ops import blocks
+
+    torch.manual_seed(0)
+    x = (torch.randn(512, 256, device=DEV) * 0.5).bfloat16().requires_grad_(True)
+    w1 = (torch.randn(1024, 256, device=DEV) / 16).bfloat16().requires_grad_(True)
+    b1 = (torch.randn(1024, device=DEV) * 0.1).bfloat16().requires_grad_(True)
+    w2 = (torch.randn(256, 1024, device=DEV) / 32).bfloat16().requires_grad_(True)
+    for act in (0, 1):
+        out = blocks.mlp(x, w1, b1, w2, act)
+        go = torch.randn_like(out)
+        grads = torch.autograd.grad(out, (x, w1, b1, w2), go)
+        xs = [t.detach().float().requires_grad_(True) for t in (x, w1, b1, w2)]
+        ref = F.linear(F.gelu(F.linear(xs[0], xs[1], xs[2]), approximate="tanh" if act else "none"), xs[3])
+        rgrads = torch.autograd.grad(ref, xs, go.float())
+        _close(out, ref.detach(), 2e-2)
+        for g_, r_ in zip(grads, rgrads):
+            _close(g_, r_, 3e-2)
+
+
 @pytest.mark.parametrize("M,N,K", [(1000, 1600, 1600), (4096, 1024, 4096)])
 def test_gemm_resid(M, N, K):
     C = _C()

@@ -14,8 +14,9 @@ def main():
     import apex._ext as e
 
     C = e.require()
-    for (M, N, K, epi) in ((32768, 4096, 1024, 0), (32768, 4096, 1024, 2), (32768, 4096, 1024, 3),
-                          (32768, 1024, 4096, 0), (32768, 1024, 3072, 4), (32768, 1024, 1024, 0)):
+    for (M, N, K, epi) in ((32768, 4096, 1024, 0), (32768, 4096, 1024, 2), (32768, 4096, 1024, 8),
+                          (32768, 4096, 1024, 3), (32768, 4096, 1024, 10), (32768, 1024, 4096, 0),
+                          (32768, 1024, 3072, 4), (32768, 1024, 1024, 0)):
         x = torch.empty(M, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)
         w = torch.empty(N, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)
         b = torch.randn(N, device="cuda", dtype=torch.bfloat16)
@@ -24,10 +25,10 @@ def main():
         def run():
             if epi == 0:
                 C.gemm(x, w, 0)
-            elif epi in (1, 2):
+            elif epi in (1, 2, 8, 9):
                 C.gemm(x, w, epi, b)
             else:
-                C.gemm(x, w, epi, None, aux, torch.bfloat16 if epi == 3 else None)
+                C.gemm(x, w, epi, None, aux, torch.bfloat16 if epi in (3, 10) else None)
         res = {"M": M, "N": N, "K": K, "epi": epi}
         for dbg in (0, 2):
             C.gemm_set_dbg(dbg)

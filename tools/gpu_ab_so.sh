@@ -8,7 +8,7 @@ mkdir -p $O
 export PYTHONUNBUFFERED=1
 for rep in 1 2; do
   for v in A B; do
-    if [ $v = B ]; then X="APEX_EXT_SO=$SO_B"; else X="APEX_AB=A"; fi
+    if [ $v = B ]; then X="${B_ENV:-APEX_EXT_SO=$SO_B}"; else X="APEX_AB=A"; fi
     env $X timeout -k 10 400 python bench.py --steps 20 --warmup 5 > $O/bert_${v}$rep.json 2> $O/bert_${v}$rep.err || { tail -5 $O/bert_${v}$rep.err; exit 3; }
     echo "$v bert $(python -c "import json;d=json.load(open('$O/bert_${v}$rep.json'));print(d['value'], d['ms_per_step'])")"
     for B in $BENCHES; do
