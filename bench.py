@@ -28,7 +28,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("APEX_BENCH_BATCH", 256)),
+    # per-GPU batch 768 (weak scaling): measured on MI355X (profiles/r1_bench_batch_sweep.json)
+    # b256 3455, b384 3590, b512 3655-3665, b768 3729, b1024 3755 seq/s — larger GEMMs amortise
+    # the epilogues and the fixed LAMB cost; 288 GB of HBM holds b768's activations easily
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("APEX_BENCH_BATCH", 768)),
                     help="per-GPU sequences per step")
     ap.add_argument("--seq", type=int, default=128)
     ap.add_argument("--fp32", action="store_true", help="fp32 (amp O0) reference run")
