@@ -17,7 +17,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--batch", type=int, default=8, help="per-GPU sequences")
+    # per-GPU batch 16: measured 66.5k (b8) / 70.5k (b16) / 71.3k (b32) tokens/s on one MI355X
+    # (profiles/r1_gpt2_batch_sweep.json); b16 keeps the step near 0.23 s
+    ap.add_argument("--batch", type=int, default=16, help="per-GPU sequences")
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
