@@ -29,6 +29,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 template <typename T> struct MfmaT;
 template <> struct MfmaT<bf16> {
@@ -41,6 +42,19 @@ template <> struct MfmaT<f16> {
   using V8 = f16x8;
   __device__ static __forceinline__ f32x16 mma(V8 a, V8 b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+  }
+};
+
+// 16x16x32 products (the backward's dQ tiles): lane l holds C[4 (l >> 4) + i][l & 15]
+template <typename T> struct Mfma16T;
+template <> struct Mfma16T<bf16> {
+  __device__ static __forceinline__ f32x4 mma(bf16x8 a, bf16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct Mfma16T<f16> {
+  __device__ static __forceinline__ f32x4 mma(f16x8 a, f16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
   }
 };
 
@@ -368,12 +382,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 6
   using V8 = typename M::V8;
   constexpr int LDR = D + 8;
   constexpr int LDS_S = kBwdBK + 8;  // dS row stride (elements)
+  constexpr int KT_LD = kBwdBK + 8;  // K^T row stride (elements); K^T shares lds_k (D*KT_LD <= kBwdBK*LDR)
+  static_assert(D * KT_LD <= kBwdBK * LDR, "K^T must fit the lds_k staging buffer");
   __shared__ __attribute__((aligned(16))) T lds_q[kBwdBQ * LDR];
   __shared__ __attribute__((aligned(16))) T lds_do[kBwdBQ * LDR];
   __shared__ __attribute__((aligned(16))) T lds_k[kBwdBK * LDR];
   __shared__ __attribute__((aligned(16))) T lds_ds[kBwdBQ * LDS_S];
   __shared__ float lds_lse[kBwdBQ], lds_delta[kBwdBQ];
-  __shared__ float lds_dqred[(D == 64) ? 2048 : 1];
   __shared__ uint32_t lds_mask[4 * kBwdBQ];  // [wave's 32-key block][q]: bit k <-> key 32 wid + k
 
   // wid through readfirstlane: wave-uniform in SGPRs, so tile-level conditions become scalar branches
@@ -468,14 +483,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 6
       vf[s] = V8{};
     }
   }
-  // whole K block to LDS (needed as the B operand of dQ = dS.K via tr reads)
+  // whole K block to LDS transposed, K^T [D][kBwdBK + 8] (the A operand of dQ^T = K^T . dS^T,
+  // read as 16-byte rows); written once per workgroup
   if (DQ)
   for (int idx = threadIdx.x; idx < kBwdBK * (D / 8); idx += 256) {
     const int row = idx / (D / 8), col = (idx % (D / 8)) * 8;
     const int key = k0 + row;
     uint4 v = make_uint4(0, 0, 0, 0);
     if (key < Sk) v = *(const uint4*)(kp + (int64_t)key * a.k_ss + col);
-    *(uint4*)(lds_k + row * LDR + col) = v;
+    const T* e = (const T*)&v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) lds_k[(col + j) * KT_LD + row] = e[j];
   }
   };
   // D = 64: the K/V loads are issued after the first query-block fetch, so both latencies
@@ -485,7 +503,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 6
   if (DEPTH2 && qstart + kBwdBQ < nq) fetch(pfb, qstart + kBwdBQ);
   if (D == 64) load_kv();
 
-  float dq_colsum = 0.f;  // DSUM: this lane's dq column (32cb + r) summed over its query rows
+  float dqcs[D / 32][4] = {};  // DSUM: this lane's dq dims (see the dQ section) summed over queries
   auto body = [&](Pf& P, const int qb) {
     uint4 (&pf_q)[NLD] = P.q;
     uint4 (&pf_do)[NLD] = P.d;
@@ -580,58 +598,42 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 6
       lds_ds[qi * LDS_S + 32 * wid + r] = (T)ds[i];
     }
     lds_barrier();
-    // dQ [32 q x D]: waves split the D/32 column blocks and the 128-key contraction:
-    // wave w: column block (w % (D/32)), key range half/quarter when D/32 < 4
+    // dQ^T [D x 32 q] = K^T . dS^T on 16x16x32 MFMAs over the full 128-key contraction: wave
+    // w owns query tile qt = w & 1 (16 queries) and D/32 dim tiles of 16 from (w >> 1) D/32;
+    // A = K^T rows, B = dS rows (16-byte LDS reads); each lane ends with 4 consecutive dims of
+    // one query (8-byte stores). No cross-wave reduction, no scattered 2-byte stores.
     {
-      constexpr int NCB = D / 32;            // column blocks
-      constexpr int KSPLIT = 4 / NCB;        // waves per column block
-      const int cb = wid % NCB;
-      const int ks = wid / NCB;
-      constexpr int KPER = kBwdBK / KSPLIT;  // keys per wave
-      f32x16 dq = f32x16{};
+      constexpr int NT = D / 32;
+      const int qt = wid & 1, dt0 = (wid >> 1) * NT;
+      const int lq = lane & 15, lg = lane >> 4;
+      f32x4 acc[NT];
 #pragma unroll
-      for (int s = 0; s < KPER / 16; ++s) {
-        const int kk = ks * KPER + 16 * s;
-        // A = dS[q=r][keys kk + 8hl .. +7] (row read)
-        const V8 aa = *(const V8*)(lds_ds + r * LDS_S + kk + 8 * hl);
-        // B = K[key][dim]: element j -> key kk + 8hl + j, column dim = 32cb + r  (tr reads,
-        // natural k order: rows kk+8hl+0..3 and +4..7)
-        const int krow = kk + 8 * hl + ((lane & 15) >> 2);
-        const int c0 = 32 * cb + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-        const V8 bb = join4<V8>(lds_tr16(lds_k + krow * LDR + c0), lds_tr16(lds_k + (krow + 4) * LDR + c0));
-        dq = M::mma(aa, bb, dq);
-      }
-      // combine the KSPLIT partial tiles of a column block through LDS (no atomics)
-      if (KSPLIT > 1) {
-        if (ks > 0) {
+      for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int i = 0; i < 16; ++i) lds_dqred[((ks - 1) * NCB + cb) * 1024 + i * 64 + lane] = dq[i];
-        }
-        lds_barrier();
-        if (ks == 0) {
+      for (int kk = 0; kk < kBwdBK; kk += 32) {
+        const V8 bb = *(const V8*)(lds_ds + (16 * qt + lq) * LDS_S + kk + 8 * lg);
 #pragma unroll
-          for (int k2 = 1; k2 < KSPLIT; ++k2)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) dq[i] += lds_dqred[((k2 - 1) * NCB + cb) * 1024 + i * 64 + lane];
+        for (int t = 0; t < NT; ++t) {
+          const V8 aa = *(const V8*)(lds_k + ((dt0 + t) * 16 + lq) * KT_LD + kk + 8 * lg);
+          acc[t] = Mfma16T<T>::mma(aa, bb, acc[t]);
         }
       }
-      // dq element i: row q = (i&3)+8(i>>2)+4hl, col dim = 32cb + r; this workgroup is the sole
-      // writer of these query rows (DQ only with a single key block): final dtype, strided
-      if (ks == 0) {
-        T* dqp = (T*)a.dq + b * a.dq_bs + h * a.dq_hs + 32 * cb + r;
-        auto store = [&](auto guarded) {
+      // this workgroup is the sole writer of these query rows (single key block): final dtype
+      const int q = qb + 16 * qt + lq;
+      if (q < nq) {
+        T* dqp = (T*)a.dq + b * a.dq_bs + h * a.dq_hs + (int64_t)q * a.dq_ss;
 #pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int q = qb + (i & 3) + 8 * (i >> 2) + 4 * hl;
-            if (!decltype(guarded)::value || q < nq) {
-              const T v = (T)(dq[i] * a.scale);
-              dqp[(int64_t)q * a.dq_ss] = v;
-              if constexpr (DSUM) dq_colsum += (float)v;
-            }
+        for (int t = 0; t < NT; ++t) {
+          typedef T t4 __attribute__((ext_vector_type(4)));
+          t4 w;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) w[i] = (T)(acc[t][i] * a.scale);
+          *(t4*)(dqp + (dt0 + t) * 16 + 4 * lg) = w;
+          if constexpr (DSUM) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) dqcs[t][i] += (float)w[i];
           }
-        };
-        if (qb + kBwdBQ <= nq) store(std::false_type{});  // uniform: no per-element guards
-        else store(std::true_type{});
+        }
       }
     }
     }  // DQ
@@ -649,9 +651,22 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 6
   T* dvp = (T*)dv_out + b * a.dv_bs + h * a.dv_hs;
   // optional bias-gradient partials: column sums of the stored dq / dk / dv over positions
   float* dsum = DSUM ? a.dsum + ((int64_t)b * 3 * a.H + h) * D : nullptr;
-  if (DSUM && DQ && wid < (D / 32)) {  // the ks == 0 waves own dq column block cb == wid
-    const float t = dq_colsum + __shfl_xor(dq_colsum, 32, 64);
-    if (hl == 0) atomicAdd(dsum + 32 * wid + r, t);
+  if (DSUM && DQ) {  // reduce over the 16 query lanes; both query-tile waves add their partials
+    const int lq = lane & 15, lg = lane >> 4, dt0 = (wid >> 1) * (D / 32);
+#pragma unroll
+    for (int t = 0; t < D / 32; ++t) {
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v[i] = dqcs[t][i];
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) v[i] += __shfl_xor(v[i], o, 64);  // all 16 lanes hold the sum
+      }
+      // lane lq < 4 of each group adds dim 4 lg + lq: one atomic instruction (16 lanes) per tile
+      // (atomics cost per instruction, so 4 single-lane instructions would cost 4x)
+      const float x = lq == 0 ? v[0] : lq == 1 ? v[1] : lq == 2 ? v[2] : v[3];
+      if (lq < 4) atomicAdd(dsum + (dt0 + t) * 16 + 4 * lg + lq, x);
+    }
   }
   // dK then dV staged through LDS ([key][D] rows in lds_k) so the global stores are 16-byte
   // row chunks (4 per thread at D = 64) instead of 2-byte column scatters (32 per lane)
