@@ -127,13 +127,20 @@ constexpr int kFwdWaves = 4;
 constexpr int kFwdBQ = 32 * kFwdWaves;  // 128 query rows per workgroup
 constexpr int kFwdKB = 64;              // keys per tile
 
-template <typename T, int D, bool CAUSAL, bool DROPOUT>
-__global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
+// SHORT (D = 64, Sk <= 128, no dropout: BERT-shape inference): the whole key range is staged into LDS once (36 KB)
+// and no register copy of K/V is live during the math, which brings the kernel to 128 VGPRs:
+// 4 workgroups (16 waves, 144 KB of LDS) per CU instead of 2 for a kernel that is one
+// load -> math -> store pass per workgroup, so the other workgroups' loads hide the HBM latency.
+template <typename T, int D, bool CAUSAL, bool DROPOUT, bool SHORT>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SHORT ? 4 : 2)))
+attn_fwd_kernel(AttnArgs a) {
+  static_assert(!SHORT || D == 64, "SHORT is the D = 64 single-pass variant");
   using M = MfmaT<T>;
   using V8 = typename M::V8;
   constexpr int LDR = D + 8;  // padded LDS row (elements)
-  __shared__ __attribute__((aligned(16))) T lds_k[kFwdKB * LDR];
-  __shared__ __attribute__((aligned(16))) T lds_v[kFwdKB * LDR];
+  constexpr int NBUF = SHORT ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) T lds_k[NBUF * kFwdKB * LDR];
+  __shared__ __attribute__((aligned(16))) T lds_v[NBUF * kFwdKB * LDR];
 
   // wid through readfirstlane: wave-uniform in SGPRs, so tile-level conditions become scalar branches
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -199,13 +206,13 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
       }
     }
   };
-  auto lstore = [&](KV& R) {
+  auto lstore = [&](KV& R, const int rowoff) {
     uint4 (&kreg)[CH] = R.k;
     uint4 (&vreg)[CH] = R.v;
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
       const int idx = threadIdx.x + 256 * c;
-      const int row = idx / CPR, col = (idx % CPR) * 8;
+      const int row = rowoff + idx / CPR, col = (idx % CPR) * 8;
       *(uint4*)(lds_k + row * LDR + col) = kreg[c];
       *(uint4*)(lds_v + row * LDR + col) = vreg[c];
     }
@@ -213,10 +220,9 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
 
   if (ntiles > 0) gload(kva, 0);
   if (KV2 && ntiles > 1) gload(kvb, 1);
-  auto tile = [&](KV& R, const int kt) {
-    lds_barrier();  // previous tile fully consumed
-    lstore(R);
-    lds_barrier();
+  // math of key tile kt, read from LDS rows lr0 ..
+  auto compute = [&](const int kt) {
+    const int lr0 = SHORT ? kt * kFwdKB : 0;
     uint32_t mcur[2] = {0u, 0u};
     if (DROPOUT) {
 #pragma unroll
@@ -228,7 +234,6 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
         mcur[sb] = hb >> (4 * hl);
       }
     }
-    if (kt + AHEAD < ntiles) gload(R, kt + AHEAD);
     const int kb = kt * kFwdKB;
 
     // ---- S^T for two 32-key sub-blocks
@@ -239,7 +244,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
     for (int sb = 0; sb < 2; ++sb)
 #pragma unroll
-      for (int s = 0; s < D / 16; ++s) kf[sb][s] = *(const V8*)(lds_k + (32 * sb + r) * LDR + 16 * s + 8 * hl);
+      for (int s = 0; s < D / 16; ++s) kf[sb][s] = *(const V8*)(lds_k + (lr0 + 32 * sb + r) * LDR + 16 * s + 8 * hl);
     __builtin_amdgcn_sched_group_barrier(0x100, 2 * (D / 16), 0);  // DS reads first
     __builtin_amdgcn_sched_group_barrier(0x008, 2 * (D / 16), 0);  // then the MFMAs
 #pragma unroll
@@ -259,7 +264,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
         for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
           for (int db = 0; db < D / 32; ++db) {
-            const int k0 = 32 * sb + 16 * s2 + 4 * hl + ((lane & 15) >> 2);
+            const int k0 = lr0 + 32 * sb + 16 * s2 + 4 * hl + ((lane & 15) >> 2);
             const int c0 = 32 * db + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
             vt[sb][s2][db] = join4<V8>(lds_tr16(lds_v + k0 * LDR + c0), lds_tr16(lds_v + (k0 + 8) * LDR + c0));
           }
@@ -320,7 +325,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) pv[j] = st[sb][8 * s2 + j];
         const V8 pf = pack8<T, V8>(pv);
-        const int k0 = 32 * sb + 16 * s2 + 4 * hl + ((lane & 15) >> 2);
+        const int k0 = lr0 + 32 * sb + 16 * s2 + 4 * hl + ((lane & 15) >> 2);
 #pragma unroll
         for (int db = 0; db < D / 32; ++db) {
           if constexpr (HOIST_V) {
@@ -335,7 +340,21 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
       }
     }
   };
-  if constexpr (KV2) {
+  auto tile = [&](KV& R, const int kt) {
+    lds_barrier();  // previous tile fully consumed
+    lstore(R, 0);
+    lds_barrier();
+    if (kt + AHEAD < ntiles) gload(R, kt + AHEAD);
+    compute(kt);
+  };
+  if constexpr (SHORT) {
+    // both (<= 2) tiles were loaded above: one LDS stage, then the math with no K/V registers live
+    if (ntiles > 0) lstore(kva, 0);
+    if (ntiles > 1) lstore(kvb, kFwdKB);
+    lds_barrier();
+    if (ntiles > 0) compute(0);
+    if (ntiles > 1) compute(1);
+  } else if constexpr (KV2) {
     for (int kt = 0; kt < ntiles; kt += 2) {
       tile(kva, kt);
       if (kt + 1 < ntiles) tile(kvb, kt + 1);
@@ -951,8 +970,16 @@ int attn_fwd(const AttnArgs& a, int dt, hipStream_t s) {
   dim3 grid((a.Sq + kFwdBQ - 1) / kFwdBQ, a.B * a.H);
   const bool drop = a.drop_thresh > 0;
   if (drop && !a.dmask) return -3;
-  ATTN_DISPATCH(dt, T, ATTN_DISPATCH_D(a.D, D, ATTN_DISPATCH_B(a.causal, C, ATTN_DISPATCH_B(drop, DR,
-      hipLaunchKernelGGL((attn_fwd_kernel<T, D, C, DR>), grid, dim3(256), 0, s, a)))));
+  // SHORT: single LDS stage (k_lens <= Sk). Without dropout only: measured at the BERT shape
+  // (tools/attn_bench.py, b256 s128 h16) p = 0 fwd 61.1 -> 56.1 us, but p = 0.1 72.7 -> 73.8 us:
+  // with dropout the kernel is bound by the Philox integer multiplies, not by load latency.
+  if (a.D == 64 && a.Sk <= 2 * kFwdKB && !drop) {
+    ATTN_DISPATCH(dt, T, ATTN_DISPATCH_B(a.causal, C,
+        hipLaunchKernelGGL((attn_fwd_kernel<T, 64, C, false, true>), grid, dim3(256), 0, s, a)));
+  } else {
+    ATTN_DISPATCH(dt, T, ATTN_DISPATCH_D(a.D, D, ATTN_DISPATCH_B(a.causal, C, ATTN_DISPATCH_B(drop, DR,
+        hipLaunchKernelGGL((attn_fwd_kernel<T, D, C, DR, false>), grid, dim3(256), 0, s, a)))));
+  }
   return (int)hipGetLastError();
 }
 
