@@ -8,12 +8,14 @@ import torch
 from ... import _ext
 
 
-def _seed_pair(p):
+def _seed_pair(p, device=None):
     if p <= 0.0:
         return 0, 0
-    # drawn from torch's CPU generator: reproducible under torch.manual_seed, no device sync
-    s = torch.randint(0, 2 ** 62, (2,), dtype=torch.int64)
-    return int(s[0]), int(s[1])
+    # from the device generator (apex.utils.rng): reproducible under torch.manual_seed, per-TP-rank
+    # inside the RNG tracker's fork, replayed by activation checkpointing; no device sync
+    from ...utils.rng import philox_seed_offset
+
+    return philox_seed_offset(device)
 
 
 class FlashAttnFunc(torch.autograd.Function):
@@ -22,7 +24,7 @@ class FlashAttnFunc(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, dropout_p, causal, scale, k_lens):
         C = _ext.require()
-        seed, offset = _seed_pair(dropout_p)
+        seed, offset = _seed_pair(dropout_p, q.device)
         o, lse, dmask = C.flash_attn_fwd(q, k, v, bool(causal), float(scale), float(dropout_p), seed, offset,
                                   k_lens)
         ctx.save_for_backward(q, k, v, o, lse, k_lens, dmask)
@@ -51,7 +53,7 @@ class FlashAttnPackedFunc(torch.autograd.Function):
     def forward(ctx, qkv, dropout_p, causal, scale, k_lens):
         C = _ext.require()
         q, k, v = qkv.unbind(2)
-        seed, offset = _seed_pair(dropout_p)
+        seed, offset = _seed_pair(dropout_p, q.device)
         o, lse, dmask = C.flash_attn_fwd(q, k, v, bool(causal), float(scale), float(dropout_p), seed, offset,
                                   k_lens)
         ctx.save_for_backward(qkv, o, lse, k_lens, dmask)

@@ -11,6 +11,7 @@ vocab_parallel_cross_entropy on sharded logits.
 """
 from __future__ import annotations
 
+import contextlib
 import math
 from dataclasses import dataclass
 
@@ -54,6 +55,13 @@ def _init(std):
     return lambda w: nn.init.normal_(w, 0.0, std)
 
 
+def _tp_rng():
+    """Dropout on tensor-parallel shards (attention probabilities) draws from the tracked
+    'model-parallel-rng' state: a different mask on every TP rank, the same on DP replicas."""
+    tr = tp.get_cuda_rng_tracker()
+    return tr.fork() if "model-parallel-rng" in tr.get_states() else contextlib.nullcontext()
+
+
 class ParallelTransformerLayer(nn.Module):
     def __init__(self, c: MegatronGPTConfig, layer_number):
         super().__init__()
@@ -82,7 +90,8 @@ class ParallelTransformerLayer(nn.Module):
         pa = self.p_attn if self.training else 0.0
         qkv, _ = self.query_key_value(self.input_layernorm(x))
         qkv = qkv.view(B, S, 3, self.heads_local, self.d)
-        ctx = fops.attention_qkv_packed(qkv, None, pa, causal=True)
+        with _tp_rng():
+            ctx = fops.attention_qkv_packed(qkv, None, pa, causal=True)
         out, bias = self.dense(ctx.reshape(B, S, -1))
         x = fops.bias_dropout_add(out, bias, x, ph)
         xn = self.post_attention_layernorm(x)

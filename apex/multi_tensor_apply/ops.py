@@ -91,7 +91,7 @@ def multi_tensor_sgd(chunk_size, noop, tensor_lists, wd, momentum, dampening, lr
         st = scale if isinstance(scale, torch.Tensor) else None
         get_plan(lists, chunk_size).sgd(float(lr), float(momentum), float(dampening), float(wd),
                                         bool(nesterov), bool(first_run), bool(wd_after_momentum),
-                                        1.0 if st is not None else float(scale), st, noop)
+                                        1.0 if st is not None else float(scale), st, noop, None)
         return
     if noop is not None and int(noop.item()) != 0:
         return
@@ -132,7 +132,8 @@ def multi_tensor_adam(chunk_size, noop, tensor_lists, lr, beta1, beta2, eps, ste
         st = grad_scale if isinstance(grad_scale, torch.Tensor) else None
         get_plan(lists, chunk_size).adam(float(lr), float(beta1), float(beta2), float(eps),
                                          float(weight_decay), bc1, bc2, int(mode) == ADAM_MODE_ADAMW,
-                                         1.0 if st is not None else float(grad_scale), st, noop)
+                                         1.0 if st is not None else float(grad_scale), st, noop, None,
+                                         bool(bias_correction))
         return
     if noop is not None and int(noop.item()) != 0:
         return
@@ -195,8 +196,7 @@ def multi_tensor_lamb(chunk_size, noop, tensor_lists, lr, beta1, beta2, eps, ste
     if not gs:
         return
     if _ext.use_native(gs[0]):
-        us = [torch.empty_like(p, dtype=torch.float32) for p in ps]
-        lists = [gs, ps, ms, vs, us] + ([tensor_lists[4]] if len(tensor_lists) > 4 else [])
+        lists = [gs, ps, ms, vs] + ([tensor_lists[4]] if len(tensor_lists) > 4 else [])
         stp = torch.full((1,), int(step) - 1, dtype=torch.int32, device=gs[0].device)
         gn = global_grad_norm if isinstance(global_grad_norm, torch.Tensor) else \
             torch.full((1,), float(global_grad_norm), device=gs[0].device)

@@ -45,11 +45,11 @@ class _AttnSublayer(torch.autograd.Function):
         x2 = _2d(x)
         qkv = G.linear(x2, wqkv, bqkv)
         q, k, v = qkv.view(B, S, 3, heads, d).unbind(2)
-        sa, oa = _seed() if p_attn > 0 else (0, 0)
+        sa, oa = _seed(x.device) if p_attn > 0 else (0, 0)
         o, lse, dmask = C.flash_attn_fwd(q, k, v, bool(causal), scale, float(p_attn), sa, oa, k_lens)
         o2 = o.view(B * S, E)
         t = G.linear(o2, wo)
-        sh, oh = _seed() if p_hidden > 0 else (0, 0)
+        sh, oh = _seed(x.device) if p_hidden > 0 else (0, 0)
         y, s, mean, rstd = C.bdaln_fwd(t, bo, x2.contiguous(), gamma, beta, float(eps), float(p_hidden), sh, oh)
         ctx.save_for_backward(x2, wqkv, qkv, o, lse, k_lens, dmask, wo, s, gamma, mean, rstd)
         ctx.cfg = (B, S, E, heads, d, scale, causal, p_attn, sa, oa, p_hidden, sh, oh, bqkv is not None,
@@ -94,7 +94,7 @@ class _FFNSublayer(torch.autograd.Function):
             g = C.bias_act_fwd(h, b1, act)
             hb = b1
         t = G.linear(g, w2)
-        seed, off = _seed() if p > 0 else (0, 0)
+        seed, off = _seed(x.device) if p > 0 else (0, 0)
         y, s, mean, rstd = C.bdaln_fwd(t, b2, x2.contiguous(), gamma, beta, float(eps), float(p), seed, off)
         ctx.save_for_backward(x2, w1, hb, h, g, w2, s, gamma, mean, rstd)
         ctx.cfg = (p, seed, off, act, b2 is not None, b1.dtype if b1 is not None else None)

@@ -14,8 +14,9 @@ the PyTorch reference formulation on CPU (also the numerics reference for the te
 
 Forward and input-gradient GEMMs run on the hand-written MFMA kernel (apex.ops.gemm, with
 bias / bias+GELU in its epilogue where it applies); weight gradients are hipBLASLt with split-K.
-Dropout masks are regenerated from a Philox seed drawn from torch's CPU generator, so
-results are reproducible under ``torch.manual_seed`` and no mask tensor is stored.
+Dropout masks are regenerated from a Philox key derived from the device's torch generator
+(apex.utils.rng), so results are reproducible under ``torch.manual_seed``, differ across
+tensor-parallel ranks inside ``get_cuda_rng_tracker().fork()``, and no mask tensor is stored.
 """
 from __future__ import annotations
 
@@ -29,9 +30,13 @@ from .. import _ext
 ACT_GELU, ACT_GELU_TANH, ACT_RELU, ACT_NONE = 0, 1, 2, 3
 
 
-def _seed():
-    s = torch.randint(0, 2 ** 62, (2,), dtype=torch.int64)
-    return int(s[0]), int(s[1])
+def _seed(device=None):
+    """(Philox key, counter base) for one dropout launch: from the device's torch generator
+    (apex.utils.rng), so masks follow torch.manual_seed, the TP RNG tracker's fork and
+    activation-checkpoint recomputation."""
+    from ..utils.rng import philox_seed_offset
+
+    return philox_seed_offset(device)
 
 
 def _native(*ts):
@@ -234,7 +239,7 @@ class _DenseBDALN(torch.autograd.Function):
         C = _ext.require()
         x2 = _2d(x)
         t = G.linear(x2, w)
-        seed, off = _seed() if p > 0 else (0, 0)
+        seed, off = _seed(x.device) if p > 0 else (0, 0)
         y, s, mean, rstd = C.bdaln_fwd(t, b, _2d(res).contiguous(), gamma, beta, float(eps), float(p),
                                        seed, off)
         ctx.save_for_backward(x2, w, s, gamma, mean, rstd)
@@ -269,7 +274,7 @@ class _BiasDropoutAdd(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, b, res, p):
         C = _ext.require()
-        seed, off = _seed() if p > 0 else (0, 0)
+        seed, off = _seed(x.device) if p > 0 else (0, 0)
         y = C.bias_dropout_add_fwd(_2d(x).contiguous(), b, _2d(res).contiguous(), float(p), seed, off)
         ctx.cfg = (p, seed, off)
         ctx.has_b = b is not None

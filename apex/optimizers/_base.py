@@ -27,6 +27,32 @@ class FusedOptimizerBase(Optimizer):
         self._amp_grad_scale = None      # fp32 [1] device tensor: 1/loss_scale
         self._amp_noop = None            # int32 [1] device tensor: skip flag
         self._plans = {}
+        # device step counters, key = (group index, ...) -> int32 [1]; advanced by the kernels
+        # only when the step is not skipped. Not part of self.state: state_dict() publishes them
+        # as param_group["step"] and load_state_dict() re-seeds them from it.
+        self._dev_steps = {}
+
+    def _device_step(self, key, group, device):
+        t = self._dev_steps.get(key)
+        if t is None or t.device != device:
+            t = self._dev_steps[key] = torch.full((1,), int(group.get("step", 0)), dtype=torch.int32,
+                                                  device=device)
+        return t
+
+    def _sync_steps_to_groups(self):
+        for gi, group in enumerate(self.param_groups):
+            vals = [int(t.item()) for k, t in self._dev_steps.items() if k[0] == gi]
+            if vals:
+                group["step"] = max(vals)
+
+    def state_dict(self):
+        self._sync_steps_to_groups()  # one host read per group; checkpointing only
+        return super().state_dict()
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        self._dev_steps = {}
+        self._plans = {}
 
     # ------------------------------------------------------------------
     def _plan(self, key, lists):

@@ -33,10 +33,6 @@ class FusedAdam(FusedOptimizerBase):
             gs, ps, models = self._group_tensors(gi, group)
             if not gs:
                 continue
-            if "step" in group:
-                group["step"] += 1
-            else:
-                group["step"] = 1
             b1, b2 = group["betas"]
             states = []
             for p in ps:
@@ -49,14 +45,19 @@ class FusedAdam(FusedOptimizerBase):
             if models is not None:
                 lists.append(models)
             if self._native(gs):
-                bc1 = 1 - b1 ** group["step"] if group["bias_correction"] else 1.0
-                bc2 = 1 - b2 ** group["step"] if group["bias_correction"] else 1.0
+                # the step count (and so the bias corrections) lives on the device and advances
+                # only when the loss scaler did not skip the step (a host counter
+                # kept counting overflow-skipped steps)
                 for key, sub in self._split_by_dtype(lists):
+                    step_t = self._device_step((gi, key), group, gs[0].device)
                     self._plan(("adam", gi, key), sub).adam(
                         float(group["lr"]), float(b1), float(b2), float(group["eps"]),
-                        float(group["weight_decay"]), bc1, bc2, self.adam_w_mode == 1,
-                        scale_f, scale_t, self._amp_noop)
+                        float(group["weight_decay"]), 1.0, 1.0, self.adam_w_mode == 1,
+                        scale_f, scale_t, self._amp_noop, step_t, bool(group["bias_correction"]))
             else:
+                if self._amp_noop is not None and int(self._amp_noop.item()) != 0:
+                    continue
+                group["step"] = group.get("step", 0) + 1
                 mt_ops.multi_tensor_adam(0, self._amp_noop, lists, group["lr"], b1, b2,
                                          group["eps"], group["step"], self.adam_w_mode,
                                          group["bias_correction"], group["weight_decay"],

@@ -8,8 +8,11 @@ reference, listed as north-star in BASELINE.json):
 
 Device pipeline per step (csrc/multi_tensor.hip): one l2norm over all grads
 (+overflow flag) -> per group: prep (device step++, bias corrections), stage1
-(moments, update, per-chunk norms), per-tensor norm reduce, stage2 (apply + bf16
-model copy). No host synchronisation.
+(moments, per-chunk norms of p and of the update u), per-tensor norm reduce, stage2
+(recompute u from the new moments, apply + bf16 model copy). No host synchronisation,
+no parameter-sized scratch buffer; the device step counters are published as
+``param_group["step"]`` by state_dict() and re-seeded from it by load_state_dict(), so a
+checkpoint loaded with ``map_location="cpu"`` resumes on the GPU.
 """
 from __future__ import annotations
 
@@ -41,12 +44,8 @@ class FusedLAMB(FusedOptimizerBase):
             st["exp_avg_sq"] = torch.zeros_like(p, dtype=torch.float32)
         return st
 
-    def _group_step(self, gi, group, device):
-        key = ("step", gi)
-        st = self.state.setdefault(key, {})
-        if "step" not in st:
-            st["step"] = torch.zeros(1, dtype=torch.int32, device=device)
-        return st["step"]
+    def _group_step(self, key, group, device):
+        return self._device_step(key, group, device)
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -82,17 +81,13 @@ class FusedLAMB(FusedOptimizerBase):
                 continue
             b1, b2 = group["betas"]
             states = [self._state_for(p) for p in ps]
-            us = self.state.setdefault(("u", gi), {})
-            ubuf = us.get("u")
-            if ubuf is None or len(ubuf) != len(ps) or any(u.shape != p.shape for u, p in zip(ubuf, ps)):
-                ubuf = us["u"] = [torch.empty_like(p, dtype=torch.float32) for p in ps]
-            lists = [gs, ps, [s["exp_avg"] for s in states], [s["exp_avg_sq"] for s in states], ubuf]
+            lists = [gs, ps, [s["exp_avg"] for s in states], [s["exp_avg_sq"] for s in states]]
             if models is not None:
                 lists.append(models)
             for key, sub in self._split_by_dtype(lists):
                 # the prep kernel advances its step counter once per launch: one counter per
                 # dtype partition keeps every partition at the group's true step
-                step_t = self._group_step((gi, key) if len(sub[0]) != len(gs) else gi, group, dev)
+                step_t = self._group_step((gi, key) if len(sub[0]) != len(gs) else (gi,), group, dev)
                 self._plan(("lamb", gi, key), sub).lamb(
                     float(group["lr"]), float(b1), float(b2), float(group["eps"]),
                     float(group["weight_decay"]), float(group["max_grad_norm"]),
@@ -114,7 +109,7 @@ class FusedLAMB(FusedOptimizerBase):
                 continue
             b1, b2 = group["betas"]
             states = [self._state_for(p) for p in ps]
-            step_t = self._group_step(gi, group, gs[0].device)
+            step_t = self._group_step((gi,), group, gs[0].device)
             step_t += 1
             mt_ops.lamb_reference(gs, ps, [s["exp_avg"] for s in states],
                                   [s["exp_avg_sq"] for s in states], group["lr"], b1, b2,

@@ -29,6 +29,7 @@ class FusedSGD(FusedOptimizerBase):
         super().__init__(params, defaults, set_grad_none)
         self.wd_after_momentum = wd_after_momentum
         self.materialize_master_grads = materialize_master_grads
+        self._first_run_flags = {}  # (group, dtype partition) -> int32[1] device flag
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -48,11 +49,19 @@ class FusedSGD(FusedOptimizerBase):
                 moms.append(st["momentum_buffer"])
             lists = [gs, ps, moms] + ([models] if models is not None else [])
             if self._native(gs):
+                # the first-run momentum init (buf = g, not (1-dampening) g) is keyed off a device
+                # flag that only a step the loss scaler did NOT skip clears (a host flag
+                # was used up by an overflow-skipped first step)
                 for key, sub in self._split_by_dtype(lists):
+                    flag = self._first_run_flags.get((gi, key))
+                    if first_run or flag is None:
+                        flag = self._first_run_flags[(gi, key)] = torch.full(
+                            (1,), int(first_run), dtype=torch.int32, device=gs[0].device)
                     self._plan(("sgd", gi, key), sub).sgd(
                         float(group["lr"]), float(group["momentum"]), float(group["dampening"]),
                         float(group["weight_decay"]), bool(group["nesterov"]), first_run,
-                        self.wd_after_momentum, scale_f, scale_t, self._amp_noop)
+                        self.wd_after_momentum, scale_f, scale_t, self._amp_noop,
+                        flag if self._amp_noop is not None else None)
             else:
                 mt_ops.multi_tensor_sgd(0, self._amp_noop, lists, group["weight_decay"],
                                         group["momentum"], group["dampening"], group["lr"],

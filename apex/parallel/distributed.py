@@ -17,10 +17,13 @@ MI355X-first redesign (same observable behaviour):
     ``delay_allreduce`` path is ONE all-reduce per dtype;
   * averaging uses RCCL's native ncclAvg (``ReduceOp.AVG``) when the backend is
     RCCL ("nccl" on ROCm), so no separate divide kernel;
-  * collectives are issued asynchronously from the backward hooks; RCCL runs them on
-    its own HIP stream, which waits on an event of the compute stream (the
-    reference's ``reduction_stream``) and the end-of-backward callback makes the
-    compute stream wait on every outstanding work handle;
+  * each full, in-order bucket is handed to a reduction stream (the reference's
+    ``reduction_stream``) that first waits on the compute stream; the collective (plus the
+    fp32 cast and copy-back under ``allreduce_always_fp32``) runs from there, so backward
+    never blocks on communication; the end-of-backward callback waits on every bucket and
+    joins the compute stream to the reduction streams (``_join_streams``);
+  * ``num_allreduce_streams`` > 1 spreads buckets round-robin over several communicators,
+    each with its own stream, so more than one RCCL collective is in flight over xGMI;
   * bucket size defaults to the reference's 1e7 elements but is tunable
     (``message_size`` / ``APEX_DDP_MESSAGE_SIZE``): on 8x MI355X each RCCL channel
     rides one of 7 xGMI links (~153 GB/s), so buckets of tens of MB keep all
@@ -31,6 +34,7 @@ from __future__ import annotations
 
 import contextlib
 import os
+import warnings
 from collections import OrderedDict
 
 import torch
@@ -164,12 +168,17 @@ class Reducer:
 # DistributedDataParallel
 # ----------------------------------------------------------------------------
 class _Bucket:
-    __slots__ = ("dtype", "flat", "start", "numel", "params", "ready", "work")
+    __slots__ = ("dtype", "flat", "start", "numel", "params", "ready", "work", "tmp", "lane", "ev_ready",
+                 "ev_done")
 
     def __init__(self, dtype, flat, start, numel, params):
         self.dtype, self.flat, self.start, self.numel, self.params = dtype, flat, start, numel, params
         self.ready = 0
         self.work = None
+        self.tmp = None       # fp32 staging copy (allreduce_always_fp32)
+        self.lane = 0         # which communicator / reduction stream carried it
+        self.ev_ready = None  # comm_timing events (reduction stream): bucket handed to comm ...
+        self.ev_done = None   # ... and reduced (after the collective's wait)
 
     @property
     def buf(self):
@@ -179,11 +188,28 @@ class _Bucket:
 class DistributedDataParallel(Module):
     """Bucketed, backward-overlapped data parallelism over RCCL.
 
-    Args mirror the reference (apex/parallel/distributed.py:96-124) plus later apex
-    options: ``message_size`` (elements per bucket, default 1e7), ``delay_allreduce``,
-    ``allreduce_always_fp32``, ``gradient_predivide_factor``, ``gradient_average``,
-    ``retain_allreduce_buffers`` (ignored: buffers are always persistent here),
-    ``first_bucket_size``, ``process_group``.
+    Args mirror the reference (apex/parallel/distributed.py:96-124) plus later apex options:
+
+    * ``message_size``: elements per bucket (default 1e7; env ``APEX_DDP_MESSAGE_SIZE``).
+    * ``first_bucket_size``: smaller first bucket so communication starts sooner.
+    * ``delay_allreduce``: one all-reduce per dtype at the end of backward.
+    * ``allreduce_trigger_params``: params whose gradients, once all have arrived, trigger the
+      all-reduce of every bucket (manual control of when communication starts).
+    * ``allreduce_always_fp32``: reduce a bucket through an fp32 copy (cast, collective and
+      copy-back all on the reduction stream, so backward is never blocked).
+    * ``num_allreduce_streams`` / ``allreduce_communicators``: buckets round-robin over k
+      communicators, each with its own reduction stream, so several RCCL collectives are in
+      flight at once (each communicator drives its own channels over the xGMI links).
+      ``allreduce_communicators`` passes the process groups explicitly.
+    * ``gradient_average`` / ``gradient_predivide_factor``: average = divide by predivide before
+      the sum and by world/predivide after it (RCCL's native ncclAvg when predivide == 1).
+      ``gradient_average_split_factor`` is the deprecated name of the predivide factor.
+    * ``retain_allreduce_buffers``: the reduced buckets are always kept — every grad is a view of
+      a persistent flat buffer per dtype (``allreduce_buffers``), so the flag needs no copy.
+    * ``prof``: emit a roctx range per bucket collective.
+    * ``comm_timing``: record HIP events per bucket and per backward so ``comm_stats()`` reports
+      bucket sizes, ready->reduced latency and the communication time the compute stream waited
+      for at the end of backward (exposed comm).
     """
 
     def __init__(self, module, message_size=10000000, delay_allreduce=False, shared_param=None,
@@ -191,7 +217,8 @@ class DistributedDataParallel(Module):
                  allreduce_always_fp32=False, num_allreduce_streams=1,
                  allreduce_communicators=None, gradient_average=True,
                  gradient_predivide_factor=1.0, gradient_average_split_factor=None, prof=False,
-                 first_bucket_size=None, process_group=None, broadcast_buffers=True):
+                 first_bucket_size=None, process_group=None, broadcast_buffers=True,
+                 comm_timing=False):
         super().__init__()
         if shared_param is not None:
             raise ValueError("shared_param is no longer supported as an option. It was misleadingly "
@@ -199,6 +226,10 @@ class DistributedDataParallel(Module):
                              "computation should work fine with shared parameters. If you still "
                              "wish to delay communication to the end of the backward pass, use "
                              "delay_allreduce=True|False instead.")
+        if gradient_average_split_factor is not None:
+            warnings.warn("gradient_average_split_factor is deprecated; use gradient_predivide_factor",
+                          DeprecationWarning)
+            gradient_predivide_factor = gradient_average_split_factor
         self.module = module
         self.group = process_group
         self.world_size = dist.get_world_size(process_group)
@@ -206,19 +237,36 @@ class DistributedDataParallel(Module):
         self.first_bucket_size = first_bucket_size
         self.delay_allreduce = delay_allreduce or bool(int(os.environ.get("APEX_DDP_DELAY", "0")))
         self.allreduce_always_fp32 = allreduce_always_fp32
+        self.retain_allreduce_buffers = True  # always: grads are views of the persistent buckets
         self.gradient_average = gradient_average
-        self.gradient_predivide_factor = gradient_predivide_factor
+        self.gradient_predivide_factor = float(gradient_predivide_factor)
         self.broadcast_buffers = broadcast_buffers
         self.prof = prof
+        self.comm_timing = comm_timing
         backend = dist.get_backend(process_group)
         self._rccl = backend == "nccl"
         if self._rccl:
             for p in module.parameters():
                 if not p.is_cuda:
                     raise ValueError("RCCL backend requires every parameter on the GPU")
-        self.reduction_stream = torch.cuda.Stream() if (self._rccl and torch.cuda.is_available()) else None
+        # communicators (lanes): bucket i rides lane i % k
+        if allreduce_communicators is not None:
+            self._groups = list(allreduce_communicators)
+        elif num_allreduce_streams > 1:
+            ranks = dist.get_process_group_ranks(process_group) if process_group is not None else \
+                list(range(dist.get_world_size()))
+            self._groups = [dist.new_group(ranks=ranks, backend=backend) for _ in range(num_allreduce_streams)]
+        else:
+            self._groups = [process_group]
+        self.num_allreduce_streams = len(self._groups)
+        self._cuda = self._rccl and torch.cuda.is_available()
+        self._make_streams()
         self._params = [p for p in module.parameters() if p.requires_grad]
         self._param_index = {id(p): i for i, p in enumerate(self._params)}
+        self._trigger = None
+        if allreduce_trigger_params is not None:
+            self._trigger = {self._param_index[id(p)] for p in allreduce_trigger_params}
+        self._trigger_seen = 0
         self._layout_ready = False
         self._buckets = []
         self._flat = {}            # dtype -> flat buffer
@@ -228,16 +276,22 @@ class DistributedDataParallel(Module):
         self._next_bucket = 0
         self._allreduce_enabled = True
         self._hooks = []
+        self._iter_events = []     # (end-of-backward, comm-done) event pairs, comm_timing only
         self._sync_params()
         self._create_hooks()
 
     # ------------------------------------------------------------ setup
+    def _make_streams(self):
+        # the reference's reduction_stream (distributed.py:144): one per communicator lane
+        self._streams = [torch.cuda.Stream() for _ in self._groups] if self._cuda else [None] * len(self._groups)
+        self.reduction_stream = self._streams[0]
+
     def _sync_params(self):
         if self.world_size == 1:
             return
         tensors = [p.data for p in self.module.parameters()]
         if self.broadcast_buffers:
-            tensors += [b.data for b in self.module.buffers() if b.is_floating_point() or True]
+            tensors += [b.data for b in self.module.buffers()]
         if tensors:
             flat_dist_call(tensors, dist.broadcast, (0,), self.group)
 
@@ -247,13 +301,14 @@ class DistributedDataParallel(Module):
 
     def __getstate__(self):
         attrs = dict(self.__dict__)
-        attrs.pop("reduction_stream", None)  # reference bug fix (distributed.py:168-172)
-        attrs.pop("_hooks", None)
+        for k in ("reduction_stream", "_streams", "_hooks", "_iter_events"):
+            attrs.pop(k, None)  # reference bug fix (distributed.py:168-172)
         return attrs
 
     def __setstate__(self, state):
         super().__setstate__(state)
-        self.reduction_stream = torch.cuda.Stream() if self._rccl else None
+        self._make_streams()
+        self._iter_events = []
         self._hooks = []
         self._create_hooks()
 
@@ -274,13 +329,20 @@ class DistributedDataParallel(Module):
         finally:
             self._allreduce_enabled = old
 
+    @property
+    def allreduce_buffers(self):
+        """The persistent flat gradient buffers (one per dtype), reduced in place."""
+        return list(self._flat.values())
+
     def forward(self, *inputs, **kwargs):
         self._callback_queued = False
         self._next_bucket = 0
+        self._trigger_seen = 0
         self._ready_order = []
         for b in self._buckets:
             b.ready = 0
             b.work = None
+            b.tmp = None
         return self.module(*inputs, **kwargs)
 
     # ------------------------------------------------------------ hooks
@@ -298,6 +360,14 @@ class DistributedDataParallel(Module):
                 self._ensure_view(idx, p)
             return
         self._ensure_view(idx, p)
+        if self._trigger is not None:
+            if idx in self._trigger:
+                self._trigger_seen += 1
+                if self._trigger_seen == len(self._trigger):
+                    for b in self._buckets:
+                        b.ready = len(b.params)
+                    self._launch_ready_in_order()
+            return
         bi = self._param_bucket[idx]
         b = self._buckets[bi]
         b.ready += 1
@@ -322,56 +392,138 @@ class DistributedDataParallel(Module):
             b = self._buckets[self._next_bucket]
             if b.ready != len(b.params):
                 break
-            b.work = self._reduce(b.buf, async_op=True)
+            self._start_bucket(b, self._next_bucket % len(self._groups))
             self._next_bucket += 1
 
-    def _reduce(self, buf, async_op):
-        if self.world_size == 1:
-            return None
-        if self.allreduce_always_fp32 and buf.dtype != torch.float32:
-            tmp = buf.float()
-            w = self._reduce_inner(tmp, async_op=False)
-            buf.copy_(tmp)
-            return None
-        return self._reduce_inner(buf, async_op)
+    # ------------------------------------------------------------ collectives
+    def _start_bucket(self, b, lane):
+        """Hand bucket b to communicator `lane`. On the GPU its reduction stream waits for the
+        compute stream (grads written), issues the collective (after an fp32 cast under
+        allreduce_always_fp32), waits for it — a stream-side wait: the host returns at once —
+        and copies an fp32 staging buffer back, so every step of the bucket is ordered on the
+        reduction stream and the compute stream only joins it at the end of backward. On the
+        CPU (gloo) the wait is a host wait, so it is deferred to the end of backward."""
+        b.lane = lane
+        stream = self._streams[lane]
+        if stream is None:
+            b.work, b.tmp = self._issue(b.buf, self._groups[lane], async_op=True)
+            return
+        stream.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(stream):
+            if self.comm_timing:
+                b.ev_ready = torch.cuda.Event(enable_timing=True)
+                b.ev_ready.record()
+            b.work, b.tmp = self._issue(b.buf, self._groups[lane], async_op=True)
+            self._complete(b)
+            if self.comm_timing:
+                b.ev_done = torch.cuda.Event(enable_timing=True)
+                b.ev_done.record()
 
-    def _reduce_inner(self, buf, async_op):
-        with prof.range("apex.ddp.allreduce[{}]".format(buf.numel())):
+    def _complete(self, b):
+        if b.work is not None:
+            b.work.wait()
+        if b.tmp is not None:
+            b.buf.copy_(b.tmp)
+        b.work = None
+        b.tmp = None
+
+    def _finish_bucket(self, b):
+        """CPU path: wait for bucket b's collective (the GPU path completed it on its stream)."""
+        if self._streams[b.lane] is None:
+            self._complete(b)
+
+    def _issue(self, buf, group, async_op):
+        """Returns (work, fp32 staging buffer or None)."""
+        tmp = None
+        target = buf
+        if self.allreduce_always_fp32 and buf.dtype != torch.float32:
+            tmp = target = buf.float()
+        rng = prof.range("apex.ddp.allreduce[{}]".format(buf.numel())) if self.prof else contextlib.nullcontext()
+        with rng:
             if not self.gradient_average:
-                return dist.all_reduce(buf, group=self.group, async_op=async_op)
-            return _all_reduce_avg(buf, self.group, async_op=async_op,
-                                   predivide=self.gradient_predivide_factor)
+                w = dist.all_reduce(target, group=group, async_op=async_op)
+            else:
+                w = _all_reduce_avg(target, group, async_op=async_op,
+                                    predivide=self.gradient_predivide_factor)
+        return w, tmp
+
+    def _reduce_now(self, buf):
+        """Synchronous (w.r.t. the compute stream) all-reduce of a whole flat buffer."""
+        b = _Bucket(buf.dtype, buf, 0, buf.numel(), [])
+        self._start_bucket(b, 0)
+        self._finish_bucket(b)
+        self._join_streams()
+
+    def _join_streams(self):
+        if self._cuda:
+            cur = torch.cuda.current_stream()
+            for s in self._streams:
+                cur.wait_stream(s)
 
     def _end_of_backward(self):
+        ev0 = None
+        if self.comm_timing and self._cuda:
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev0.record()
         if not self._layout_ready:
             self._build_layout()
-            for dt, flat in self._flat.items():
-                self._reduce(flat, async_op=False)
+            for flat in self._flat.values():
+                self._reduce_now(flat)
             self._layout_ready = True
             return
         if self.delay_allreduce:
-            for dt, flat in self._flat.items():
+            for flat in self._flat.values():
                 # any param that produced no grad this step still has a view (zeroed)
-                self._reduce(flat, async_op=False)
-            return
-        # params that did not receive a grad this iteration: treat as ready (zero grads)
-        for b in self._buckets:
-            if b.ready != len(b.params):
-                for idx in b.params:
-                    p = self._params[idx]
-                    if p.grad is None:
-                        self._views[idx].zero_()
-                        p.grad = self._views[idx]
-                b.ready = len(b.params)
-        self._launch_ready_in_order()
-        for b in self._buckets:
-            if b.work is not None:
-                b.work.wait()
-                b.work = None
-        if self._next_bucket != len(self._buckets):
-            raise RuntimeError("In epilogue, next_bucket ({}) != num_buckets ({}). This probably "
-                               "indicates some buckets were not allreduced."
-                               .format(self._next_bucket, len(self._buckets)))
+                self._reduce_now(flat)
+        else:
+            # params that did not receive a grad this iteration: treat as ready (zero grads)
+            for b in self._buckets:
+                if b.ready != len(b.params):
+                    for idx in b.params:
+                        p = self._params[idx]
+                        if p.grad is None:
+                            self._views[idx].zero_()
+                            p.grad = self._views[idx]
+                    b.ready = len(b.params)
+            self._launch_ready_in_order()
+            for b in self._buckets:
+                self._finish_bucket(b)
+            self._join_streams()
+            if self._next_bucket != len(self._buckets):
+                raise RuntimeError("In epilogue, next_bucket ({}) != num_buckets ({}). This probably "
+                                   "indicates some buckets were not allreduced."
+                                   .format(self._next_bucket, len(self._buckets)))
+        if ev0 is not None:
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev1.record()
+            self._iter_events.append((ev0, ev1))
+            del self._iter_events[:-64]
+
+    def comm_stats(self):
+        """Bucket layout and (with comm_timing) timings of the most recent backward passes.
+        Synchronises the device: call it outside timed regions."""
+        out = {"world_size": self.world_size,
+               "backend": dist.get_backend(self.group),
+               "num_buckets": len(self._buckets),
+               "num_communicators": len(self._groups),
+               "message_size": self.message_size,
+               "bucket_bytes": [b.numel * b.flat.element_size() for b in self._buckets],
+               "allreduce_always_fp32": self.allreduce_always_fp32,
+               "delay_allreduce": self.delay_allreduce}
+        if self.comm_timing and self._cuda:
+            torch.cuda.synchronize()
+            lat = [b.ev_ready.elapsed_time(b.ev_done) for b in self._buckets
+                   if b.ev_ready is not None and b.ev_done is not None]
+            exposed = [max(0.0, a.elapsed_time(c)) for a, c in self._iter_events]
+            out["bucket_ready_to_reduced_ms"] = [round(x, 3) for x in lat]
+            if exposed:
+                out["exposed_comm_ms_mean"] = round(sum(exposed) / len(exposed), 3)
+                out["exposed_comm_ms_max"] = round(max(exposed), 3)
+                out["exposed_comm_samples"] = len(exposed)
+        return out
+
+    def reset_comm_stats(self):
+        self._iter_events = []
 
     # ------------------------------------------------------------ layout
     def _build_layout(self):
@@ -383,6 +535,9 @@ class DistributedDataParallel(Module):
             t = torch.tensor(order, dtype=torch.int64, device=dev if self._rccl else "cpu")
             dist.broadcast(t, 0, group=self.group)  # C3: rank 0's layout wins
             order = [int(x) for x in t.tolist()]
+        self._layout_from_order(order)
+
+    def _layout_from_order(self, order):
         by_dtype = OrderedDict()
         for idx in order:
             p = self._params[idx]

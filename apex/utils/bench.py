@@ -51,8 +51,22 @@ class DistEnv:
         return self.rank == 0
 
 
-def init_distributed(backend=None, device="cuda"):
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def init_distributed(backend=None, device="cuda", single_rank_group=False):
     """Read RANK/WORLD_SIZE/LOCAL_RANK (torchrun), bind the GPU, init the process group.
+
+    ``single_rank_group``: at WORLD_SIZE=1 still create a one-rank process group (RCCL on a GPU),
+    so a data-parallel wrapper runs its hooks, bucket views and collectives at N=1 exactly as
+    at N>1 (the 1-GPU line then measures the same code path as the scaling runs).
 
     Rehearsal knobs (not for measurements): ``APEX_DIST_BACKEND`` overrides the backend
     (e.g. ``gloo``), ``APEX_DIST_SHARE_GPU=1`` binds every rank to device 0, so the multi-rank
@@ -73,6 +87,12 @@ def init_distributed(backend=None, device="cuda"):
             backend = "nccl" if dev.type == "cuda" else "gloo"
         kw = {"device_id": dev} if (dev.type == "cuda" and backend == "nccl") else {}
         dist.init_process_group(backend, **kw)
+    elif world == 1 and single_rank_group and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if dev.type == "cuda" else "gloo"
+        kw = {"device_id": dev} if (dev.type == "cuda" and backend == "nccl") else {}
+        dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0,
+                                world_size=1, **kw)
     return DistEnv(rank, world, local_rank, dev)
 
 
@@ -81,8 +101,12 @@ def _sync(env):
         torch.cuda.synchronize()
 
 
-def time_steps(env: DistEnv, step, steps: int, warmup: int):
-    """Run ``step(i)`` warmup + steps times; return (max-over-ranks seconds, last result)."""
+def time_steps(env: DistEnv, step, steps: int, warmup: int, timer=None, sampler=None, on_timed_start=None):
+    """Run ``step(i)`` warmup + steps times; return (max-over-ranks seconds, last result).
+
+    ``timer`` (telemetry.StepTimer) records a HIP event between timed steps (no host sync);
+    ``sampler`` (telemetry.GpuSampler) samples clocks/power while the timed steps run;
+    ``on_timed_start`` runs after warmup, before the timed region (e.g. reset comm stats)."""
     out = None
     for i in range(warmup):
         out = step(i)
@@ -90,14 +114,24 @@ def time_steps(env: DistEnv, step, steps: int, warmup: int):
     if env.world > 1:
         dist.barrier()
     _sync(env)
+    if on_timed_start is not None:
+        on_timed_start()
+    if sampler is not None:
+        sampler.start()
     t0 = time.perf_counter()
+    if timer is not None:
+        timer.mark()
     for i in range(steps):
         out = step(i)
+        if timer is not None:
+            timer.mark()
     _sync(env)
     if env.world > 1:
         dist.barrier()
     _sync(env)
     elapsed = time.perf_counter() - t0
+    if sampler is not None:
+        sampler.stop()
     if env.world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64,
                          device=env.device if env.device.type == "cuda" else "cpu")
@@ -133,6 +167,15 @@ def emit(env: DistEnv, *, metric, items_per_step, unit, steps, warmup, elapsed, 
     return out
 
 
+def max_over_ranks(env: DistEnv, value: float) -> float:
+    if env.world > 1:
+        t = torch.tensor([value], dtype=torch.float64,
+                         device=env.device if env.device.type == "cuda" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+    return value
+
+
 def finish(env: DistEnv):
-    if env.world > 1 and dist.is_initialized():
+    if dist.is_initialized():
         dist.destroy_process_group()

@@ -6,16 +6,25 @@ BASELINE.json metric: "seq/sec BERT-Large amp-O2+FusedLAMB DDP at 1/2/4/8 MI355X
 speedup vs fp32". Synthetic data of the real pre-training shapes, random-init weights
 (no network access). Weak scaling: fixed per-GPU batch.
 
+The model is wrapped in apex DDP at every N (at N=1 over a one-rank RCCL group), so the
+gradient hooks, bucket views and bucket all-reduces are inside the timed region at 1 GPU too.
+
+After the timed bf16 loop a second, shorter pass runs the SAME step in fp32 (amp O0, same
+per-GPU batch: micro-batches of ``--fp32-microbatch`` accumulated, because fp32 activations
+of 768 sequences do not fit) and reports ``speedup_vs_fp32`` = fp32 ms/step / bf16 ms/step —
+the second half of the metric. ``--no-fp32`` skips it.
+
 Usage:
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--seq S] [--fp32]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--seq S] [--fp32-only]
   (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
 Rank 0 prints ONE JSON line on stdout.
 """
 from __future__ import annotations
 
 import argparse
+import contextlib
+import gc
 import os
-import sys
 
 import torch
 
@@ -34,62 +43,134 @@ def parse():
     ap.add_argument("--batch", type=int, default=int(os.environ.get("APEX_BENCH_BATCH", 768)),
                     help="per-GPU sequences per step")
     ap.add_argument("--seq", type=int, default=128)
-    ap.add_argument("--fp32", action="store_true", help="fp32 (amp O0) reference run")
+    ap.add_argument("--fp32-only", action="store_true", help="time only the fp32 (amp O0) step")
+    ap.add_argument("--no-fp32", action="store_true", help="skip the fp32 speedup pass")
+    ap.add_argument("--fp32-steps", type=int, default=2)
+    ap.add_argument("--fp32-microbatch", type=int, default=256)
     ap.add_argument("--layers", type=int, default=24, help="(debug only; the metric needs 24)")
-    ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--message-size", type=int, default=int(os.environ.get("APEX_DDP_MESSAGE_SIZE", 25_000_000)))
     return ap.parse_args()
+
+
+def build(env, cfg, fp32, message_size):
+    from apex import amp
+    from apex.amp._amp_state import _amp_state
+    from apex.models.bert import BertForPreTraining, param_groups_for_lamb
+    from apex.optimizers import FusedLAMB
+    from apex.parallel import DistributedDataParallel as DDP
+
+    _amp_state.optimizers, _amp_state.loss_scalers = [], []
+    torch.manual_seed(1234)
+    model = BertForPreTraining(cfg).to(env.device)
+    opt = FusedLAMB(param_groups_for_lamb(model, 0.01), lr=6e-3, betas=(0.9, 0.999), eps=1e-6,
+                    max_grad_norm=1.0)
+    if fp32:
+        model, opt = amp.initialize(model, opt, opt_level="O0", verbosity=0)
+    else:
+        model, opt = amp.initialize(model, opt, opt_level="O2", cast_model_type=torch.bfloat16,
+                                    verbosity=0)
+    model = DDP(model, message_size=message_size, comm_timing=True)
+    return model, opt
+
+
+def make_step(model, opt, batches, micro):
+    from apex import amp
+
+    def step(i):
+        b = batches[i % len(batches)]
+        n = b["input_ids"].shape[0]
+        chunks = max(1, n // micro) if micro else 1
+        loss = None
+        for c in range(chunks):
+            sub = {k: v[c * n // chunks:(c + 1) * n // chunks] for k, v in b.items()} if chunks > 1 else b
+            last = c == chunks - 1
+            ctx = model.no_sync() if not last else contextlib.nullcontext()
+            with ctx:
+                loss = model(**sub)
+                with amp.scale_loss(loss / chunks if chunks > 1 else loss, opt,
+                                    delay_unscale=not last) as scaled:
+                    scaled.backward()
+        opt.step()
+        opt.zero_grad()
+        return loss
+
+    return step
 
 
 def main():
     args = parse()
-    from apex.utils.bench import emit, finish, init_distributed, log, time_steps
-    from apex.utils.gemm_tuning import enable_tuned_gemms
+    from apex.utils import telemetry
+    from apex.utils.bench import emit, finish, init_distributed, log, max_over_ranks, time_steps
+    from apex.utils.gemm_tuning import DEFAULT_DIR, enable_tuned_gemms
 
     tuned = enable_tuned_gemms()  # committed hipBLASLt/rocBLAS selections, read-only
-    env = init_distributed()  # also reserves stdout for the result line
+    env = init_distributed(single_rank_group=True)  # also reserves stdout for the result line
     if env.world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={env.world}; using WORLD_SIZE")
     dev = env.device
 
     import apex
-    from apex import amp
-    from apex.models.bert import BertConfig, BertForPreTraining, param_groups_for_lamb, synthetic_batch
-    from apex.optimizers import FusedLAMB
-    from apex.parallel import DistributedDataParallel as DDP
+    from apex.models.bert import BertConfig, synthetic_batch
 
     apex._ext.require()
-    torch.manual_seed(1234)
     cfg = BertConfig.large()
     cfg.num_hidden_layers = args.layers
-    model = BertForPreTraining(cfg).to(dev)
-    opt = FusedLAMB(param_groups_for_lamb(model, 0.01), lr=6e-3, betas=(0.9, 0.999), eps=1e-6,
-                    max_grad_norm=1.0)
-    if args.fp32:
-        model, opt = amp.initialize(model, opt, opt_level="O0", verbosity=0)
-    else:
-        model, opt = amp.initialize(model, opt, opt_level="O2", cast_model_type=torch.bfloat16,
-                                    verbosity=0)
-    if env.world > 1:
-        model = DDP(model, message_size=int(os.environ.get("APEX_DDP_MESSAGE_SIZE", 25_000_000)))
-
-    g = torch.Generator(device=dev)
-    g.manual_seed(42 + env.rank)
-    batches = [synthetic_batch(cfg, args.batch, args.seq, device=dev, generator=g) for _ in range(4)]
-
-    def step(i):
-        b = batches[i % len(batches)]
-        loss = model(**b)
-        with amp.scale_loss(loss, opt) as scaled:
-            scaled.backward()
-        opt.step()
-        opt.zero_grad()
-        return loss
-
-    elapsed, loss = time_steps(env, step, args.steps, args.warmup)
-    final_loss = float(loss.float().item())
     world = env.world
-    emit(env, metric=METRIC, items_per_step=args.batch * world, unit="seq/s", steps=args.steps,
-         warmup=args.warmup, elapsed=elapsed, baseline=BASELINE_VALUE, dtype="fp32" if args.fp32 else "bf16",
+
+    def batches_for(n):
+        g = torch.Generator(device=dev)
+        g.manual_seed(42 + env.rank)
+        return [synthetic_batch(cfg, n, args.seq, device=dev, generator=g) for _ in range(4)]
+
+    sampler = telemetry.GpuSampler(dev.index or 0)
+    idle = sampler.snapshot()
+    extra = {}
+    if not args.fp32_only:
+        model, opt = build(env, cfg, False, args.message_size)
+        batches = batches_for(args.batch)
+        timer = telemetry.StepTimer()
+        elapsed, loss = time_steps(env, make_step(model, opt, batches, 0), args.steps, args.warmup,
+                                   timer=timer, sampler=sampler, on_timed_start=model.reset_comm_stats)
+        final_loss = float(loss.float().item())
+        ms = elapsed / args.steps * 1000.0
+        extra["final_loss"] = round(final_loss, 4)
+        extra["step_ms"] = timer.summary()
+        extra["ddp"] = model.comm_stats()
+        extra["peak_mem_gb"] = round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1)
+        del model, opt, batches, loss
+        gc.collect()
+        torch.cuda.empty_cache()
+    fp32_ms = None
+    if args.fp32_only or not args.no_fp32:
+        model, opt = build(env, cfg, True, args.message_size)
+        batches = batches_for(args.batch)
+        f_el, _ = time_steps(env, make_step(model, opt, batches, args.fp32_microbatch),
+                             max(1, args.fp32_steps), 1)
+        fp32_ms = f_el / max(1, args.fp32_steps) * 1000.0
+        del model, opt, batches
+        gc.collect()
+        torch.cuda.empty_cache()
+    if args.fp32_only:
+        elapsed, ms = f_el, fp32_ms
+        steps = max(1, args.fp32_steps)
+    else:
+        steps = args.steps
+        if fp32_ms is not None:
+            fp32_ms = max_over_ranks(env, fp32_ms)
+            extra["fp32_ms_per_step"] = round(fp32_ms, 2)
+            extra["fp32_seq_per_s"] = round(args.batch * world / fp32_ms * 1000.0, 2)
+            extra["speedup_vs_fp32"] = round(fp32_ms / ms, 3)
+            extra["fp32_config"] = f"amp O0 fp32, micro-batches of {args.fp32_microbatch} accumulated to {args.batch}"
+    extra["gpu"] = {"idle": idle, "timed": sampler.summary()}
+    tstat = telemetry.tunableop_status()
+    tstat["committed_validators_match"] = None
+    committed = telemetry.committed_validators(os.path.join(DEFAULT_DIR, "tunableop_results0.csv"))
+    if committed and tstat.get("validators"):
+        tstat["committed_validators_match"] = all(tstat["validators"].get(k) == v for k, v in committed.items())
+    extra["tunableop"] = tstat
+    extra["versions"] = telemetry.library_versions()
+    emit(env, metric=METRIC, items_per_step=args.batch * world, unit="seq/s", steps=steps,
+         warmup=args.warmup, elapsed=elapsed, baseline=BASELINE_VALUE, dtype="fp32" if args.fp32_only else "bf16",
          data="synthetic (random token ids, 15% masked positions, random NSP labels); random-init weights",
          config={
              "model": "BERT-Large (24L, H1024, A16, FFN4096, vocab 30522)" if args.layers == 24
@@ -99,13 +180,14 @@ def main():
              "seq_len": args.seq,
              "max_predictions_per_seq": max(1, int(round(args.seq * 0.15))),
              "parallelism": f"dp{world}",
-             "amp": "O0" if args.fp32 else "O2 bf16",
+             "amp": "O0" if args.fp32_only else "O2 bf16",
              "optimizer": "FusedLAMB",
              "norm": "FusedLayerNorm",
-             "ddp": "apex.parallel.DistributedDataParallel (RCCL)" if world > 1 else "none (1 GPU)",
+             "ddp": f"apex.parallel.DistributedDataParallel ({'RCCL' if dev.type == 'cuda' else 'gloo'}, "
+                    f"message_size {args.message_size})",
              "gemm_selection": "TunableOp pre-tuned (tuning/)" if tuned else "hipBLASLt default",
          },
-         extra={"final_loss": round(final_loss, 4)})
+         extra=extra)
     finish(env)
 
 

@@ -145,33 +145,44 @@ struct MTPlan {
     return {glob, per};
   }
 
+  // first_run_t: optional int32[1] device flag (nonzero until a non-skipped step ran); when given
+  // it replaces the host first_run so an overflow-skipped step does not use it up
   void sgd(double lr, double momentum, double dampening, double wd, bool nesterov, bool first_run,
            bool wd_after_momentum, double grad_scale, const c10::optional<Tensor>& grad_scale_t,
-           const c10::optional<Tensor>& noop) {
+           const c10::optional<Tensor>& noop, const c10::optional<Tensor>& first_run_t) {
+    if (first_run_t) TORCH_CHECK(first_run_t->scalar_type() == at::kInt && first_run_t->is_cuda(), "first_run flag must be int32 device");
     apex::SgdArgs a{(float)lr, (float)momentum, (float)dampening, (float)wd, nesterov, first_run,
                     wd_after_momentum, (float)grad_scale, opt_ptr<float>(grad_scale_t),
-                    opt_ptr<int>(noop)};
+                    opt_ptr<int>(noop), opt_ptr<int>(first_run_t)};
     const int c_dt = nlists > 3 ? dtypes[3] : dtypes[1];
     check(apex::mt_sgd(view(), dtypes[0], dtypes[1], c_dt, a, cur_stream()), "mt_sgd");
   }
 
+  // step_t: optional int32[1] device step counter; when given it is advanced on the device only by
+  // non-skipped steps and the bias corrections come from it (bc1/bc2 ignored)
   void adam(double lr, double b1, double b2, double eps, double wd, double bc1, double bc2,
             bool adamw, double grad_scale, const c10::optional<Tensor>& grad_scale_t,
-            const c10::optional<Tensor>& noop) {
+            const c10::optional<Tensor>& noop, const c10::optional<Tensor>& step_t, bool bias_correction) {
+    Tensor scal;
+    if (step_t) {
+      TORCH_CHECK(step_t->scalar_type() == at::kInt && step_t->is_cuda(), "step must be int32 device");
+      scal = at::empty({2}, meta.options().dtype(at::kFloat));
+    }
     apex::AdamArgs a{(float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (float)bc1, (float)bc2,
-                     adamw, (float)grad_scale, opt_ptr<float>(grad_scale_t), opt_ptr<int>(noop)};
+                     adamw, (float)grad_scale, opt_ptr<float>(grad_scale_t), opt_ptr<int>(noop),
+                     opt_ptr<int>(step_t), bias_correction, step_t ? scal.data_ptr<float>() : nullptr};
     const int c_dt = nlists > 4 ? dtypes[4] : dtypes[1];
     check(apex::mt_adam(view(), dtypes[0], dtypes[1], c_dt, a, cur_stream()), "mt_adam");
   }
 
-  // lists: g, p, m, v, u(fp32 scratch), [copy]; step: int32[1] device counter
+  // lists: g, p, m, v, [copy]; step: int32[1] device counter
   // workspace is returned so python can read the grad norm (ws[0]).
   Tensor lamb(double lr, double b1, double b2, double eps, double wd, double max_grad_norm,
               bool adamw, bool bias_correction, bool grad_averaging, bool use_nvlamb,
               double grad_scale, const c10::optional<Tensor>& grad_scale_t,
               const c10::optional<Tensor>& noop, const c10::optional<Tensor>& overflow_out,
               Tensor step, const c10::optional<Tensor>& gnorm_in) {
-    TORCH_CHECK(nlists >= 5, "lamb needs [g, p, m, v, u, (copy)]");
+    TORCH_CHECK(nlists >= 4, "lamb needs [g, p, m, v, (copy)]");
     TORCH_CHECK(step.scalar_type() == at::kInt && step.is_cuda(), "step must be int32 device");
     Tensor ws = at::empty({4 + 3 * (int64_t)std::max(nchunks, 1) + 2 * (int64_t)ntensors},
                           meta.options().dtype(at::kFloat));
@@ -179,7 +190,7 @@ struct MTPlan {
                      adamw, bias_correction, grad_averaging, use_nvlamb, (float)grad_scale,
                      opt_ptr<float>(grad_scale_t), opt_ptr<int>(noop), opt_ptr<int>(overflow_out),
                      opt_ptr<float>(gnorm_in)};
-    const int c_dt = nlists > 5 ? dtypes[5] : dtypes[1];
+    const int c_dt = nlists > 4 ? dtypes[4] : dtypes[1];
     check(apex::mt_lamb(view(), dtypes[0], dtypes[1], c_dt, a, ws.data_ptr<float>(),
                         step.data_ptr<int>(), cur_stream()),
           "mt_lamb");

@@ -20,6 +20,7 @@ struct SgdArgs {
   float grad_scale;
   const float* grad_scale_ptr;
   const int* noop;
+  int* first_run_dev;  // optional device flag: nonzero until the first NON-skipped step ran
 };
 
 struct AdamArgs {
@@ -28,6 +29,9 @@ struct AdamArgs {
   float grad_scale;
   const float* grad_scale_ptr;
   const int* noop;
+  int* step;           // optional device step counter, advanced only by non-skipped steps;
+  int bias_correction; // with `step`, bc1/bc2 are computed on the device from it
+  float* scal;         // 2-float workspace for the device bias corrections
 };
 
 struct LambArgs {

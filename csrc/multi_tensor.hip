@@ -168,6 +168,7 @@ template <typename G, typename P, typename C>
 __global__ void __launch_bounds__(kBlock) sgd_kernel(MTMeta m, SgdArgs a) {
   if (a.noop && *a.noop) return;
   const float gs = read_scale(a.grad_scale_ptr, a.grad_scale);
+  if (a.first_run_dev) a.first_run = *a.first_run_dev != 0;
   const bool has_copy = m.nlists > 3;
   for (int c = blockIdx.x; c < m.nchunks; c += gridDim.x) {
     const ChunkView cv = chunk_view(m, c);
@@ -199,6 +200,21 @@ __global__ void __launch_bounds__(kBlock) sgd_kernel(MTMeta m, SgdArgs a) {
   }
 }
 
+// After a (possibly skipped) step: a device flag/counter advances only when the step ran, so a
+// dynamic-loss-scale overflow never consumes SGD's first-run momentum init or an Adam step.
+__global__ void clear_flag_unless_noop_kernel(int* flag, const int* noop) {
+  if (!(noop && *noop)) *flag = 0;
+}
+
+// Adam step counter and bias corrections on the device (1 thread, before the update kernel)
+__global__ void adam_prep_kernel(int* step, const int* noop, float beta1, float beta2, int bias_correction,
+                                 float* scal) {
+  int st = *step;
+  if (!(noop && *noop)) *step = ++st;
+  scal[0] = bias_correction ? 1.f - powf(beta1, (float)st) : 1.f;
+  scal[1] = bias_correction ? 1.f - powf(beta2, (float)st) : 1.f;
+}
+
 // ---------------------------------------------------------------------------
 // Adam / AdamW. lists: g, p, m, v, [copy]
 // ---------------------------------------------------------------------------
@@ -208,7 +224,7 @@ __global__ void __launch_bounds__(kBlock) adam_kernel(MTMeta m, AdamArgs a) {
   const float gs = read_scale(a.grad_scale_ptr, a.grad_scale);
   const bool has_copy = m.nlists > 4;
   const float b1 = a.beta1, b2 = a.beta2;
-  const float rbc1 = 1.f / a.bc1, rbc2 = 1.f / a.bc2;
+  const float rbc1 = 1.f / (a.step ? a.scal[0] : a.bc1), rbc2 = 1.f / (a.step ? a.scal[1] : a.bc2);
   for (int c = blockIdx.x; c < m.nchunks; c += gridDim.x) {
     const ChunkView cv = chunk_view(m, c);
     const G* g = (const G*)m.ptr(0, cv.t) + cv.start;
@@ -247,9 +263,19 @@ __global__ void __launch_bounds__(kBlock) adam_kernel(MTMeta m, AdamArgs a) {
 //  prep  (1 block): global grad norm -> clip divisor, device step++, bias corrections
 //  stage1: m,v update; u = m^/(sqrt(v^)+eps) (+wd*p); partial sums of p^2 and u^2
 //  finalize per-tensor norms (norm_finalize_kernel twice)
-//  stage2: p -= lr * trust * u ; optional low-precision copy
+//  stage2: recompute u from the updated m, v and p (lamb_u, the same expression), then
+//          p -= lr * trust * u ; optional low-precision copy
+// u never reaches HBM: stage 1 writes m, v (8 B) instead of m, v, u (12 B) and stage 2 reads
+// p, m, v (12 B) instead of p, u (8 B) — the same 40 B per parameter as a stored fp32 u, minus
+// a parameter-sized fp32 scratch buffer (1.3 GB for BERT-Large) and its state-dict entry.
 // scal layout: [0] grad norm, [1] clip divisor, [2] bc1, [3] bc2
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ float lamb_u(float mv, float vv, float pv, float rbc1, float rbc2, const LambArgs& a) {
+  float u = (mv * rbc1) / (sqrtf(vv * rbc2) + a.eps);
+  if (a.adamw && a.wd != 0.f) u += a.wd * pv;
+  return u;
+}
+
 __global__ void lamb_prep_kernel(const float* partial, int nchunks, LambArgs a, float* scal,
                                  int* step) {
   __shared__ float red[kBlock / kWave];
@@ -295,7 +321,6 @@ __global__ void __launch_bounds__(kBlock) lamb_stage1_kernel(MTMeta m, LambArgs 
     const P* p = (const P*)m.ptr(1, cv.t) + cv.start;
     float* mm = (float*)m.ptr(2, cv.t) + cv.start;
     float* vv = (float*)m.ptr(3, cv.t) + cv.start;
-    float* uu = (float*)m.ptr(4, cv.t) + cv.start;
     float sp = 0.f, su = 0.f;
     chunk_for(m, cv.n, [&](auto NC, int64_t i) {
       constexpr int N = decltype(NC)::value;
@@ -310,14 +335,12 @@ __global__ void __launch_bounds__(kBlock) lamb_stage1_kernel(MTMeta m, LambArgs 
         if (!a.adamw && a.wd != 0.f) gg += a.wd * pv[k];
         mv[k] = b1 * mv[k] + b3 * gg;
         vv2[k] = b2 * vv2[k] + (1.f - b2) * gg * gg;
-        u[k] = (mv[k] * rbc1) / (sqrtf(vv2[k] * rbc2) + a.eps);
-        if (a.adamw && a.wd != 0.f) u[k] += a.wd * pv[k];
+        u[k] = lamb_u(mv[k], vv2[k], pv[k], rbc1, rbc2, a);
         sp += pv[k] * pv[k];
         su += u[k] * u[k];
       }
       store_f<float, N>(mm + i, mv);
       store_f<float, N>(vv + i, vv2);
-      store_f<float, N>(uu + i, u);
     });
     sp = block_sum(sp, red);
     su = block_sum(su, red);
@@ -329,15 +352,17 @@ __global__ void __launch_bounds__(kBlock) lamb_stage1_kernel(MTMeta m, LambArgs 
 }
 
 template <typename P, typename C>
-__global__ void __launch_bounds__(kBlock) lamb_stage2_kernel(MTMeta m, LambArgs a, const float* pnorm,
-                                                            const float* unorm) {
+__global__ void __launch_bounds__(kBlock) lamb_stage2_kernel(MTMeta m, LambArgs a, const float* scal,
+                                                            const float* pnorm, const float* unorm) {
   if (a.noop && *a.noop) return;
-  const bool has_copy = m.nlists > 5;
+  const bool has_copy = m.nlists > 4;
+  const float rbc1 = 1.f / scal[2], rbc2 = 1.f / scal[3];
   for (int c = blockIdx.x; c < m.nchunks; c += gridDim.x) {
     const ChunkView cv = chunk_view(m, c);
     P* p = (P*)m.ptr(1, cv.t) + cv.start;
-    const float* uu = (const float*)m.ptr(4, cv.t) + cv.start;
-    C* cp = has_copy ? (C*)m.ptr(5, cv.t) + cv.start : nullptr;
+    const float* mm = (const float*)m.ptr(2, cv.t) + cv.start;
+    const float* vv = (const float*)m.ptr(3, cv.t) + cv.start;
+    C* cp = has_copy ? (C*)m.ptr(4, cv.t) + cv.start : nullptr;
     float ratio = a.lr;
     if (a.use_nvlamb || a.wd != 0.f) {
       const float pn = pnorm[cv.t], un = unorm[cv.t];
@@ -345,11 +370,12 @@ __global__ void __launch_bounds__(kBlock) lamb_stage2_kernel(MTMeta m, LambArgs 
     }
     chunk_for(m, cv.n, [&](auto NC, int64_t i) {
       constexpr int N = decltype(NC)::value;
-      float pv[N], u[N];
+      float pv[N], mv[N], vv2[N];
       load_f<P, N>(p + i, pv);
-      load_f<float, N>(uu + i, u);
+      load_f<float, N>(mm + i, mv);
+      load_f<float, N>(vv + i, vv2);
 #pragma unroll
-      for (int k = 0; k < N; ++k) pv[k] -= ratio * u[k];
+      for (int k = 0; k < N; ++k) pv[k] -= ratio * lamb_u(mv[k], vv2[k], pv[k], rbc1, rbc2, a);
       store_f<P, N>(p + i, pv);
       if (cp) store_f<C, N>(cp + i, pv);
     });
@@ -430,12 +456,17 @@ int mt_sgd(const MTMeta& m, int g_dt, int p_dt, int c_dt, const SgdArgs& a, hipS
   APEX_DISPATCH1(g_dt, G, APEX_DISPATCH1(p_dt, P, APEX_DISPATCH1(c_dt, C,
       hipLaunchKernelGGL((sgd_kernel<G, P, C>), dim3(grid_for(m.nchunks)), dim3(kBlock), 0, s, m,
                          a))));
+  if (a.first_run_dev)
+    hipLaunchKernelGGL(clear_flag_unless_noop_kernel, dim3(1), dim3(1), 0, s, a.first_run_dev, a.noop);
   return (int)hipGetLastError();
 }
 
 int mt_adam(const MTMeta& m, int g_dt, int p_dt, int c_dt, const AdamArgs& a, hipStream_t s) {
   if (m.nchunks == 0) return 0;
   if (m.nlists <= 4) c_dt = p_dt;
+  if (a.step)
+    hipLaunchKernelGGL(adam_prep_kernel, dim3(1), dim3(1), 0, s, a.step, a.noop, a.beta1, a.beta2,
+                       a.bias_correction, a.scal);
   APEX_DISPATCH1(g_dt, G, APEX_DISPATCH1(p_dt, P, APEX_DISPATCH1(c_dt, C,
       hipLaunchKernelGGL((adam_kernel<G, P, C>), dim3(grid_for(m.nchunks)), dim3(kBlock), 0, s, m,
                          a))));
@@ -446,7 +477,7 @@ int mt_lamb(const MTMeta& m, int g_dt, int p_dt, int c_dt, const LambArgs& a, fl
             int* step, hipStream_t s) {
   // ws layout: [4 scal][C gpart][C ppart][C upart][T pnorm][T unorm]
   if (m.nchunks == 0) return 0;
-  if (m.nlists <= 5) c_dt = p_dt;
+  if (m.nlists <= 4) c_dt = p_dt;
   const int C = m.nchunks, T = m.ntensors;
   float* scal = ws;
   float* gpart = ws + 4;
@@ -460,7 +491,7 @@ int mt_lamb(const MTMeta& m, int g_dt, int p_dt, int c_dt, const LambArgs& a, fl
         hipLaunchKernelGGL((sumsq_kernel<G>), dim3(grid), dim3(kBlock), 0, s, m, 0, gpart,
                            a.overflow_out));
   }
-  hipLaunchKernelGGL(lamb_prep_kernel, dim3(1), dim3(1024), 0, s, gpart, C, a, scal, step);
+  hipLaunchKernelGGL(lamb_prep_kernel, dim3(1), dim3(kBlock), 0, s, gpart, C, a, scal, step);
   APEX_DISPATCH1(g_dt, G, APEX_DISPATCH1(p_dt, P,
       hipLaunchKernelGGL((lamb_stage1_kernel<G, P>), dim3(grid), dim3(kBlock), 0, s, m, a, scal,
                          ppart, upart)));
@@ -469,7 +500,7 @@ int mt_lamb(const MTMeta& m, int g_dt, int p_dt, int c_dt, const LambArgs& a, fl
   hipLaunchKernelGGL(norm_finalize_kernel, dim3(T), dim3(kBlock), 0, s, m, upart, unorm,
                      (float*)nullptr, (const float*)nullptr, 1.f);
   APEX_DISPATCH1(p_dt, P, APEX_DISPATCH1(c_dt, C,
-      hipLaunchKernelGGL((lamb_stage2_kernel<P, C>), dim3(grid), dim3(kBlock), 0, s, m, a, pnorm,
+      hipLaunchKernelGGL((lamb_stage2_kernel<P, C>), dim3(grid), dim3(kBlock), 0, s, m, a, scal, pnorm,
                          unorm)));
   return (int)hipGetLastError();
 }

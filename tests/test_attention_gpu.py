@@ -92,7 +92,7 @@ def test_flash_dropout_matches_masked_reference(causal):
     torch.manual_seed(11)
     o = flash.flash_attention_packed(qkv, p, causal, None)
     torch.manual_seed(11)
-    seed, offset = flash._seed_pair(p)
+    seed, offset = flash._seed_pair(p, qkv.device)
     mask = C.flash_dropout_mask(B, H, S, S, p, seed, offset, qkv.device)
     keep = mask.float().mean().item()
     assert abs(keep - (1 - p)) < 0.01
