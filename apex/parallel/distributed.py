@@ -243,6 +243,7 @@ class DistributedDataParallel(Module):
         self.broadcast_buffers = broadcast_buffers
         self.prof = prof
         self.comm_timing = comm_timing
+        self.single_rank_collectives = False
         backend = dist.get_backend(process_group)
         self._rccl = backend == "nccl"
         if self._rccl:
@@ -433,7 +434,11 @@ class DistributedDataParallel(Module):
             self._complete(b)
 
     def _issue(self, buf, group, async_op):
-        """Returns (work, fp32 staging buffer or None)."""
+        """Returns (work, fp32 staging buffer or None). A one-rank group's average is the identity,
+        so nothing is launched (RCCL would still run a full copy kernel over the bucket,
+        ~0.66 ms per 50 MB bucket on MI355X) unless ``single_rank_collectives`` is set (tests)."""
+        if self.world_size == 1 and not self.single_rank_collectives:
+            return None, None
         tmp = None
         target = buf
         if self.allreduce_always_fp32 and buf.dtype != torch.float32:
