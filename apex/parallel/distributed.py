@@ -104,12 +104,21 @@ class _PostScaleWork:
             self.flat.mul_(self.post)
 
 
+def _group_root(group):
+    """Global rank of a group's rank 0 (collective src/dst arguments are global ranks)."""
+    return dist.get_global_rank(group, 0) if group is not None else 0
+
+
 def apply_flat_dist_call(bucket, call, extra_args=None, group=None):
     """Flatten a same-dtype bucket, run ``call`` on it, average after all_reduce,
-    and copy the result back (reference semantics, apex/parallel/distributed.py:11-23)."""
+    and copy the result back (reference semantics, apex/parallel/distributed.py:11-23).
+    For broadcast, ``extra_args[0]`` is the source as a rank WITHIN ``group``."""
     coalesced = _flatten(bucket)
     if call is dist.all_reduce:
         _all_reduce_avg(coalesced, group)
+    elif call is dist.broadcast and group is not None:
+        src = dist.get_global_rank(group, extra_args[0] if extra_args else 0)
+        dist.broadcast(coalesced, src, group=group)
     elif extra_args is not None:
         call(coalesced, *extra_args, group=group) if group is not None else call(coalesced, *extra_args)
     else:
@@ -335,6 +344,18 @@ class DistributedDataParallel(Module):
         """The persistent flat gradient buffers (one per dtype), reduced in place."""
         return list(self._flat.values())
 
+    def reduce_gradients(self):
+        """All-reduce every gradient now (one collective per dtype), outside any backward pass:
+        for callers that ran all their backward passes under ``no_sync()`` (e.g. a pipeline
+        schedule). Builds the bucket layout on first use."""
+        if not self._layout_ready:
+            self._build_layout()
+            self._layout_ready = True
+        for i, p in enumerate(self._params):
+            self._ensure_view(i, p)
+        for flat in self._flat.values():
+            self._reduce_now(flat)
+
     def forward(self, *inputs, **kwargs):
         self._callback_queued = False
         self._next_bucket = 0
@@ -538,7 +559,7 @@ class DistributedDataParallel(Module):
         if self.world_size > 1:
             dev = self._params[0].device
             t = torch.tensor(order, dtype=torch.int64, device=dev if self._rccl else "cpu")
-            dist.broadcast(t, 0, group=self.group)  # C3: rank 0's layout wins
+            dist.broadcast(t, _group_root(self.group), group=self.group)  # C3: rank 0's layout wins
             order = [int(x) for x in t.tolist()]
         self._layout_from_order(order)
 

@@ -57,7 +57,7 @@ def initialize_model_parallel(tensor_model_parallel_size_=1, pipeline_model_para
 
     global _VIRTUAL_PIPELINE_MODEL_PARALLEL_RANK, _VIRTUAL_PIPELINE_MODEL_PARALLEL_WORLD_SIZE
     if virtual_pipeline_model_parallel_size_ is not None:
-        assert pp > 2, "interleaved schedule needs pipeline_model_parallel_size > 2"
+        assert pp > 1, "interleaved schedule needs pipeline_model_parallel_size > 1"
         _VIRTUAL_PIPELINE_MODEL_PARALLEL_RANK = 0
         _VIRTUAL_PIPELINE_MODEL_PARALLEL_WORLD_SIZE = virtual_pipeline_model_parallel_size_
     global _PIPELINE_MODEL_PARALLEL_SPLIT_RANK

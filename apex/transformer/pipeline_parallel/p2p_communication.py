@@ -31,7 +31,6 @@ def _communicate(tensor_send_next, tensor_send_prev, recv_prev, recv_next, tenso
     dev, compute = _devices(sent)
     t_prev = torch.empty(tensor_shape, dtype=dtype, device=dev) if recv_prev else None
     t_next = torch.empty(tensor_shape, dtype=dtype, device=dev) if recv_next else None
-    ops = []
     group = ps.get_pipeline_model_parallel_group()
     # the wire format is the agreed (shape, dtype): a stage whose output is wider (amp O2 casts
     # model outputs to fp32) sends it in the agreed dtype, or the peer's receive size mismatches
@@ -39,16 +38,21 @@ def _communicate(tensor_send_next, tensor_send_prev, recv_prev, recv_next, tenso
         tensor_send_prev = tensor_send_prev.detach().to(device=dev, dtype=dtype)
     if tensor_send_next is not None:
         tensor_send_next = tensor_send_next.detach().to(device=dev, dtype=dtype)
-    if tensor_send_prev is not None:
-        ops.append(dist.P2POp(dist.isend, tensor_send_prev.contiguous(), ps.get_pipeline_model_parallel_prev_rank(),
-                              group))
-    if t_prev is not None:
-        ops.append(dist.P2POp(dist.irecv, t_prev, ps.get_pipeline_model_parallel_prev_rank(), group))
-    if tensor_send_next is not None:
-        ops.append(dist.P2POp(dist.isend, tensor_send_next.contiguous(), ps.get_pipeline_model_parallel_next_rank(),
-                              group))
-    if t_next is not None:
-        ops.append(dist.P2POp(dist.irecv, t_next, ps.get_pipeline_model_parallel_next_rank(), group))
+    prev, nxt = ps.get_pipeline_model_parallel_prev_rank(), ps.get_pipeline_model_parallel_next_rank()
+    send_prev = dist.P2POp(dist.isend, tensor_send_prev.contiguous(), prev, group) if tensor_send_prev is not None else None
+    recv_prev_op = dist.P2POp(dist.irecv, t_prev, prev, group) if t_prev is not None else None
+    send_next = dist.P2POp(dist.isend, tensor_send_next.contiguous(), nxt, group) if tensor_send_next is not None else None
+    recv_next_op = dist.P2POp(dist.irecv, t_next, nxt, group) if t_next is not None else None
+    # Messages between one pair of ranks are matched in issue order (RCCL p2p has no tags). With
+    # two stages the previous and the next rank are the SAME peer, so an activation and a gradient
+    # travel between the pair in one grouped call: even ranks issue (send next, recv prev,
+    # send prev, recv next) and odd ranks (recv prev, send next, recv next, send prev), so each
+    # direction carries the activation first and the gradient second on both ends.
+    if ps.get_pipeline_model_parallel_rank() % 2 == 0:
+        order = (send_next, recv_prev_op, send_prev, recv_next_op)
+    else:
+        order = (recv_prev_op, send_next, recv_next_op, send_prev)
+    ops = [op for op in order if op is not None]
     if ops:
         # wait() orders the compute stream after RCCL's stream (no host synchronisation)
         for r in dist.batch_isend_irecv(ops):

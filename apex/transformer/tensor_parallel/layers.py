@@ -10,6 +10,17 @@ that is one RCCL ring over the TP group's direct xGMI links per sublayer.
 With ``sequence_parallel_enabled`` the all-reduces become reduce-scatter / all-gather
 along the sequence dimension (activations stay sharded between blocks).
 GEMMs + bias use apex.ops.fused.fused_dense (bias grad via HIP colsum).
+
+Backward overlap (``LinearWithGradAccumulationAndAsyncCommunication``, Megatron semantics):
+  * async TP all-reduce (column-parallel, default on; ``no_async_tensor_model_parallel_allreduce``
+    turns it off): the input gradient dX = dY W is computed first and its all-reduce (or, under
+    sequence parallelism, its reduce-scatter) is launched asynchronously; the weight-gradient
+    GEMM dW = dY^T X runs while RCCL moves dX over xGMI, and the wait comes last;
+  * ``gradient_accumulation_fusion``: dW is accumulated straight into the parameter's fp32
+    ``main_grad`` buffer (hipBLASLt with fp32 output, no bf16 dW tensor, no separate add); the
+    weight then gets no ``.grad`` from autograd;
+  * sequence parallel: the all-gather of the sequence-sharded input is redone in backward
+    instead of keeping the gathered activation alive.
 """
 from __future__ import annotations
 
@@ -19,6 +30,8 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 from torch.nn.parameter import Parameter
+
+import torch.distributed as dist
 
 from ...ops import fused as fops
 from .. import parallel_state as ps
@@ -72,6 +85,76 @@ def _initialize_affine_weight(weight, output_size, input_size, per_partition_siz
     return master if return_master_weight else None
 
 
+def _accumulate_main_grad(weight, dy2, x2):
+    """weight.main_grad (fp32) += dy2^T x2 without materialising a low-precision dW."""
+    mg = weight.main_grad
+    if dy2.is_cuda and dy2.dtype in (torch.bfloat16, torch.float16):
+        try:
+            torch.addmm(mg, dy2.t(), x2, out_dtype=torch.float32, out=mg)
+            return
+        except (TypeError, RuntimeError):
+            pass
+    mg.add_(torch.mm(dy2.t().float(), x2.float()))
+
+
+class LinearWithGradAccumulationAndAsyncCommunication(torch.autograd.Function):
+    """y = x W^T (+ b) for a tensor-parallel shard, with the backward overlap described above."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, gradient_accumulation_fusion, async_grad_allreduce, sequence_parallel):
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        ctx.flags = (gradient_accumulation_fusion, async_grad_allreduce, sequence_parallel)
+        total = _gather_seq(x) if sequence_parallel else x
+        return fops.fused_dense(total, weight, bias)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        fusion, async_ar, sp = ctx.flags
+        total = _gather_seq(x) if sp else x
+        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        t2 = total.reshape(-1, total.shape[-1])
+        from ...ops import gemm as G
+
+        dx = G.dgrad(dy2, weight).view(*dy.shape[:-1], weight.shape[1])
+        handle, out = None, dx
+        tp_group = ps.get_tensor_model_parallel_group()
+        if ps.get_tensor_model_parallel_world_size() > 1:
+            if sp:
+                out = torch.empty((dx.shape[0] // ps.get_tensor_model_parallel_world_size(),) + tuple(dx.shape[1:]),
+                                  dtype=dx.dtype, device=dx.device)
+                handle = dist.reduce_scatter_tensor(out, dx.contiguous(), group=tp_group, async_op=True)
+            elif async_ar:
+                handle = dist.all_reduce(dx, group=tp_group, async_op=True)
+        # weight gradient while the input-gradient collective is in flight
+        if fusion and hasattr(weight, "main_grad"):
+            _accumulate_main_grad(weight, dy2, t2)
+            dw = None
+        else:
+            dw = fops._wgrad(dy2, t2) if dy2.is_cuda else dy2.t().mm(t2)
+        db = dy2.sum(0) if ctx.has_bias else None
+        if handle is not None:
+            handle.wait()
+        return out, dw, db, None, None, None
+
+
+def _gather_seq(x):
+    ws = ps.get_tensor_model_parallel_world_size()
+    if ws == 1:
+        return x
+    x = x.contiguous()
+    out = torch.empty((ws * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(out, x, group=ps.get_tensor_model_parallel_group())
+    return out
+
+
+def linear_with_grad_accumulation_and_async_allreduce(x, weight, bias, gradient_accumulation_fusion,
+                                                      async_grad_allreduce, sequence_parallel_enabled):
+    return LinearWithGradAccumulationAndAsyncCommunication.apply(x, weight, bias, gradient_accumulation_fusion,
+                                                                 async_grad_allreduce, sequence_parallel_enabled)
+
+
 class VocabParallelEmbedding(nn.Module):
     """Embedding with the vocabulary split across the TP group; out-of-range ids produce 0
     locally and the all-reduce assembles the full lookup."""
@@ -108,7 +191,7 @@ class ColumnParallelLinear(nn.Module):
 
     def __init__(self, input_size, output_size, bias=True, gather_output=True, init_method=nn.init.xavier_normal_,
                  stride=1, keep_master_weight_for_test=False, skip_bias_add=False, *,
-                 no_async_tensor_model_parallel_allreduce=True, params_dtype=torch.float32,
+                 no_async_tensor_model_parallel_allreduce=False, params_dtype=torch.float32,
                  use_cpu_initialization=False, gradient_accumulation_fusion=False,
                  accumulation_in_fp16=False, sequence_parallel_enabled=False, device=None):
         super().__init__()
@@ -119,6 +202,10 @@ class ColumnParallelLinear(nn.Module):
         self.output_size_per_partition = divide(output_size, ws)
         self.skip_bias_add = skip_bias_add
         self.sequence_parallel_enabled = sequence_parallel_enabled
+        self.gradient_accumulation_fusion = gradient_accumulation_fusion
+        # async dX all-reduce only where a backward all-reduce exists (TP > 1, no sequence parallel)
+        self.async_tensor_model_parallel_allreduce = (not no_async_tensor_model_parallel_allreduce and ws > 1
+                                                      and not sequence_parallel_enabled)
         self.weight = Parameter(torch.empty(self.output_size_per_partition, input_size, dtype=params_dtype,
                                             device=device))
         self.master_weight = _initialize_affine_weight(self.weight, output_size, input_size,
@@ -131,12 +218,14 @@ class ColumnParallelLinear(nn.Module):
             self.register_parameter("bias", None)
 
     def forward(self, input_):
-        if self.sequence_parallel_enabled:
-            x = gather_from_sequence_parallel_region(input_, True)
-        else:
-            x = copy_to_tensor_model_parallel_region(input_)
         bias = self.bias if not self.skip_bias_add else None
-        out = fops.fused_dense(x, self.weight, bias)
+        if self.async_tensor_model_parallel_allreduce or self.sequence_parallel_enabled or \
+                self.gradient_accumulation_fusion:
+            out = linear_with_grad_accumulation_and_async_allreduce(
+                input_, self.weight, bias, self.gradient_accumulation_fusion,
+                self.async_tensor_model_parallel_allreduce, self.sequence_parallel_enabled)
+        else:
+            out = fops.fused_dense(copy_to_tensor_model_parallel_region(input_), self.weight, bias)
         if self.gather_output:
             assert not self.sequence_parallel_enabled
             out = gather_from_tensor_model_parallel_region(out)
@@ -159,6 +248,7 @@ class RowParallelLinear(nn.Module):
         self.input_size_per_partition = divide(input_size, ws)
         self.skip_bias_add = skip_bias_add
         self.sequence_parallel_enabled = sequence_parallel_enabled
+        self.gradient_accumulation_fusion = gradient_accumulation_fusion
         if sequence_parallel_enabled and not input_is_parallel:
             raise RuntimeError("To enable `sequence_parallel_enabled`, `input_is_parallel` must be `True`")
         self.weight = Parameter(torch.empty(output_size, self.input_size_per_partition, dtype=params_dtype,
@@ -174,7 +264,10 @@ class RowParallelLinear(nn.Module):
 
     def forward(self, input_):
         x = input_ if self.input_is_parallel else scatter_to_tensor_model_parallel_region(input_)
-        partial = fops.fused_dense(x, self.weight, None)
+        if self.gradient_accumulation_fusion:
+            partial = linear_with_grad_accumulation_and_async_allreduce(x, self.weight, None, True, False, False)
+        else:
+            partial = fops.fused_dense(x, self.weight, None)
         if self.sequence_parallel_enabled:
             out = reduce_scatter_to_sequence_parallel_region(partial)
         else:

@@ -140,6 +140,30 @@ def time_steps(env: DistEnv, step, steps: int, warmup: int, timer=None, sampler=
     return elapsed, out
 
 
+def instrumented_steps(env: DistEnv, step, steps: int, warmup: int, ddp=None):
+    """time_steps plus the run telemetry every benchmark line carries: per-step device time
+    spread, GPU clocks / power / temperature during the timed steps (amdsmi), TunableOp state,
+    library versions and, with an apex DDP wrapper, its bucket layout and comm timings.
+    Returns (elapsed_s, last step result, extra dict)."""
+    from . import telemetry
+
+    timer = telemetry.StepTimer(enabled=env.device.type == "cuda")
+    sampler = telemetry.GpuSampler(env.device.index or 0) if env.device.type == "cuda" else None
+    idle = sampler.snapshot() if sampler is not None else None
+    reset = ddp.reset_comm_stats if ddp is not None and hasattr(ddp, "reset_comm_stats") else None
+    elapsed, out = time_steps(env, step, steps, warmup, timer=timer if timer.enabled else None,
+                              sampler=sampler, on_timed_start=reset)
+    extra = {"step_ms": timer.summary() if timer.enabled else None,
+             "gpu": {"idle": idle, "timed": sampler.summary() if sampler is not None else None},
+             "tunableop": telemetry.tunableop_status() if env.device.type == "cuda" else None,
+             "versions": telemetry.library_versions()}
+    if ddp is not None and hasattr(ddp, "comm_stats"):
+        extra["ddp"] = ddp.comm_stats()
+    if env.device.type == "cuda":
+        extra["peak_mem_gb"] = round(torch.cuda.max_memory_allocated(env.device) / 2 ** 30, 1)
+    return elapsed, out, extra
+
+
 def emit(env: DistEnv, *, metric, items_per_step, unit, steps, warmup, elapsed, dtype, data, config,
          baseline=None, scaling="weak", extra=None):
     """Rank 0 prints the one-line JSON result; ``items_per_step`` is the whole-job count."""

@@ -97,6 +97,28 @@ def make_step(model, opt, batches, micro):
     return step
 
 
+def allreduce_probe(env, numel, iters=5):
+    """Bus bandwidth of one DDP-bucket-sized bf16 all-reduce on this job's communicator (the
+    scaling runs' diagnostic: compare with tools/allreduce_sweep.py's curve)."""
+    import time
+
+    import torch.distributed as dist
+
+    buf = torch.ones(numel, dtype=torch.bfloat16, device=env.device)
+    for _ in range(2):
+        dist.all_reduce(buf)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        dist.all_reduce(buf)
+    torch.cuda.synchronize()
+    t = (time.perf_counter() - t0) / iters
+    nbytes = numel * 2
+    algbw = nbytes / t / 1e9
+    return {"bytes": nbytes, "us": round(t * 1e6, 1), "algbw_gbs": round(algbw, 2),
+            "busbw_gbs": round(algbw * 2 * (env.world - 1) / env.world, 2)}
+
+
 def main():
     args = parse()
     from apex.utils import telemetry
@@ -140,6 +162,8 @@ def main():
         del model, opt, batches, loss
         gc.collect()
         torch.cuda.empty_cache()
+    if world > 1 and not args.fp32_only:
+        extra["allreduce_probe"] = allreduce_probe(env, args.message_size)
     fp32_ms = None
     if args.fp32_only or not args.no_fp32:
         model, opt = build(env, cfg, True, args.message_size)

@@ -29,7 +29,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     args = ap.parse_args()
 
-    from apex.utils.bench import emit, finish, init_distributed, time_steps
+    from apex.utils.bench import emit, finish, init_distributed, instrumented_steps
     from apex.utils.gemm_tuning import enable_tuned_gemms
 
     enable_tuned_gemms()
@@ -42,6 +42,7 @@ def main():
     from apex.models.megatron_gpt import (MegatronGPTConfig, build_stage, sync_embedding_grads,
                                           sync_initial_embeddings)
     from apex.optimizers import FusedAdam
+    from apex.parallel import DistributedDataParallel as DDP
     from apex.transformer import parallel_state as ps
     from apex.transformer import tensor_parallel as tp
     from apex.transformer.pipeline_parallel import get_forward_backward_func, setup_microbatch_calculator
@@ -63,6 +64,12 @@ def main():
     sync_initial_embeddings(model)
     opt = FusedAdam(model.parameters(), lr=1e-4, weight_decay=0.01)
     model, opt = amp.initialize(model, opt, opt_level="O2", cast_model_type=torch.bfloat16, verbosity=0)
+    # data-parallel gradient reduction on apex DDP buckets over the DP group; the pipeline schedule
+    # keeps the hooks off (no_sync) until each chunk's last microbatch backward, whose bucket
+    # all-reduces then overlap it
+    model = DDP(model, message_size=int(os.environ.get("APEX_DDP_MESSAGE_SIZE", 25_000_000)),
+                process_group=ps.get_data_parallel_group(), comm_timing=True)
+    stage = model.module
     n_local = args.global_batch // dp
     g = torch.Generator(device=env.device).manual_seed(7 + ps.get_data_parallel_rank())
     ids = torch.randint(0, cfg.vocab_size, (n_local, args.seq), device=env.device, generator=g)
@@ -75,16 +82,12 @@ def main():
     def step(i):
         losses = fb(fwd_step, ids, model, forward_only=False,
                     tensor_shape=(args.micro_batch, args.seq, args.hidden), dtype=torch.bfloat16)
-        sync_embedding_grads(model)
-        if dp > 1:
-            for p in model.parameters():
-                if p.grad is not None:
-                    dist.all_reduce(p.grad, op=dist.ReduceOp.AVG, group=ps.get_data_parallel_group())
+        sync_embedding_grads(stage)
         opt.step()
         opt.zero_grad()
         return losses
 
-    elapsed, losses = time_steps(env, step, args.steps, args.warmup)
+    elapsed, losses, extra = instrumented_steps(env, step, args.steps, args.warmup, ddp=model)
     loss = float(torch.stack([l["loss"] for l in losses]).float().mean()) if losses else None
     emit(env, metric="tokens/s Megatron-style GPT apex.transformer TP x PP over RCCL",
          items_per_step=args.global_batch * args.seq, unit="tokens/s", steps=args.steps, warmup=args.warmup,
@@ -92,7 +95,7 @@ def main():
          config={"model": f"GPT {args.layers}L H{args.hidden} {args.heads} heads", "global_batch": args.global_batch,
                  "micro_batch": args.micro_batch, "seq_len": args.seq,
                  "parallelism": f"tp{args.tp}xpp{args.pp}xdp{dp}"},
-         extra={"final_loss_last_stage_rank": loss})
+         extra=dict(extra, final_loss_last_stage_rank=loss))
     finish(env)
 
 

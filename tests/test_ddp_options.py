@@ -251,3 +251,21 @@ def test_broadcast_layout_from_rank0_world8(fake_world8, monkeypatch):
     model = DDP(M(), message_size=1)
     model().backward()
     assert [b.params for b in model._buckets] == [[i] for i in rank0_order]
+
+
+def test_allreduce_sweep_tool_gloo():
+    """tools/allreduce_sweep.py end to end under torchrun (gloo, 2 ranks, tiny sizes)."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, APEX_DIST_BACKEND="gloo")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                        os.path.join(root, "tools", "allreduce_sweep.py"), "--cpu", "--min-mb", "0.25",
+                        "--max-mb", "0.5", "--comms", "1,2", "--iters", "2", "--dtypes", "fp32"],
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=240, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rows = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(rows) == 4 and all(x["busbw_gbs"] > 0 and x["world"] == 2 for x in rows), rows
