@@ -19,30 +19,31 @@ def _seed_pair(p, device=None):
 
 
 class FlashAttnFunc(torch.autograd.Function):
-    """q, k, v: [B, S, H, D] views (D contiguous) -> o [B, Sq, H, D]."""
+    """q, k, v: [B, S, H, D] views (D contiguous) -> o [B, Sq, H, D]; ``bias``: optional additive
+    score bias (apex.contrib.multihead_attn.attention.prepare_bias layout), a constant."""
 
     @staticmethod
-    def forward(ctx, q, k, v, dropout_p, causal, scale, k_lens):
+    def forward(ctx, q, k, v, dropout_p, causal, scale, k_lens, bias=None):
         C = _ext.require()
         seed, offset = _seed_pair(dropout_p, q.device)
         o, lse, dmask = C.flash_attn_fwd(q, k, v, bool(causal), float(scale), float(dropout_p), seed, offset,
-                                  k_lens)
-        ctx.save_for_backward(q, k, v, o, lse, k_lens, dmask)
+                                         k_lens, bias)
+        ctx.save_for_backward(q, k, v, o, lse, k_lens, dmask, bias)
         ctx.cfg = (dropout_p, causal, scale, seed, offset)
         return o
 
     @staticmethod
     def backward(ctx, do):
         C = _ext.require()
-        q, k, v, o, lse, k_lens, dmask = ctx.saved_tensors
+        q, k, v, o, lse, k_lens, dmask, bias = ctx.saved_tensors
         p, causal, scale, seed, offset = ctx.cfg
         do = do.contiguous() if do.stride(-1) != 1 else do
         dq = torch.empty_like(q, memory_format=torch.contiguous_format) if not q.is_contiguous() else torch.empty_like(q)
         dk = torch.empty_like(k, memory_format=torch.contiguous_format) if not k.is_contiguous() else torch.empty_like(k)
         dv = torch.empty_like(v, memory_format=torch.contiguous_format) if not v.is_contiguous() else torch.empty_like(v)
         C.flash_attn_bwd(do, q, k, v, o, lse, dq, dk, dv, bool(causal), float(scale), float(p), seed,
-                         offset, k_lens, dmask)
-        return dq, dk, dv, None, None, None, None
+                         offset, k_lens, dmask, None, 0, bias)
+        return dq, dk, dv, None, None, None, None, None
 
 
 class FlashAttnPackedFunc(torch.autograd.Function):
@@ -50,20 +51,20 @@ class FlashAttnPackedFunc(torch.autograd.Function):
     The gradient is produced directly in the packed [B, S, 3, H, D] layout (no cat)."""
 
     @staticmethod
-    def forward(ctx, qkv, dropout_p, causal, scale, k_lens):
+    def forward(ctx, qkv, dropout_p, causal, scale, k_lens, bias=None):
         C = _ext.require()
         q, k, v = qkv.unbind(2)
-        seed, offset = _seed_pair(dropout_p, q.device)
+        seed, offset = _seed_pair(dropout_p, qkv.device)
         o, lse, dmask = C.flash_attn_fwd(q, k, v, bool(causal), float(scale), float(dropout_p), seed, offset,
-                                  k_lens)
-        ctx.save_for_backward(qkv, o, lse, k_lens, dmask)
+                                         k_lens, bias)
+        ctx.save_for_backward(qkv, o, lse, k_lens, dmask, bias)
         ctx.cfg = (dropout_p, causal, scale, seed, offset)
         return o
 
     @staticmethod
     def backward(ctx, do):
         C = _ext.require()
-        qkv, o, lse, k_lens, dmask = ctx.saved_tensors
+        qkv, o, lse, k_lens, dmask, bias = ctx.saved_tensors
         p, causal, scale, seed, offset = ctx.cfg
         if do.stride(-1) != 1 or do.stride(1) % 8 or do.stride(0) % 8 or do.stride(2) % 8:
             do = do.contiguous()
@@ -71,17 +72,17 @@ class FlashAttnPackedFunc(torch.autograd.Function):
         dqkv = torch.empty(qkv.shape, dtype=qkv.dtype, device=qkv.device)
         dq, dk, dv = dqkv.unbind(2)
         C.flash_attn_bwd(do, q, k, v, o, lse, dq, dk, dv, bool(causal), float(scale), float(p), seed,
-                         offset, k_lens, dmask)
-        return dqkv, None, None, None, None
+                         offset, k_lens, dmask, None, 0, bias)
+        return dqkv, None, None, None, None, None
 
 
-def flash_attention_packed(qkv, dropout_p=0.0, causal=False, scale=None, k_lens=None):
+def flash_attention_packed(qkv, dropout_p=0.0, causal=False, scale=None, k_lens=None, bias=None):
     d = qkv.shape[-1]
     scale = 1.0 / math.sqrt(d) if scale is None else scale
-    return FlashAttnPackedFunc.apply(qkv, float(dropout_p), bool(causal), float(scale), k_lens)
+    return FlashAttnPackedFunc.apply(qkv, float(dropout_p), bool(causal), float(scale), k_lens, bias)
 
 
-def flash_attention(q, k, v, dropout_p=0.0, causal=False, scale=None, k_lens=None):
+def flash_attention(q, k, v, dropout_p=0.0, causal=False, scale=None, k_lens=None, bias=None):
     d = q.shape[-1]
     scale = 1.0 / math.sqrt(d) if scale is None else scale
-    return FlashAttnFunc.apply(q, k, v, float(dropout_p), bool(causal), float(scale), k_lens)
+    return FlashAttnFunc.apply(q, k, v, float(dropout_p), bool(causal), float(scale), k_lens, bias)

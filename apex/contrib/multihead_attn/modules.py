@@ -6,7 +6,9 @@ attention that reads Q/K/V straight out of the projection output through strides
 split / transpose copies) -> output projection with the bias gradient folded into a HIP
 column-sum; with ``include_norm_add`` the pre-LayerNorm is the HIP FusedLayerNorm and the
 residual + dropout epilogue is one fused kernel each way.
-Key padding masks are consumed as per-sequence valid lengths (right padding).
+Key padding masks ([B, Sk], nonzero = padded) become an additive [B, 1, 1, Sk] bias (any padding
+pattern, no host synchronisation), combined with ``attn_mask`` (bool: True = masked; float:
+additive when ``mask_additive``, else nonzero = masked) inside the flash kernel.
 """
 from __future__ import annotations
 
@@ -21,22 +23,28 @@ from ...ops import fused as fops
 from . import attention as _attn
 
 
-def _k_lens(key_padding_mask):
-    if key_padding_mask is None:
-        return None
-    kp = key_padding_mask
-    if kp.dtype != torch.bool:
-        kp = kp != 0
-    return (~kp).sum(1, dtype=torch.int32)
-
-
-def _bias_from_attn_mask(attn_mask, dtype):
+def _bias_from_attn_mask(attn_mask, dtype, additive=True):
     if attn_mask is None:
         return None
-    if attn_mask.dtype == torch.bool:
-        return torch.zeros(attn_mask.shape, dtype=dtype, device=attn_mask.device).masked_fill(
-            attn_mask, float("-inf"))
+    if attn_mask.dtype == torch.bool or not additive:
+        masked = attn_mask if attn_mask.dtype == torch.bool else attn_mask != 0
+        return torch.zeros(attn_mask.shape, dtype=dtype, device=attn_mask.device).masked_fill(masked, float("-inf"))
     return attn_mask.to(dtype)
+
+
+def _combined_bias(attn_mask, key_padding_mask, dtype, additive=True):
+    """[Sq, Sk] / [B|1, H|1, Sq, Sk] attn_mask and [B, Sk] key_padding_mask -> one additive bias."""
+    bias = _bias_from_attn_mask(attn_mask, dtype, additive)
+    if key_padding_mask is not None:
+        kp = key_padding_mask if key_padding_mask.dtype == torch.bool else key_padding_mask != 0
+        kb = torch.zeros(kp.shape, dtype=dtype, device=kp.device).masked_fill(kp, float("-inf"))[:, None, None, :]
+        if bias is None:
+            bias = kb
+        else:
+            while bias.dim() < 4:
+                bias = bias.unsqueeze(0)
+            bias = bias + kb
+    return bias
 
 
 class SelfMultiheadAttn(nn.Module):
@@ -103,10 +111,8 @@ class SelfMultiheadAttn(nn.Module):
         w, b = self._in_proj()
         qkv = fops.fused_dense(x, w, b).view(S, B, 3, self.num_heads, self.head_dim)
         q, k, v = (t.transpose(0, 1) for t in qkv.unbind(2))  # [B, S, H, D] strided views
-        bias = _bias_from_attn_mask(attn_mask, q.dtype)
-        if bias is not None and not self.mask_additive and attn_mask is not None and attn_mask.dtype != torch.bool:
-            bias = bias.masked_fill(attn_mask != 0, float("-inf"))
-        ctx = _attn.attention(q, k, v, bias, p, causal, self.scaling, _k_lens(key_padding_mask))
+        bias = _combined_bias(attn_mask, key_padding_mask, q.dtype, self.mask_additive)
+        ctx = _attn.attention(q, k, v, bias, p, causal, self.scaling)
         ctx = ctx.transpose(0, 1).reshape(S, B, E)
         if self.include_norm_add:
             return fops.bias_dropout_add(fops.fused_dense(ctx, self.out_proj_weight, None),
@@ -160,8 +166,8 @@ class EncdecMultiheadAttn(nn.Module):
         kv = fops.fused_dense(key, self.in_proj_weight_kv, self.in_proj_bias_kv)
         q = q.view(Sq, B, self.num_heads, self.head_dim).transpose(0, 1)
         k, v = (t.transpose(0, 1) for t in kv.view(Sk, B, 2, self.num_heads, self.head_dim).unbind(2))
-        ctx = _attn.attention(q, k, v, _bias_from_attn_mask(attn_mask, q.dtype), p, False, self.scaling,
-                              _k_lens(key_padding_mask))
+        ctx = _attn.attention(q, k, v, _combined_bias(attn_mask, key_padding_mask, q.dtype), p, False,
+                              self.scaling)
         ctx = ctx.transpose(0, 1).reshape(Sq, B, E)
         if self.include_norm_add:
             return fops.bias_dropout_add(fops.fused_dense(ctx, self.out_proj_weight, None),

@@ -173,7 +173,7 @@ def attention_sublayer(x, wqkv, bqkv, wo, bo, gamma, beta, heads, p_attn=0.0, p_
     not apply (caller falls back to the op-by-op composition)."""
     E = x.shape[-1]
     d = E // heads
-    if not (_ok(x, E) and d in (64, 128) and gamma is not None and beta is not None):
+    if not (_ok(x, E) and d in (32, 64, 128, 256) and gamma is not None and beta is not None):
         return None
     p_attn = p_attn if training else 0.0
     p_hidden = p_hidden if training else 0.0

@@ -1,928 +1,9 @@
-// Flash attention forward + backward on CDNA4 MFMA (NS-05; apex.contrib.multihead_attn core).
-//
-// Layout: q/k/v/o are [B, S, H, D] views with arbitrary batch / seq strides (so the packed
-// QKV projection output [B, S, 3, H, D] is consumed in place, no split/transposes).
-// D in {64, 128}; bf16 / fp16 in, fp32 accumulate; optional causal mask, per-batch key
-// lengths and Philox dropout regenerated identically in backward.
-//
-// Forward (one workgroup = 4 wave64 = 128 query rows, 32 per wave; K/V streamed in 64-key
-// tiles through LDS):
-//   S^T = K . Q^T with v_mfma_f32_32x32x16 — the swapped product puts ONE query per lane
-//   (16 keys in registers, the other 16 in lane^32), so row max / row sum need a single
-//   cross-half exchange and the rescale factor is lane-local;
-//   O^T += V^T . P^T reuses the S^T accumulator registers directly as the B operand
-//   (k-order permuted to match, no LDS round trip for P); the V^T operand comes from the
-//   row-major V tile with ds_read_b64_tr_b16 (hardware transpose read).
-// Backward (one workgroup = 4 waves x 32 keys = 128 keys; loop over 32-query blocks):
-//   S = Q.K^T and dP = dO.V^T with K, V rows held in registers; dV += P^T.dO and
-//   dK += dS^T.Q use the accumulators as A operands with tr-read B operands from the
-//   Q/dO tiles in LDS; dQ = dS.K goes through LDS (dS) and, when several workgroups
-//   share a query block (Sk > 128), fp32 atomics.
-#include "common.h"
-#include "kernels.h"
-
-#include <type_traits>
+// Flash attention (NS-05): head-dim dispatch and the dropout-mask debug kernel. The kernel
+// templates live in attention_impl.h; attention_d{32,64,128,256}.hip instantiate one head dim
+// each so the (many) variants compile in parallel.
+#include "attention_impl.h"
 
 namespace apex {
-
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-template <typename T> struct MfmaT;
-template <> struct MfmaT<bf16> {
-  using V8 = bf16x8;
-  __device__ static __forceinline__ f32x16 mma(V8 a, V8 b, f32x16 c) {
-    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-  }
-};
-template <> struct MfmaT<f16> {
-  using V8 = f16x8;
-  __device__ static __forceinline__ f32x16 mma(V8 a, V8 b, f32x16 c) {
-    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
-  }
-};
-
-// 16x16x32 products (the backward's dQ tiles): lane l holds C[4 (l >> 4) + i][l & 15]
-template <typename T> struct Mfma16T;
-template <> struct Mfma16T<bf16> {
-  __device__ static __forceinline__ f32x4 mma(bf16x8 a, bf16x8 b, f32x4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-  }
-};
-template <> struct Mfma16T<f16> {
-  __device__ static __forceinline__ f32x4 mma(f16x8 a, f16x8 b, f32x4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
-  }
-};
-
-constexpr float kLog2e = 1.4426950408889634f;
-constexpr float kLn2 = 0.6931471805599453f;
-
-// transposed LDS read: 4 rows x 16 cols block, lane i of each 16-lane group gets column i
-__device__ __forceinline__ s16x4 lds_tr16(const void* p) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (__attribute__((address_space(3))) s16x4*)(p));
-}
-
-// Workgroup barrier ordering LDS traffic only: the fences are restricted to the "local"
-// address space, so outstanding global loads (register prefetches) are NOT drained at the
-// barrier the way __syncthreads()'s full workgroup fence drains them.
-__device__ __forceinline__ void lds_barrier() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
-template <typename V8>
-__device__ __forceinline__ V8 join4(s16x4 lo, s16x4 hi) {
-  typedef short s16x8 __attribute__((ext_vector_type(8)));
-  s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(V8, r);
-}
-
-template <typename T, typename V8>
-__device__ __forceinline__ V8 pack8(const float* x) {
-  typedef T t8 __attribute__((ext_vector_type(8)));
-  t8 r;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = (T)x[j];
-  return __builtin_bit_cast(V8, r);
-}
-
-// Attention dropout keep bits: 8-bit uniforms (keep iff u8 >= thresh), 16 per Philox4x32-7
-// call. One call per (row, 16-key half of a 32-key block); the four 32-bit outputs are compared
-// against the threshold four bytes at a time (SWAR: the carry out of u + (256 - thresh) in each
-// byte is the keep bit — u & 0x7f.. plus the low 7 bits of the addend, then the majority of the
-// three top bits), and the carries are shifted into the natural bit order: the returned 16 bits
-// land at positions 4 hl + {0..3, 8..11, 16..19, 24..27}, i.e. bit k of the OR of both halves is
-// key k of the block (random word j = k & 3 of half hl = (k >> 2) & 1, byte k >> 3).
-struct DropGen {
-  uint64_t seed, offset;
-  uint32_t thresh;
-  __device__ __forceinline__ uint32_t half_bits(int64_t bh, int64_t row, int64_t blk, int hl, int64_t Sq) const {
-    Philox ph(seed, (uint64_t)(bh * Sq + row), offset + (uint64_t)(2 * blk + hl));
-    const uint4 r = ph.next();
-    const uint32_t C = (256u - thresh) * 0x01010101u;
-    const uint32_t C7 = C & 0x7f7f7f7fu;
-    const uint32_t w[4] = {r.x, r.y, r.z, r.w};
-    uint32_t out = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t u = w[j];
-      const uint32_t s7 = (u & 0x7f7f7f7fu) + C7;
-      const uint32_t carry = ((u & C) | ((u | C) & s7)) & 0x80808080u;  // bit 8b+7: keep of byte b
-      out |= carry >> (7 - j);                                           // -> bit 8b + j
-    }
-    return out << (4 * hl);
-  }
-  __device__ __forceinline__ uint32_t block_bits(int64_t bh, int64_t row, int64_t blk, int64_t Sq) const {
-    return half_bits(bh, row, blk, 0, Sq) | half_bits(bh, row, blk, 1, Sq);
-  }
-};
-
-constexpr int kFwdWaves = 4;
-constexpr int kFwdBQ = 32 * kFwdWaves;  // 128 query rows per workgroup
-constexpr int kFwdKB = 64;              // keys per tile
-
-// SHORT (D = 64, Sk <= 128, no dropout: BERT-shape inference): the whole key range is staged into LDS once (36 KB)
-// and no register copy of K/V is live during the math, which brings the kernel to 128 VGPRs:
-// 4 workgroups (16 waves, 144 KB of LDS) per CU instead of 2 for a kernel that is one
-// load -> math -> store pass per workgroup, so the other workgroups' loads hide the HBM latency.
-template <typename T, int D, bool CAUSAL, bool DROPOUT, bool SHORT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SHORT ? 4 : 2)))
-attn_fwd_kernel(AttnArgs a) {
-  static_assert(!SHORT || D == 64, "SHORT is the D = 64 single-pass variant");
-  using M = MfmaT<T>;
-  using V8 = typename M::V8;
-  constexpr int LDR = D + 8;  // padded LDS row (elements)
-  constexpr int NBUF = SHORT ? 2 : 1;
-  __shared__ __attribute__((aligned(16))) T lds_k[NBUF * kFwdKB * LDR];
-  __shared__ __attribute__((aligned(16))) T lds_v[NBUF * kFwdKB * LDR];
-
-  // wid through readfirstlane: wave-uniform in SGPRs, so tile-level conditions become scalar branches
-  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int r = lane & 31, hl = lane >> 5;
-  const int bh = blockIdx.y;
-  const int b = bh / a.H, h = bh % a.H;
-  const int q0 = blockIdx.x * kFwdBQ;
-  const int qrow = q0 + 32 * wid + r;
-  const int Sk = a.k_lens ? min(a.k_lens[b], a.Sk) : a.Sk;
-
-  const T* qp = (const T*)a.q + b * a.q_bs + h * a.q_hs;
-  const T* kp = (const T*)a.k + b * a.k_bs + h * a.k_hs;
-  const T* vp = (const T*)a.v + b * a.v_bs + h * a.v_hs;
-
-  // Q^T fragments (B operand): lane (q=r, hl) holds Q[q][16s + 8hl .. +7]
-  V8 qf[D / 16];
-#pragma unroll
-  for (int s = 0; s < D / 16; ++s) {
-    if (qrow < a.Sq) qf[s] = *(const V8*)(qp + (int64_t)qrow * a.q_ss + 16 * s + 8 * hl);
-    else qf[s] = V8{};
-  }
-
-  f32x16 o[D / 32];
-#pragma unroll
-  for (int i = 0; i < D / 32; ++i) o[i] = f32x16{};
-  float m = -INFINITY, l = 0.f;
-
-  int kend = Sk;
-  if (CAUSAL) kend = min(kend, q0 + kFwdBQ);
-  const int ntiles = (kend + kFwdKB - 1) / kFwdKB;
-
-  // tile loader: 64 x D elements, 16B chunks, CH chunks per thread
-  constexpr int CPR = D / 8;               // chunks per row
-  constexpr int CH = kFwdKB * CPR / 256;   // chunks per thread per tensor
-  // K/V tiles of the tile TWO ahead are loaded into registers while the current tile computes
-  // (two register sets, loop unrolled by two) at D = 64; one ahead at D = 128 (register budget)
-  constexpr bool KV2 = D == 64;
-  constexpr int AHEAD = KV2 ? 2 : 1;
-  struct KV {
-    uint4 k[CH], v[CH];
-  };
-  KV kva, kvb;
-  // dropout: each lane draws the keep bits of its own 16 keys of every 32-key block in the
-  // loop (one Philox call per block, DropGen::half_bits), and the two lane halves' words are
-  // combined and stored for the backward kernels
-  uint32_t* mrow =
-      DROPOUT && qrow < a.Sq ? (uint32_t*)(a.dmask + ((int64_t)bh * a.Sq + qrow) * a.mask_words) : nullptr;
-  const DropGen dg{a.seed, a.offset, a.drop_thresh};
-  auto gload = [&](KV& R, int kt) {
-    uint4 (&kreg)[CH] = R.k;
-    uint4 (&vreg)[CH] = R.v;
-#pragma unroll
-    for (int c = 0; c < CH; ++c) {
-      const int idx = threadIdx.x + 256 * c;
-      const int row = idx / CPR, col = (idx % CPR) * 8;
-      const int key = kt * kFwdKB + row;
-      if (key < Sk) {
-        kreg[c] = *(const uint4*)(kp + (int64_t)key * a.k_ss + col);
-        vreg[c] = *(const uint4*)(vp + (int64_t)key * a.v_ss + col);
-      } else {
-        kreg[c] = make_uint4(0, 0, 0, 0);
-        vreg[c] = make_uint4(0, 0, 0, 0);
-      }
-    }
-  };
-  auto lstore = [&](KV& R, const int rowoff) {
-    uint4 (&kreg)[CH] = R.k;
-    uint4 (&vreg)[CH] = R.v;
-#pragma unroll
-    for (int c = 0; c < CH; ++c) {
-      const int idx = threadIdx.x + 256 * c;
-      const int row = rowoff + idx / CPR, col = (idx % CPR) * 8;
-      *(uint4*)(lds_k + row * LDR + col) = kreg[c];
-      *(uint4*)(lds_v + row * LDR + col) = vreg[c];
-    }
-  };
-
-  if (ntiles > 0) gload(kva, 0);
-  if (KV2 && ntiles > 1) gload(kvb, 1);
-  // math of key tile kt, read from LDS rows lr0 ..
-  auto compute = [&](const int kt) {
-    const int lr0 = SHORT ? kt * kFwdKB : 0;
-    uint32_t mcur[2] = {0u, 0u};
-    if (DROPOUT) {
-#pragma unroll
-      for (int sb = 0; sb < 2; ++sb) {
-        const int blk = (kt * kFwdKB >> 5) + sb;
-        const uint32_t hb = dg.half_bits(bh, qrow, blk, hl, a.Sq);  // bits at 4 hl + {0-3, 8-11, ..}
-        const uint32_t word = hb | __shfl_xor(hb, 32, 64);
-        if (hl == 0 && mrow && blk * 32 < a.Sk) mrow[blk] = word;
-        mcur[sb] = hb >> (4 * hl);
-      }
-    }
-    const int kb = kt * kFwdKB;
-
-    // ---- S^T for two 32-key sub-blocks
-    // all K fragments of the tile are read before the MFMA chain (one LDS latency per tile
-    // instead of one per MFMA)
-    f32x16 st[2];
-    V8 kf[2][D / 16];
-#pragma unroll
-    for (int sb = 0; sb < 2; ++sb)
-#pragma unroll
-      for (int s = 0; s < D / 16; ++s) kf[sb][s] = *(const V8*)(lds_k + (lr0 + 32 * sb + r) * LDR + 16 * s + 8 * hl);
-    __builtin_amdgcn_sched_group_barrier(0x100, 2 * (D / 16), 0);  // DS reads first
-    __builtin_amdgcn_sched_group_barrier(0x008, 2 * (D / 16), 0);  // then the MFMAs
-#pragma unroll
-    for (int sb = 0; sb < 2; ++sb) {
-      st[sb] = f32x16{};
-#pragma unroll
-      for (int s = 0; s < D / 16; ++s) st[sb] = M::mma(kf[sb][s], qf[s], st[sb]);
-    }
-    // D = 64: the V^T fragments of the PV product are read now, their LDS latency hidden
-    // behind the softmax (D = 128 would not fit in the register budget of 2 workgroups/CU)
-    constexpr bool HOIST_V = D == 64;
-    V8 vt[2][2][HOIST_V ? D / 32 : 1];
-    if constexpr (HOIST_V) {
-#pragma unroll
-      for (int sb = 0; sb < 2; ++sb)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-          for (int db = 0; db < D / 32; ++db) {
-            const int k0 = lr0 + 32 * sb + 16 * s2 + 4 * hl + ((lane & 15) >> 2);
-            const int c0 = 32 * db + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-            vt[sb][s2][db] = join4<V8>(lds_tr16(lds_v + k0 * LDR + c0), lds_tr16(lds_v + (k0 + 8) * LDR + c0));
-          }
-    }
-    // ---- mask (boundary tiles only) + running max on the RAW scores; the softmax scale is
-    // folded into the exp2 argument (one FMA per element) and exp2 is the bare v_exp_f32
-    // (no denormal range reduction: underflow to 0 is what softmax wants).
-    const bool interior = (kb + kFwdKB <= Sk) && (!CAUSAL || kb + kFwdKB - 1 <= q0 + 32 * wid);
-    if (!interior) {
-      // keys valid for this lane's query: key < lim (one compare + select per element)
-      const int lim = CAUSAL ? min(Sk, qrow + 1) : Sk;
-#pragma unroll
-      for (int sb = 0; sb < 2; ++sb) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int key = kb + 32 * sb + (i & 3) + 8 * (i >> 2) + 4 * hl;
-          if (key >= lim) st[sb][i] = -INFINITY;
-        }
-      }
-    }
-    float tmax = -INFINITY;
-#pragma unroll
-    for (int sb = 0; sb < 2; ++sb)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) tmax = fmaxf(tmax, st[sb][i]);
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float mnew = fmaxf(m, tmax);
-    const float muse = mnew == -INFINITY ? 0.f : mnew;
-    const float alpha = __builtin_amdgcn_exp2f((m - muse) * a.scale_log2);
-    const float mscaled = -muse * a.scale_log2;
-    m = mnew;
-    float psum = 0.f;
-#pragma unroll
-    for (int sb = 0; sb < 2; ++sb) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float p = __builtin_amdgcn_exp2f(fmaf(st[sb][i], a.scale_log2, mscaled));
-        psum += p;
-        // dropped: keep bit i selects p or +0 (bfe sign-extends the bit to an all-ones mask);
-        // the 1/(1-p) rescale is applied once in the epilogue
-        // element i = key (i & 3) + 8 (i >> 2) + 4 hl: bit (i & 3) + 8 (i >> 2) of the shifted word
-        st[sb][i] = DROPOUT ? __builtin_bit_cast(float, __builtin_bit_cast(int, p) &
-                                                            __builtin_amdgcn_sbfe((int)mcur[sb], (i & 3) + 8 * (i >> 2), 1))
-                            : p;
-      }
-    }
-    l = l * alpha + psum;
-#pragma unroll
-    for (int db = 0; db < D / 32; ++db)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) o[db][i] *= alpha;
-    // ---- O^T += V^T . P^T
-#pragma unroll
-    for (int sb = 0; sb < 2; ++sb) {
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        float pv[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) pv[j] = st[sb][8 * s2 + j];
-        const V8 pf = pack8<T, V8>(pv);
-        const int k0 = lr0 + 32 * sb + 16 * s2 + 4 * hl + ((lane & 15) >> 2);
-#pragma unroll
-        for (int db = 0; db < D / 32; ++db) {
-          if constexpr (HOIST_V) {
-            o[db] = M::mma(vt[sb][s2][db], pf, o[db]);
-          } else {
-            const int c0 = 32 * db + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-            const s16x4 lo = lds_tr16(lds_v + k0 * LDR + c0);
-            const s16x4 hi = lds_tr16(lds_v + (k0 + 8) * LDR + c0);
-            o[db] = M::mma(join4<V8>(lo, hi), pf, o[db]);
-          }
-        }
-      }
-    }
-  };
-  auto tile = [&](KV& R, const int kt) {
-    lds_barrier();  // previous tile fully consumed
-    lstore(R, 0);
-    lds_barrier();
-    if (kt + AHEAD < ntiles) gload(R, kt + AHEAD);
-    compute(kt);
-  };
-  if constexpr (SHORT) {
-    // both (<= 2) tiles were loaded above: one LDS stage, then the math with no K/V registers live
-    if (ntiles > 0) lstore(kva, 0);
-    if (ntiles > 1) lstore(kvb, kFwdKB);
-    lds_barrier();
-    if (ntiles > 0) compute(0);
-    if (ntiles > 1) compute(1);
-  } else if constexpr (KV2) {
-    for (int kt = 0; kt < ntiles; kt += 2) {
-      tile(kva, kt);
-      if (kt + 1 < ntiles) tile(kvb, kt + 1);
-    }
-  } else {
-    for (int kt = 0; kt < ntiles; ++kt) tile(kva, kt);
-  }
-  // ---- epilogue
-  const float ltot = l + __shfl_xor(l, 32, 64);
-  if (qrow < a.Sq) {
-    const float inv = ltot > 0.f ? (DROPOUT ? a.drop_scale : 1.f) / ltot : 0.f;
-    T* op = (T*)a.o + b * a.o_bs + h * a.o_hs + (int64_t)qrow * a.o_ss;
-#pragma unroll
-    for (int db = 0; db < D / 32; ++db) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        typedef T t4 __attribute__((ext_vector_type(4)));
-        t4 w;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) w[e] = (T)(o[db][4 * g + e] * inv);
-        *(t4*)(op + 32 * db + 8 * g + 4 * hl) = w;
-      }
-    }
-    if (hl == 0 && a.lse)
-      a.lse[(int64_t)bh * a.Sq + qrow] = ltot > 0.f ? (m * a.scale_log2 + log2f(ltot)) * kLn2 : INFINITY;
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Backward
-// ---------------------------------------------------------------------------
-constexpr int kBwdWaves = 4;
-constexpr int kBwdBK = 32 * kBwdWaves;  // 128 keys per workgroup
-constexpr int kBwdBQ = 32;              // queries per inner step
-
-// DQ = true (Sk <= 128: the workgroup holds every key, so it is the sole owner of dQ for its
-// query rows and writes it directly). DQ = false (longer key ranges): dK/dV only; the key-block-0
-// workgroups also store delta = rowsum(dO * O) into delta_out, and attn_bwd_dq_kernel computes dQ
-// from a query-stationary loop (no cross-workgroup fp32 atomics; see the kernel below).
-template <typename T, int D, bool CAUSAL, bool DROPOUT, bool DSUM, bool DQ>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 64 ? 2 : 1, D == 64 ? 2 : 1))) attn_bwd_kernel(AttnArgs a, const void* dout, float* delta_out,
-                                                         void* dk_out, void* dv_out) {
-  using M = MfmaT<T>;
-  using V8 = typename M::V8;
-  constexpr int LDR = D + 8;
-  constexpr int LDS_S = kBwdBK + 8;  // dS row stride (elements)
-  constexpr int KT_LD = kBwdBK + 8;  // K^T row stride (elements); K^T shares lds_k (D*KT_LD <= kBwdBK*LDR)
-  static_assert(D * KT_LD <= kBwdBK * LDR, "K^T must fit the lds_k staging buffer");
-  __shared__ __attribute__((aligned(16))) T lds_q[kBwdBQ * LDR];
-  __shared__ __attribute__((aligned(16))) T lds_do[kBwdBQ * LDR];
-  __shared__ __attribute__((aligned(16))) T lds_k[kBwdBK * LDR];
-  __shared__ __attribute__((aligned(16))) T lds_ds[kBwdBQ * LDS_S];
-  __shared__ float lds_lse[kBwdBQ], lds_delta[kBwdBQ];
-  __shared__ uint32_t lds_mask[4 * kBwdBQ];  // [wave's 32-key block][q]: bit k <-> key 32 wid + k
-
-  // wid through readfirstlane: wave-uniform in SGPRs, so tile-level conditions become scalar branches
-  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int r = lane & 31, hl = lane >> 5;
-  const int bh = blockIdx.y;
-  const int b = bh / a.H, h = bh % a.H;
-  const int k0 = blockIdx.x * kBwdBK;
-  const int Sk = a.k_lens ? min(a.k_lens[b], a.Sk) : a.Sk;
-  const int mykey = k0 + 32 * wid + r;  // key row this lane holds as K/V operand
-
-  const T* qp = (const T*)a.q + b * a.q_bs + h * a.q_hs;
-  const T* kp = (const T*)a.k + b * a.k_bs + h * a.k_hs;
-  const T* vp = (const T*)a.v + b * a.v_bs + h * a.v_hs;
-  const T* dop = (const T*)dout + b * a.do_bs + h * a.do_hs;
-  const T* op = (const T*)a.o + b * a.o_bs + h * a.o_hs;
-  const float* lsep = a.lse + (int64_t)bh * a.Sq;
-
-  // accumulators: dK, dV  [key x dim]: C rows = keys (regs), cols = dim (lanes)
-  f32x16 dk[D / 32], dv[D / 32];
-#pragma unroll
-  for (int i = 0; i < D / 32; ++i) {
-    dk[i] = f32x16{};
-    dv[i] = f32x16{};
-  }
-
-  int qstart = 0;
-  if (CAUSAL) qstart = (k0 / kBwdBQ) * kBwdBQ;
-  const int nq = a.Sq;
-  const float rkeep = a.drop_scale;
-
-  // Q / dO / O tiles (32 x D), lse and the dropout words of the query block TWO steps ahead
-  // are loaded into registers while the current block computes (two register sets, the loop
-  // unrolled by two, so every global load has two steps of compute to land in); the barriers
-  // below only wait for LDS traffic so these global loads stay in flight across them.
-  constexpr int CPR = D / 8;
-  constexpr int NLD = kBwdBQ * CPR / 256;
-  struct Pf {
-    uint4 q[NLD], d[NLD], o[NLD];
-    float lse;
-    uint32_t mask;
-  };
-  // two register sets where they fit (dK/dV-only kernel at D = 64); one set (prefetch one step
-  // ahead) for the fused single-key-block kernel and D = 128, which would spill
-  constexpr bool DEPTH2 = !DQ && D == 64;
-  constexpr int AHEAD = DEPTH2 ? 2 : 1;
-  Pf pfa, pfb;
-  auto fetch = [&](Pf& P, int qb) {
-    uint4 (&pf_q)[NLD] = P.q;
-    uint4 (&pf_do)[NLD] = P.d;
-    uint4 (&pf_o)[NLD] = P.o;
-    float& pf_lse = P.lse;
-    uint32_t& pf_mask = P.mask;
-    pf_lse = INFINITY;
-    pf_mask = 0u;
-#pragma unroll
-    for (int c = 0; c < NLD; ++c) {
-      const int idx = threadIdx.x + 256 * c;
-      const int row = idx / CPR, col = (idx % CPR) * 8;
-      const int q = qb + row;
-      if (q < nq) {
-        pf_q[c] = *(const uint4*)(qp + (int64_t)q * a.q_ss + col);
-        pf_do[c] = *(const uint4*)(dop + (int64_t)q * a.do_ss + col);
-        pf_o[c] = *(const uint4*)(op + (int64_t)q * a.o_ss + col);
-      } else {
-        pf_q[c] = pf_do[c] = pf_o[c] = make_uint4(0, 0, 0, 0);
-      }
-    }
-    // raw values only: any arithmetic on a loaded value here would make the compiler wait for
-    // the whole prefetch (s_waitcnt vmcnt(0)) instead of letting it land during the next step
-    if (threadIdx.x < kBwdBQ) {
-      const int q = qb + threadIdx.x;
-      if (q < nq) pf_lse = lsep[q];  // natural log; x log2(e) at staging
-    }
-    if (DROPOUT && threadIdx.x < 4 * kBwdBQ) {
-      // dropout words written by the forward: one per (query, 32-key block), bit k <-> key k
-      const int qi = threadIdx.x & (kBwdBQ - 1), w = threadIdx.x / kBwdBQ;
-      const int q = qb + qi, blk = (k0 >> 5) + w;
-      if (q < nq && blk * 32 < a.Sk) pf_mask = ((const uint32_t*)(a.dmask + ((int64_t)bh * a.Sq + q) * a.mask_words))[blk];
-    }
-  };
-  V8 kf[D / 16], vf[D / 16];
-  auto load_kv = [&]() {
-  // K and V rows for this wave's 32 keys as B operands: lane (key=r, hl) holds X[key][16s+8hl..]
-#pragma unroll
-  for (int s = 0; s < D / 16; ++s) {
-    if (mykey < Sk) {
-      kf[s] = *(const V8*)(kp + (int64_t)mykey * a.k_ss + 16 * s + 8 * hl);
-      vf[s] = *(const V8*)(vp + (int64_t)mykey * a.v_ss + 16 * s + 8 * hl);
-    } else {
-      kf[s] = V8{};
-      vf[s] = V8{};
-    }
-  }
-  // whole K block to LDS transposed, K^T [D][kBwdBK + 8] (the A operand of dQ^T = K^T . dS^T,
-  // read as 16-byte rows); written once per workgroup
-  if (DQ)
-  for (int idx = threadIdx.x; idx < kBwdBK * (D / 8); idx += 256) {
-    const int row = idx / (D / 8), col = (idx % (D / 8)) * 8;
-    const int key = k0 + row;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (key < Sk) v = *(const uint4*)(kp + (int64_t)key * a.k_ss + col);
-    const T* e = (const T*)&v;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) lds_k[(col + j) * KT_LD + row] = e[j];
-  }
-  };
-  // D = 64: the K/V loads are issued after the first query-block fetch, so both latencies
-  // overlap (at D = 128 that order spills registers)
-  if (D == 128) load_kv();
-  if (qstart < nq) fetch(pfa, qstart);
-  if (DEPTH2 && qstart + kBwdBQ < nq) fetch(pfb, qstart + kBwdBQ);
-  if (D == 64) load_kv();
-
-  float dqcs[D / 32][4] = {};  // DSUM: this lane's dq dims (see the dQ section) summed over queries
-  auto body = [&](Pf& P, const int qb) {
-    uint4 (&pf_q)[NLD] = P.q;
-    uint4 (&pf_do)[NLD] = P.d;
-    uint4 (&pf_o)[NLD] = P.o;
-    lds_barrier();
-    // stage the prefetched tiles; delta = rowsum(dO * O) is computed here from O
-    // (CPR consecutive threads own one row -> xor-shuffle reduce), no separate pass.
-#pragma unroll
-    for (int c = 0; c < NLD; ++c) {
-      const int idx = threadIdx.x + 256 * c;
-      const int row = idx / CPR, col = (idx % CPR) * 8;
-      float ov[8], dov[8];
-      load_f<T, 8>((const T*)&pf_o[c], ov);
-      load_f<T, 8>((const T*)&pf_do[c], dov);
-      float part = 0.f;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) part += ov[e] * dov[e];
-#pragma unroll
-      for (int o = CPR / 2; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
-      if ((idx % CPR) == 0) {
-        lds_delta[row] = part;
-        if (!DQ && blockIdx.x == 0 && qb + row < nq) delta_out[(int64_t)bh * a.Sq + qb + row] = part;
-      }
-      *(uint4*)(lds_q + row * LDR + col) = pf_q[c];
-      *(uint4*)(lds_do + row * LDR + col) = pf_do[c];
-    }
-    if (threadIdx.x < kBwdBQ) lds_lse[threadIdx.x] = P.lse * kLog2e;  // +inf stays +inf
-    if (DROPOUT && threadIdx.x < 4 * kBwdBQ) lds_mask[threadIdx.x] = P.mask;
-    if (qb + AHEAD * kBwdBQ < nq && !(a.dbg & 8)) fetch(P, qb + AHEAD * kBwdBQ);
-    lds_barrier();
-
-    // S = Q . K^T  [32 q x 32 keys]: A = Q rows (LDS), B = K rows (regs)
-    f32x16 sacc = f32x16{}, dpacc = f32x16{};
-#pragma unroll
-    for (int s = 0; s < D / 16; ++s) {
-      const V8 qa = *(const V8*)(lds_q + r * LDR + 16 * s + 8 * hl);
-      const V8 da = *(const V8*)(lds_do + r * LDR + 16 * s + 8 * hl);
-      sacc = M::mma(qa, kf[s], sacc);
-      dpacc = M::mma(da, vf[s], dpacc);
-    }
-    // element i: q = qb + (i&3) + 8(i>>2) + 4hl, key = mykey.
-    // pd = P * keep (the 1/(1-p) factor of dV is applied once, in the epilogue),
-    // ds = P * (dP * keep / (1-p) - delta) (the softmax scale of dK / dQ likewise).
-    float pd[16], ds[16];
-    const bool interior = (k0 + 32 * wid + 31 < Sk) && (qb + kBwdBQ <= nq) && (!CAUSAL || k0 + 32 * wid + 31 <= qb);
-    // exp2 is the bare v_exp_f32 (no denormal range reduction)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int qr0 = (g * 8) + 4 * hl;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int i = 4 * g + e;
-        const int qi = qr0 + e;
-        float p = __builtin_amdgcn_exp2f(fmaf(sacc[i], a.scale_log2, -lds_lse[qi]));
-        if (!interior) {
-          const int q = qb + qi;
-          const bool valid = (mykey < Sk) && (q < nq) && !(CAUSAL && mykey > q);
-          p = valid ? p : 0.f;
-        }
-        float dpv = dpacc[i];
-        float pk = p;
-        if (DROPOUT) {
-          const int m = __builtin_amdgcn_sbfe((int)lds_mask[wid * kBwdBQ + qi], r, 1);
-          pk = __builtin_bit_cast(float, __builtin_bit_cast(int, p) & m);
-          dpv = __builtin_bit_cast(float, __builtin_bit_cast(int, dpv) & m);
-        }
-        pd[i] = pk;
-        ds[i] = p * fmaf(dpv, rkeep, -lds_delta[qi]);
-      }
-    }
-    // dV += P^T . dO : accumulator-as-A (contraction over q = rows), B = dO via tr reads
-    // dK += dS^T . Q : same with Q
-#pragma unroll
-    for (int s2 = 0; s2 < 2 && !(a.dbg & 2); ++s2) {
-      const V8 pa = pack8<T, V8>(pd + 8 * s2);
-      const V8 sa = pack8<T, V8>(ds + 8 * s2);
-      const int kq = 16 * s2 + 4 * hl + ((lane & 15) >> 2);
-#pragma unroll
-      for (int db = 0; db < D / 32; ++db) {
-        const int c0 = 32 * db + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-        const V8 dob = join4<V8>(lds_tr16(lds_do + kq * LDR + c0), lds_tr16(lds_do + (kq + 8) * LDR + c0));
-        const V8 qbf = join4<V8>(lds_tr16(lds_q + kq * LDR + c0), lds_tr16(lds_q + (kq + 8) * LDR + c0));
-        dv[db] = M::mma(pa, dob, dv[db]);
-        dk[db] = M::mma(sa, qbf, dk[db]);
-      }
-    }
-    if (DQ && !(a.dbg & 1)) {
-    // dS to LDS as [q][key] (bf16) for dQ = dS . K
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int qi = (i & 3) + 8 * (i >> 2) + 4 * hl;
-      lds_ds[qi * LDS_S + 32 * wid + r] = (T)ds[i];
-    }
-    lds_barrier();
-    // dQ^T [D x 32 q] = K^T . dS^T on 16x16x32 MFMAs over the full 128-key contraction: wave
-    // w owns query tile qt = w & 1 (16 queries) and D/32 dim tiles of 16 from (w >> 1) D/32;
-    // A = K^T rows, B = dS rows (16-byte LDS reads); each lane ends with 4 consecutive dims of
-    // one query (8-byte stores). No cross-wave reduction, no scattered 2-byte stores.
-    {
-      constexpr int NT = D / 32;
-      const int qt = wid & 1, dt0 = (wid >> 1) * NT;
-      const int lq = lane & 15, lg = lane >> 4;
-      f32x4 acc[NT];
-#pragma unroll
-      for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kk = 0; kk < kBwdBK; kk += 32) {
-        const V8 bb = *(const V8*)(lds_ds + (16 * qt + lq) * LDS_S + kk + 8 * lg);
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-          const V8 aa = *(const V8*)(lds_k + ((dt0 + t) * 16 + lq) * KT_LD + kk + 8 * lg);
-          acc[t] = Mfma16T<T>::mma(aa, bb, acc[t]);
-        }
-      }
-      // this workgroup is the sole writer of these query rows (single key block): final dtype
-      const int q = qb + 16 * qt + lq;
-      if (q < nq) {
-        T* dqp = (T*)a.dq + b * a.dq_bs + h * a.dq_hs + (int64_t)q * a.dq_ss;
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-          typedef T t4 __attribute__((ext_vector_type(4)));
-          t4 w;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) w[i] = (T)(acc[t][i] * a.scale);
-          *(t4*)(dqp + (dt0 + t) * 16 + 4 * lg) = w;
-          if constexpr (DSUM) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) dqcs[t][i] += (float)w[i];
-          }
-        }
-      }
-    }
-    }  // DQ
-  };
-  if constexpr (DEPTH2) {
-    for (int qb = qstart; qb < nq; qb += 2 * kBwdBQ) {
-      body(pfa, qb);
-      if (qb + kBwdBQ < nq) body(pfb, qb + kBwdBQ);
-    }
-  } else {
-    for (int qb = qstart; qb < nq; qb += kBwdBQ) body(pfa, qb);
-  }
-  // write dK, dV: element i of block db -> key = k0 + 32wid + (i&3)+8(i>>2)+4hl, dim = 32db + r
-  T* dkp = (T*)dk_out + b * a.dk_bs + h * a.dk_hs;
-  T* dvp = (T*)dv_out + b * a.dv_bs + h * a.dv_hs;
-  // optional bias-gradient partials: column sums of the stored dq / dk / dv over positions
-  float* dsum = DSUM ? a.dsum + ((int64_t)b * 3 * a.H + h) * D : nullptr;
-  if (DSUM && DQ) {  // reduce over the 16 query lanes; both query-tile waves add their partials
-    const int lq = lane & 15, lg = lane >> 4, dt0 = (wid >> 1) * (D / 32);
-#pragma unroll
-    for (int t = 0; t < D / 32; ++t) {
-      float v[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        v[i] = dqcs[t][i];
-#pragma unroll
-        for (int o = 8; o > 0; o >>= 1) v[i] += __shfl_xor(v[i], o, 64);  // all 16 lanes hold the sum
-      }
-      // lane lq < 4 of each group adds dim 4 lg + lq: one atomic instruction (16 lanes) per tile
-      // (atomics cost per instruction, so 4 single-lane instructions would cost 4x)
-      const float x = lq == 0 ? v[0] : lq == 1 ? v[1] : lq == 2 ? v[2] : v[3];
-      if (lq < 4) atomicAdd(dsum + (dt0 + t) * 16 + 4 * lg + lq, x);
-    }
-  }
-  // dK then dV staged through LDS ([key][D] rows in lds_k) so the global stores are 16-byte
-  // row chunks (4 per thread at D = 64) instead of 2-byte column scatters (32 per lane)
-  lds_barrier();  // every wave is done reading lds_k (dQ products)
-  auto emit = [&](const f32x16 (&acc)[D / 32], const float mul, T* dst, const int64_t ss, float* dsum_t) {
-#pragma unroll
-    for (int db = 0; db < D / 32; ++db) {
-      float sum = 0.f;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int kl = 32 * wid + (i & 3) + 8 * (i >> 2) + 4 * hl;
-        const T v = (T)(acc[db][i] * mul);
-        lds_k[kl * LDR + 32 * db + r] = v;
-        if constexpr (DSUM) sum += (k0 + kl < a.Sk) ? (float)v : 0.f;
-      }
-      if constexpr (DSUM) {
-        sum += __shfl_xor(sum, 32, 64);
-        if (hl == 0) atomicAdd(dsum_t + 32 * db + r, sum);
-      }
-    }
-    lds_barrier();
-    for (int idx = threadIdx.x; idx < kBwdBK * (D / 8); idx += 256) {
-      const int row = idx / (D / 8), col = (idx % (D / 8)) * 8;
-      if (k0 + row < a.Sk) *(uint4*)(dst + (int64_t)(k0 + row) * ss + col) = *(const uint4*)(lds_k + row * LDR + col);
-    }
-    lds_barrier();
-  };
-  emit(dk, a.scale, dkp, a.dk_ss, DSUM ? dsum + (int64_t)a.H * D : nullptr);
-  emit(dv, rkeep, dvp, a.dv_ss, DSUM ? dsum + (int64_t)2 * a.H * D : nullptr);
-}
-
-// dQ for key ranges longer than one backward key block: query-stationary, the forward's
-// structure (one workgroup = 4 waves x 32 query rows, K/V streamed in 64-key tiles):
-//   S^T = K . Q^T and dP^T = V . dO^T (32x32x16, one query per lane, so lse and delta are
-//   lane-local scalars), dS^T = P^T * (dP^T * keep - delta) in registers, and
-//   dQ^T += K^T . dS^T with the dS^T accumulators reused directly as the B operand (the same
-//   register reuse as O^T += V^T . P^T in the forward). Every dQ row has exactly one writer:
-//   no fp32 atomics, no accumulator buffer, no conversion pass. The extra S / dP products (vs
-//   the fused single-kernel backward) cost less than the fp32 atomic traffic they replace.
-template <typename T, int D, bool CAUSAL, bool DROPOUT, bool DSUM>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 64 ? 2 : 1, D == 64 ? 2 : 1))) attn_bwd_dq_kernel(AttnArgs a, const void* dout, const float* delta_in) {
-  using M = MfmaT<T>;
-  using V8 = typename M::V8;
-  constexpr int LDR = D + 8;
-  __shared__ __attribute__((aligned(16))) T lds_k[kFwdKB * LDR];
-  __shared__ __attribute__((aligned(16))) T lds_v[kFwdKB * LDR];
-
-  // wid through readfirstlane: wave-uniform in SGPRs, so tile-level conditions become scalar branches
-  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int r = lane & 31, hl = lane >> 5;
-  const int bh = blockIdx.y;
-  const int b = bh / a.H, h = bh % a.H;
-  const int q0 = blockIdx.x * kFwdBQ;
-  const int qrow = q0 + 32 * wid + r;
-  const int Sk = a.k_lens ? min(a.k_lens[b], a.Sk) : a.Sk;
-
-  const T* qp = (const T*)a.q + b * a.q_bs + h * a.q_hs;
-  const T* dop = (const T*)dout + b * a.do_bs + h * a.do_hs;
-  const T* kp = (const T*)a.k + b * a.k_bs + h * a.k_hs;
-  const T* vp = (const T*)a.v + b * a.v_bs + h * a.v_hs;
-
-  // Q^T and dO^T fragments (B operands): lane (q=r, hl) holds X[q][16s + 8hl .. +7]
-  V8 qf[D / 16], df[D / 16];
-#pragma unroll
-  for (int s = 0; s < D / 16; ++s) {
-    if (qrow < a.Sq) {
-      qf[s] = *(const V8*)(qp + (int64_t)qrow * a.q_ss + 16 * s + 8 * hl);
-      df[s] = *(const V8*)(dop + (int64_t)qrow * a.do_ss + 16 * s + 8 * hl);
-    } else {
-      qf[s] = V8{};
-      df[s] = V8{};
-    }
-  }
-  // log2-domain lse (+inf for padding rows and fully masked rows: P = 0) and delta
-  const float lse2 = qrow < a.Sq ? a.lse[(int64_t)bh * a.Sq + qrow] * kLog2e : INFINITY;
-  const float delta = qrow < a.Sq ? delta_in[(int64_t)bh * a.Sq + qrow] : 0.f;
-
-  f32x16 dq[D / 32];
-#pragma unroll
-  for (int i = 0; i < D / 32; ++i) dq[i] = f32x16{};
-
-  int kend = Sk;
-  if (CAUSAL) kend = min(kend, q0 + kFwdBQ);
-  const int ntiles = (kend + kFwdKB - 1) / kFwdKB;
-
-  constexpr int CPR = D / 8;
-  constexpr int CH = kFwdKB * CPR / 256;
-  // K/V tiles of the tile TWO ahead are loaded into registers while the current tile computes
-  // (two register sets, loop unrolled by two) at D = 64; one ahead at D = 128 (register budget)
-  constexpr bool KV2 = D == 64;
-  constexpr int AHEAD = KV2 ? 2 : 1;
-  struct KV {
-    uint4 k[CH], v[CH];
-    uint32_t m[2];
-  };
-  KV kva, kvb;
-  const uint32_t* mrow =
-      DROPOUT && qrow < a.Sq ? (const uint32_t*)(a.dmask + ((int64_t)bh * a.Sq + qrow) * a.mask_words) : nullptr;
-  auto gload = [&](KV& R, int kt) {
-    uint4 (&kreg)[CH] = R.k;
-    uint4 (&vreg)[CH] = R.v;
-#pragma unroll
-    for (int c = 0; c < CH; ++c) {
-      const int idx = threadIdx.x + 256 * c;
-      const int row = idx / CPR, col = (idx % CPR) * 8;
-      const int key = kt * kFwdKB + row;
-      if (key < Sk) {
-        kreg[c] = *(const uint4*)(kp + (int64_t)key * a.k_ss + col);
-        vreg[c] = *(const uint4*)(vp + (int64_t)key * a.v_ss + col);
-      } else {
-        kreg[c] = make_uint4(0, 0, 0, 0);
-        vreg[c] = make_uint4(0, 0, 0, 0);
-      }
-    }
-    if (DROPOUT) {
-      // the forward's keep bits for this lane's 16 keys of each 32-key block (same layout)
-#pragma unroll
-      for (int sb = 0; sb < 2; ++sb) {
-        const int blk = (kt * kFwdKB >> 5) + sb;
-        R.m[sb] = 0u;
-        if (mrow && blk * 32 < a.Sk) R.m[sb] = mrow[blk];  // raw: shifted at use (no wait here)
-      }
-    }
-  };
-  auto lstore = [&](KV& R) {
-    uint4 (&kreg)[CH] = R.k;
-    uint4 (&vreg)[CH] = R.v;
-#pragma unroll
-    for (int c = 0; c < CH; ++c) {
-      const int idx = threadIdx.x + 256 * c;
-      const int row = idx / CPR, col = (idx % CPR) * 8;
-      *(uint4*)(lds_k + row * LDR + col) = kreg[c];
-      *(uint4*)(lds_v + row * LDR + col) = vreg[c];
-    }
-  };
-
-  const float rkeep = a.drop_scale;
-  if (ntiles > 0) gload(kva, 0);
-  if (KV2 && ntiles > 1) gload(kvb, 1);
-  auto tile = [&](KV& R, const int kt) {
-    lds_barrier();  // previous tile fully consumed
-    lstore(R);
-    const uint32_t mcur[2] = {R.m[0] >> (4 * hl), R.m[1] >> (4 * hl)};
-    lds_barrier();
-    if (kt + AHEAD < ntiles) gload(R, kt + AHEAD);
-    const int kb = kt * kFwdKB;
-
-    f32x16 st[2], dpt[2];
-#pragma unroll
-    for (int sb = 0; sb < 2; ++sb) {
-      V8 kf[D / 16], vf[D / 16];
-#pragma unroll
-      for (int s = 0; s < D / 16; ++s) {
-        kf[s] = *(const V8*)(lds_k + (32 * sb + r) * LDR + 16 * s + 8 * hl);
-        vf[s] = *(const V8*)(lds_v + (32 * sb + r) * LDR + 16 * s + 8 * hl);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x100, 2 * (D / 16), 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 2 * (D / 16), 0);
-      st[sb] = f32x16{};
-      dpt[sb] = f32x16{};
-#pragma unroll
-      for (int s = 0; s < D / 16; ++s) {
-        st[sb] = M::mma(kf[s], qf[s], st[sb]);
-        dpt[sb] = M::mma(vf[s], df[s], dpt[sb]);
-      }
-    }
-    const bool interior = (kb + kFwdKB <= Sk) && (!CAUSAL || kb + kFwdKB - 1 <= q0 + 32 * wid);
-    const int lim = CAUSAL ? min(Sk, qrow + 1) : Sk;
-#pragma unroll
-    for (int sb = 0; sb < 2; ++sb) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        float p = __builtin_amdgcn_exp2f(fmaf(st[sb][i], a.scale_log2, -lse2));
-        if (!interior) {
-          const int key = kb + 32 * sb + (i & 3) + 8 * (i >> 2) + 4 * hl;
-          if (key >= lim) p = 0.f;
-        }
-        float dp = dpt[sb][i];
-        if (DROPOUT)
-          dp = __builtin_bit_cast(float, __builtin_bit_cast(int, dp) & __builtin_amdgcn_sbfe((int)mcur[sb], (i & 3) + 8 * (i >> 2), 1));
-        st[sb][i] = p * fmaf(dp, rkeep, -delta);  // dS^T (the softmax scale is applied once, at the end)
-      }
-    }
-    // dQ^T += K^T . dS^T
-#pragma unroll
-    for (int sb = 0; sb < 2; ++sb) {
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        float sv[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) sv[j] = st[sb][8 * s2 + j];
-        const V8 sf = pack8<T, V8>(sv);
-        const int k0 = 32 * sb + 16 * s2 + 4 * hl + ((lane & 15) >> 2);
-#pragma unroll
-        for (int db = 0; db < D / 32; ++db) {
-          const int c0 = 32 * db + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-          const s16x4 lo = lds_tr16(lds_k + k0 * LDR + c0);
-          const s16x4 hi = lds_tr16(lds_k + (k0 + 8) * LDR + c0);
-          dq[db] = M::mma(join4<V8>(lo, hi), sf, dq[db]);
-        }
-      }
-    }
-  };
-  if constexpr (KV2) {
-    for (int kt = 0; kt < ntiles; kt += 2) {
-      tile(kva, kt);
-      if (kt + 1 < ntiles) tile(kvb, kt + 1);
-    }
-  } else {
-    for (int kt = 0; kt < ntiles; ++kt) tile(kva, kt);
-  }
-  // ---- epilogue: element 4g+e of block db -> dim 32db + 8g + 4hl + e of query qrow
-  float* dsum = DSUM ? a.dsum + ((int64_t)b * 3 * a.H + h) * D : nullptr;
-#pragma unroll
-  for (int db = 0; db < D / 32; ++db) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      typedef T t4 __attribute__((ext_vector_type(4)));
-      t4 w;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) w[e] = (T)(dq[db][4 * g + e] * a.scale);
-      if (qrow < a.Sq)
-        *(t4*)((T*)a.dq + b * a.dq_bs + h * a.dq_hs + (int64_t)qrow * a.dq_ss + 32 * db + 8 * g + 4 * hl) = w;
-      if constexpr (DSUM) {
-        // column sums of the stored values over this wave's 32 query rows (lanes r), then one
-        // atomic per dim per wave
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float t = qrow < a.Sq ? (float)w[e] : 0.f;
-#pragma unroll
-          for (int o = 16; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
-          if (r == 0) atomicAdd(dsum + 32 * db + 8 * g + 4 * hl + e, t);
-        }
-      }
-    }
-  }
-}
 
 // debug / test: materialise the keep-mask the kernels use (uint8 [B*H, Sq, Sk])
 __global__ void attn_dropout_mask_kernel(uint8_t* out, int64_t BH, int Sq, int Sk, uint64_t seed,
@@ -949,38 +30,17 @@ int attn_dropout_mask(uint8_t* out, int64_t BH, int Sq, int Sk, uint64_t seed, u
   return (int)hipGetLastError();
 }
 
-#define ATTN_DISPATCH(DT, T, ...)                         \
-  switch (DT) {                                             \
-    case kF16: { using T = f16; __VA_ARGS__; } break;       \
-    case kBF16: { using T = bf16; __VA_ARGS__; } break;     \
-    default: return -1;                                     \
-  }
-#define ATTN_DISPATCH_D(DD, D, ...)                         \
-  switch (DD) {                                             \
-    case 64: { constexpr int D = 64; __VA_ARGS__; } break;  \
-    case 128: { constexpr int D = 128; __VA_ARGS__; } break;\
-    default: return -1;                                     \
-  }
-#define ATTN_DISPATCH_B(X, NAME, ...)                       \
-  if (X) { constexpr bool NAME = true; __VA_ARGS__; }       \
-  else { constexpr bool NAME = false; __VA_ARGS__; }
 
 int attn_fwd(const AttnArgs& a, int dt, hipStream_t s) {
   if (a.B * a.H == 0 || a.Sq == 0) return 0;
-  dim3 grid((a.Sq + kFwdBQ - 1) / kFwdBQ, a.B * a.H);
-  const bool drop = a.drop_thresh > 0;
-  if (drop && !a.dmask) return -3;
-  // SHORT: single LDS stage (k_lens <= Sk). Without dropout only: measured at the BERT shape
-  // (tools/attn_bench.py, b256 s128 h16) p = 0 fwd 61.1 -> 56.1 us, but p = 0.1 72.7 -> 73.8 us:
-  // with dropout the kernel is bound by the Philox integer multiplies, not by load latency.
-  if (a.D == 64 && a.Sk <= 2 * kFwdKB && !drop) {
-    ATTN_DISPATCH(dt, T, ATTN_DISPATCH_B(a.causal, C,
-        hipLaunchKernelGGL((attn_fwd_kernel<T, 64, C, false, true>), grid, dim3(256), 0, s, a)));
-  } else {
-    ATTN_DISPATCH(dt, T, ATTN_DISPATCH_D(a.D, D, ATTN_DISPATCH_B(a.causal, C, ATTN_DISPATCH_B(drop, DR,
-        hipLaunchKernelGGL((attn_fwd_kernel<T, D, C, DR, false>), grid, dim3(256), 0, s, a)))));
+  if (a.drop_thresh > 0 && !a.dmask) return -3;
+  switch (a.D) {
+    case 32: return attn_fwd_d32(a, dt, s);
+    case 64: return attn_fwd_d64(a, dt, s);
+    case 128: return attn_fwd_d128(a, dt, s);
+    case 256: return attn_fwd_d256(a, dt, s);
+    default: return -1;
   }
-  return (int)hipGetLastError();
 }
 
 bool attn_bwd_needs_dq_acc(const AttnArgs& a) { return a.Sk > kBwdBK; }
@@ -988,26 +48,14 @@ bool attn_bwd_needs_dq_acc(const AttnArgs& a) { return a.Sk > kBwdBK; }
 int attn_bwd(const AttnArgs& a, const void* dout, float* delta_ws, void* dk, void* dv, int dt,
              hipStream_t s) {
   if (a.B * a.H == 0 || a.Sq == 0) return 0;
-  const bool drop = a.drop_thresh > 0;
-  if (drop && !a.dmask) return -3;  // backward needs the forward's dropout bits
-  const bool multi = attn_bwd_needs_dq_acc(a);
-  if (multi && !delta_ws) return -4;
-  ATTN_DISPATCH(dt, T, ATTN_DISPATCH_D(a.D, D, {
-    dim3 grid((a.Sk + kBwdBK - 1) / kBwdBK, a.B * a.H);
-    ATTN_DISPATCH_B(a.causal, C, ATTN_DISPATCH_B(drop, DR, ATTN_DISPATCH_B(a.dsum != nullptr, DS, {
-      if (multi) {
-        hipLaunchKernelGGL((attn_bwd_kernel<T, D, C, DR, DS, false>), grid, dim3(256), 0, s, a, dout, delta_ws, dk,
-                           dv);
-        dim3 qgrid((a.Sq + kFwdBQ - 1) / kFwdBQ, a.B * a.H);
-        hipLaunchKernelGGL((attn_bwd_dq_kernel<T, D, C, DR, DS>), qgrid, dim3(256), 0, s, a, dout,
-                           (const float*)delta_ws);
-      } else {
-        hipLaunchKernelGGL((attn_bwd_kernel<T, D, C, DR, DS, true>), grid, dim3(256), 0, s, a, dout, nullptr, dk,
-                           dv);
-      }
-    })));
-  }));
-  return (int)hipGetLastError();
+  if (a.drop_thresh > 0 && !a.dmask) return -3;  // backward needs the forward's dropout bits
+  switch (a.D) {
+    case 32: return attn_bwd_d32(a, dout, delta_ws, dk, dv, dt, s);
+    case 64: return attn_bwd_d64(a, dout, delta_ws, dk, dv, dt, s);
+    case 128: return attn_bwd_d128(a, dout, delta_ws, dk, dv, dt, s);
+    case 256: return attn_bwd_d256(a, dout, delta_ws, dk, dv, dt, s);
+    default: return -1;
+  }
 }
 
 }  // namespace apex

@@ -321,7 +321,8 @@ apex::AttnArgs attn_common(const Tensor& q, const Tensor& k, const Tensor& v, bo
   a.Sk = (int)k.size(1);
   TORCH_CHECK(k.size(0) == a.B && k.size(2) == a.H && k.size(3) == a.D && v.sizes() == k.sizes(),
               "k/v shape mismatch");
-  TORCH_CHECK(a.D == 64 || a.D == 128, "flash attention supports head dim 64 or 128");
+  TORCH_CHECK(a.D == 32 || a.D == 64 || a.D == 128 || a.D == 256,
+              "flash attention supports head dims 32, 64, 128, 256 (pad others)");
   a.causal = causal;
   a.scale = (float)scale;
   a.scale_log2 = (float)(scale * 1.4426950408889634);
@@ -339,10 +340,29 @@ apex::AttnArgs attn_common(const Tensor& q, const Tensor& k, const Tensor& v, bo
   return a;
 }
 
+// optional additive score bias: a [B|1, H|1, Sq|1, Sk] view (broadcast dims stride 0) in q's dtype,
+// key stride 1, 8-byte aligned rows
+void attn_set_bias(apex::AttnArgs& a, const c10::optional<Tensor>& bias, const Tensor& q) {
+  if (!bias.has_value() || !bias->defined()) return;
+  const Tensor& t = *bias;
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == q.scalar_type(), "attention bias must be a device tensor in q's dtype");
+  TORCH_CHECK(t.dim() == 4 && t.size(3) == a.Sk && t.stride(3) == 1, "attention bias must be [B|1, H|1, Sq|1, Sk], key-contiguous");
+  TORCH_CHECK((t.size(0) == a.B || t.stride(0) == 0 || t.size(0) == 1) && (t.size(1) == a.H || t.size(1) == 1 || t.stride(1) == 0) &&
+                  (t.size(2) == a.Sq || t.size(2) == 1 || t.stride(2) == 0),
+              "attention bias does not broadcast to [B, H, Sq, Sk]");
+  TORCH_CHECK(((uintptr_t)t.data_ptr() & 7) == 0 && t.stride(2) % 4 == 0 && t.stride(1) % 4 == 0 && t.stride(0) % 4 == 0,
+              "attention bias rows must be 8-byte aligned");
+  a.bias = t.data_ptr();
+  a.bias_bs = t.size(0) == 1 ? 0 : t.stride(0);
+  a.bias_hs = t.size(1) == 1 ? 0 : t.stride(1);
+  a.bias_qs = t.size(2) == 1 ? 0 : t.stride(2);
+}
+
 std::vector<Tensor> flash_attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, double scale,
                                    double p_drop, int64_t seed, int64_t offset,
-                                   const c10::optional<Tensor>& k_lens) {
+                                   const c10::optional<Tensor>& k_lens, const c10::optional<Tensor>& bias) {
   apex::AttnArgs a = attn_common(q, k, v, causal, scale, p_drop, seed, offset, k_lens);
+  attn_set_bias(a, bias, q);
   Tensor o = at::empty({a.B, a.Sq, a.H, a.D}, q.options());
   Tensor lse = at::empty({a.B, a.H, a.Sq}, q.options().dtype(at::kFloat));
   a.o = o.data_ptr();
@@ -363,9 +383,12 @@ std::vector<Tensor> flash_attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, do
 void flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor dq,
                     Tensor dk, Tensor dv, bool causal, double scale, double p_drop, int64_t seed,
                     int64_t offset, const c10::optional<Tensor>& k_lens,
-                    const c10::optional<Tensor>& dmask, const c10::optional<Tensor>& dsum, int64_t dbg) {
+                    const c10::optional<Tensor>& dmask, const c10::optional<Tensor>& dsum, int64_t dbg,
+                    const c10::optional<Tensor>& bias) {
   apex::AttnArgs a = attn_common(q, k, v, causal, scale, p_drop, seed, offset, k_lens);
   a.dbg = (int)dbg;
+  attn_set_bias(a, bias, q);
+  TORCH_CHECK(!(a.bias && dsum.has_value() && dsum->defined()), "flash_attn_bwd: dsum with a score bias is not supported");
   if (dsum.has_value() && dsum->defined()) {
     TORCH_CHECK(dsum->is_cuda() && dsum->scalar_type() == at::kFloat && dsum->is_contiguous() &&
                     dsum->numel() == (int64_t)a.B * 3 * a.H * a.D,
@@ -925,12 +948,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ln_bwd", &ln_bwd);
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd", &xent_bwd);
-  m.def("flash_attn_fwd", &flash_attn_fwd);
+  m.def("flash_attn_fwd", &flash_attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("causal"),
+        py::arg("scale"), py::arg("p_drop"), py::arg("seed"), py::arg("offset"), py::arg("k_lens"),
+        py::arg("bias") = py::none());
   m.def("gemm_set_dbg", [](int64_t v) { check(apex::gemm_set_dbg((int)v), "gemm_set_dbg"); });
   m.def("flash_attn_bwd", &flash_attn_bwd, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"),
         py::arg("o"), py::arg("lse"), py::arg("dq"), py::arg("dk"), py::arg("dv"), py::arg("causal"),
         py::arg("scale"), py::arg("p_drop"), py::arg("seed"), py::arg("offset"), py::arg("k_lens"),
-        py::arg("dmask"), py::arg("dsum") = py::none(), py::arg("dbg") = 0);
+        py::arg("dmask"), py::arg("dsum") = py::none(), py::arg("dbg") = 0, py::arg("bias") = py::none());
   m.def("partial_colsum", &k_partial_colsum);
   m.def("flash_dropout_mask", &flash_dropout_mask);
   m.def("weight_norm_fwd", &k_wn_fwd);

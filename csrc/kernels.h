@@ -99,6 +99,8 @@ struct AttnArgs {
   int dbg;               // diagnostics only (tools/attn_bench.py --dbg): bits skip backward sections
   float* dsum;           // optional, zeroed [B][3][H][D]: bwd adds the column sums (over positions)
                          // of dq, dk, dv — the packed-QKV projection's bias gradient, per batch
+  const void* bias;      // optional additive score bias (input dtype), element (b, h, q, key) at
+  int64_t bias_bs, bias_hs, bias_qs;  // b*bias_bs + h*bias_hs + q*bias_qs + key (0 = broadcast)
 };
 inline uint32_t attn_drop_thresh(double p) {  // 8-bit keep threshold in [1, 255], 0 = off
   if (p <= 0.0) return 0u;
