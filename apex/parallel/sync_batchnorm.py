@@ -88,15 +88,16 @@ class SyncBatchnormFunction(torch.autograd.Function):
             if fuse_relu:
                 y = torch.relu(y)
             y = y.to(x.dtype)
-        ctx.save_for_backward(x, weight, mean, invstd, y if fuse_relu else None)
-        ctx.cfg = (group, channel_last, fuse_relu, float(count[0]) if count.numel() else 1.0, native,
-                   bias is not None)
+        # the global count stays on the device (a float(count) here was one host round trip per
+        # BatchNorm layer per forward)
+        ctx.save_for_backward(x, weight, mean, invstd, y if fuse_relu else None, count)
+        ctx.cfg = (group, channel_last, fuse_relu, native, bias is not None)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, weight, mean, invstd, y = ctx.saved_tensors
-        group, channel_last, fuse_relu, total, native, has_bias = ctx.cfg
+        x, weight, mean, invstd, y, count = ctx.saved_tensors
+        group, channel_last, fuse_relu, native, has_bias = ctx.cfg
         dy = dy.contiguous()
         if fuse_relu:
             dy = dy * (y > 0).to(dy.dtype)
@@ -113,9 +114,10 @@ class SyncBatchnormFunction(torch.autograd.Function):
         dw = (sums[1] * invstd).to(weight.dtype) if weight is not None and ctx.needs_input_grad[1] else None
         db = sums[0].to(weight.dtype) if has_bias and ctx.needs_input_grad[2] else None
         if native:
-            dx = C.bn_bwd_elemt(dy, x, mean, invstd, weight, sums, total, channel_last)
+            dx = C.bn_bwd_elemt(dy, x, mean, invstd, weight, sums, count.contiguous(), channel_last)
         else:
             sh = _bshape(x, channel_last)
+            total = count.clamp(min=1)
             mdy = (sums[0] / total).view(sh)
             mdx = (sums[1] / total).view(sh)
             xm = x.float() - mean.view(sh)

@@ -26,12 +26,12 @@ def main():
     ap.add_argument("--size", default="1.5b", choices=["1.5b", "medium", "tiny"])
     args = ap.parse_args()
 
-    from apex.utils.bench import emit, finish, init_distributed, time_steps
+    from apex.utils.bench import emit, finish, init_distributed, instrumented_steps
     from apex.utils.gemm_tuning import enable_tuned_gemms
 
     enable_tuned_gemms()
 
-    env = init_distributed()
+    env = init_distributed(single_rank_group=True)  # apex DDP at every N (hooks + buckets timed at N=1 too)
     import apex
     from apex import amp
     from apex.models.gpt import GPTConfig, GPTModel, param_groups, synthetic_batch
@@ -44,8 +44,7 @@ def main():
     model = GPTModel(cfg).to(env.device)
     opt = FusedAdam(param_groups(model, 0.1), lr=1.5e-4, betas=(0.9, 0.95), eps=1e-8)
     model, opt = amp.initialize(model, opt, opt_level="O2", cast_model_type=torch.bfloat16, verbosity=0)
-    if env.world > 1:
-        model = DDP(model, message_size=int(os.environ.get("APEX_DDP_MESSAGE_SIZE", 25_000_000)))
+    model = DDP(model, message_size=int(os.environ.get("APEX_DDP_MESSAGE_SIZE", 25_000_000)), comm_timing=True)
     g = torch.Generator(device=env.device).manual_seed(1 + env.rank)
     batches = [synthetic_batch(cfg, args.batch, args.seq, device=env.device, generator=g) for _ in range(2)]
 
@@ -57,15 +56,15 @@ def main():
         opt.zero_grad()
         return loss
 
-    elapsed, loss = time_steps(env, step, args.steps, args.warmup)
-    nparams = sum(p.numel() for p in (model.module if env.world > 1 else model).parameters())
+    elapsed, loss, extra = instrumented_steps(env, step, args.steps, args.warmup, ddp=model)
+    nparams = sum(p.numel() for p in model.module.parameters())
     emit(env, metric="tokens/s GPT-2 1.5B fused multihead_attn + xentropy, amp-O2 bf16 + FusedAdam, DDP",
          items_per_step=args.batch * args.seq * env.world, unit="tokens/s", steps=args.steps,
          warmup=args.warmup, elapsed=elapsed, dtype="bf16", data="synthetic token ids; random-init weights",
          config={"model": f"GPT-2 {args.size} ({cfg.n_layer}L, H{cfg.n_embd}, {cfg.n_head} heads, "
                           f"{nparams / 1e9:.2f}B params)",
                  "global_batch": args.batch * env.world, "seq_len": args.seq, "parallelism": f"dp{env.world}"},
-         extra={"final_loss": round(float(loss), 4)})
+         extra=dict(extra, final_loss=round(float(loss), 4)))
     finish(env)
 
 

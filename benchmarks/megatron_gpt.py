@@ -34,7 +34,7 @@ def main():
 
     enable_tuned_gemms()
 
-    env = init_distributed()
+    env = init_distributed(single_rank_group=True)  # parallel_state needs a process group at N=1 too
     import torch.distributed as dist
 
     import apex
@@ -50,9 +50,6 @@ def main():
     apex._ext.require()
     if env.world == 1:
         args.tp = args.pp = 1
-    if not dist.is_initialized():  # 1 GPU: a trivial group keeps parallel_state uniform
-        dist.init_process_group("nccl", init_method="tcp://127.0.0.1:29533", rank=0, world_size=1,
-                                device_id=env.device)
     ps.initialize_model_parallel(args.tp, args.pp)
     dp = ps.get_data_parallel_world_size()
     setup_microbatch_calculator(env.rank, None, args.global_batch, args.micro_batch, dp)

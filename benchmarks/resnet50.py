@@ -28,9 +28,9 @@ def main():
     ap.add_argument("--fp32", action="store_true")
     args = ap.parse_args()
 
-    from apex.utils.bench import emit, finish, init_distributed, time_steps
+    from apex.utils.bench import emit, finish, init_distributed, instrumented_steps
 
-    env = init_distributed()
+    env = init_distributed(single_rank_group=True)  # apex DDP at every N (hooks + buckets timed at N=1 too)
     import apex
     from apex import amp
     from apex.models.resnet import resnet50, synthetic_batch
@@ -50,8 +50,7 @@ def main():
         model, opt = amp.initialize(model, opt, opt_level="O0", verbosity=0)
     else:
         model, opt = amp.initialize(model, opt, opt_level="O2", cast_model_type=torch.bfloat16, verbosity=0)
-    if env.world > 1:
-        model = DDP(model, message_size=int(os.environ.get("APEX_DDP_MESSAGE_SIZE", 25_000_000)))
+    model = DDP(model, message_size=int(os.environ.get("APEX_DDP_MESSAGE_SIZE", 25_000_000)), comm_timing=True)
     g = torch.Generator(device=env.device).manual_seed(1 + env.rank)
     dt = torch.float32 if args.fp32 else torch.bfloat16
     batches = [synthetic_batch(args.batch, args.image_size, device=env.device, dtype=dt, channels_last=cl,
@@ -66,14 +65,14 @@ def main():
         opt.zero_grad()
         return loss
 
-    elapsed, loss = time_steps(env, step, args.steps, args.warmup)
+    elapsed, loss, extra = instrumented_steps(env, step, args.steps, args.warmup, ddp=model)
     emit(env, metric="img/s ResNet-50 amp-O2 bf16 + FusedSGD + SyncBatchNorm", items_per_step=args.batch * env.world,
          unit="img/s", steps=args.steps, warmup=args.warmup, elapsed=elapsed,
          dtype="fp32" if args.fp32 else "bf16", data="synthetic normalised images; random-init weights",
          config={"model": "ResNet-50", "global_batch": args.batch * env.world, "image_size": args.image_size,
                  "parallelism": f"dp{env.world}", "syncbn": not args.no_syncbn,
                  "memory_format": "channels_last" if cl else "nchw"},
-         extra={"final_loss": round(float(loss), 4)})
+         extra=dict(extra, final_loss=round(float(loss), 4)))
     finish(env)
 
 

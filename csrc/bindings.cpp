@@ -699,15 +699,17 @@ Tensor k_bn_bwd_reduce(Tensor dy, Tensor x, Tensor mean, bool nhwc) {
 }
 
 Tensor k_bn_bwd_elemt(Tensor dy, Tensor x, Tensor mean, Tensor invstd, const c10::optional<Tensor>& w,
-                      Tensor sums, double total_count, bool nhwc) {
+                      Tensor sums, Tensor count, bool nhwc) {
   auto d = bn_dims(x, nhwc);
+  TORCH_CHECK(count.is_cuda() && count.scalar_type() == at::kFloat && count.numel() == d[1] && count.is_contiguous(),
+              "bn_bwd_elemt: count must be the fp32 [C] device tensor from bn_combine");
   Tensor dyc = dy.contiguous();
   Tensor dx = at::empty_like(x);
   Tensor sc = sums.contiguous();
   const int wdt = w.has_value() && w->defined() ? dt_code(w->scalar_type()) : apex::kF32Code;
   check(apex::bn_bwd_elemt(dyc.data_ptr(), x.data_ptr(), mean.data_ptr<float>(), invstd.data_ptr<float>(),
                            opt_vptr(w), sc.data_ptr<float>(), sc.data_ptr<float>() + d[1],
-                           (float)(1.0 / total_count), dx.data_ptr(), d[0], d[1], d[2], nhwc,
+                           count.data_ptr<float>(), dx.data_ptr(), d[0], d[1], d[2], nhwc,
                            dt_code(x.scalar_type()), wdt, cur_stream()),
         "bn_bwd_elemt");
   return dx;

@@ -164,7 +164,7 @@ int bn_elemt(const void* x, const float* mean, const float* invstd, const void* 
 int bn_bwd_reduce(const void* dy, const void* x, const float* mean, float* part, float* sum_dy,
                   float* sum_dy_xmu, int64_t N, int64_t C, int64_t S, int nhwc, int dt, hipStream_t s);
 int bn_bwd_elemt(const void* dy, const void* x, const float* mean, const float* invstd, const void* w,
-                 const float* sum_dy, const float* sum_dy_xmu, float inv_count, void* dx, int64_t N, int64_t C,
+                 const float* sum_dy, const float* sum_dy_xmu, const float* count, void* dx, int64_t N, int64_t C,
                  int64_t S, int nhwc, int dt, int wdt, hipStream_t s);
 
 // ----------------------------- fused scale-mask softmax --------------------

@@ -401,19 +401,22 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int split
   sum_dy_xmu[c] = b;
 }
 
-// dx = (dy - mean_dy - (x-mean)*invstd^2*mean_dy_xmu) * invstd * w ; count = global element count
+// dx = (dy - mean_dy - (x-mean)*invstd^2*mean_dy_xmu) * invstd * w ; count[c] = global element count
+// of channel c, read on the device (the combine kernel's output: no host round trip per layer)
 template <typename T, typename W>
 __global__ void __launch_bounds__(256) bn_bwd_elemt_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                           const float* __restrict__ mean,
                                                           const float* __restrict__ invstd,
                                                           const W* __restrict__ w, const float* __restrict__ sum_dy,
-                                                          const float* __restrict__ sum_dy_xmu, float inv_count,
+                                                          const float* __restrict__ sum_dy_xmu,
+                                                          const float* __restrict__ count,
                                                           T* __restrict__ dx, int64_t N, int64_t C, int64_t S,
                                                           int nhwc) {
   const int64_t total = N * C * S;
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
     const int64_t c = nhwc ? e % C : (e / S) % C;
     const float is = invstd[c];
+    const float inv_count = 1.f / fmaxf(count[c], 1.f);
     const float mdy = sum_dy[c] * inv_count, mdx = sum_dy_xmu[c] * inv_count;
     const float xm = to_f(x[e]) - mean[c];
     float v = (to_f(dy[e]) - mdy - xm * is * is * mdx) * is;
@@ -478,7 +481,7 @@ int bn_bwd_reduce(const void* dy, const void* x, const float* mean, float* part,
 }
 
 int bn_bwd_elemt(const void* dy, const void* x, const float* mean, const float* invstd, const void* w,
-                 const float* sum_dy, const float* sum_dy_xmu, float inv_count, void* dx, int64_t N, int64_t C,
+                 const float* sum_dy, const float* sum_dy_xmu, const float* count, void* dx, int64_t N, int64_t C,
                  int64_t S, int nhwc, int dt, int wdt, hipStream_t s) {
   const int64_t total = N * C * S;
   if (total == 0) return 0;
@@ -486,7 +489,7 @@ int bn_bwd_elemt(const void* dy, const void* x, const float* mean, const float* 
   if (!w) wdt = kF32;
   NM_DISPATCH(dt, T, NM_DISPATCH(wdt, W,
       hipLaunchKernelGGL((bn_bwd_elemt_kernel<T, W>), dim3((unsigned)grid), dim3(256), 0, s, (const T*)dy,
-                         (const T*)x, mean, invstd, (const W*)w, sum_dy, sum_dy_xmu, inv_count, (T*)dx, N, C,
+                         (const T*)x, mean, invstd, (const W*)w, sum_dy, sum_dy_xmu, count, (T*)dx, N, C,
                          S, nhwc)));
   return (int)hipGetLastError();
 }
