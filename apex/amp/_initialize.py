@@ -146,6 +146,10 @@ def _patch_step(optimizer):
         for scaler in _amp_state.loss_scalers:
             scaler._post_step_pending = True
         _post_step_scalers(self)
+        if getattr(_amp_state, "fp8", False):
+            from .. import fp8 as _fp8
+
+            _fp8.step()  # fold this step's amaxes into the scales; drop the cached fp8 weights
         return retval
 
     optimizer.step = types.MethodType(new_step, optimizer)

@@ -147,9 +147,14 @@ opt_levels = {"O3": O3(), "O2": O2(), "O1": O1(), "O0": O0()}
 def initialize(models, optimizers=None, enabled=True, opt_level="O1", cast_model_type=None,
                patch_torch_functions=None, keep_batchnorm_fp32=None, master_weights=None,
                loss_scale=None, cast_model_outputs=None, num_losses=1, verbosity=1,
-               min_loss_scale=None, max_loss_scale=2.0 ** 24, half_dtype=None):
+               min_loss_scale=None, max_loss_scale=2.0 ** 24, half_dtype=None, fp8=False):
     """Configure models/optimizers for mixed precision. Returns (models, optimizers)
-    with the same structure that was passed in (single object or list)."""
+    with the same structure that was passed in (single object or list).
+
+    ``fp8`` (MI355X extension, not in the reference): True or an ``apex.fp8.Fp8Recipe`` runs the
+    fused ops' forward / input-gradient GEMMs in per-tensor scaled fp8 on top of ``opt_level``
+    (O2 / O3 recommended: the weights are then bf16/fp16 model params); each patched
+    ``optimizer.step()`` then updates the fp8 scales (apex.fp8.step)."""
     from ._initialize import _initialize
 
     _amp_state.opt_properties = Properties()
@@ -178,6 +183,17 @@ def initialize(models, optimizers=None, enabled=True, opt_level="O1", cast_model
         maybe_print("{:22} : {}".format(k, v), True)
     _amp_state.min_loss_scale = min_loss_scale
     _amp_state.max_loss_scale = max_loss_scale
+    _amp_state.fp8 = bool(fp8)
+    if fp8:
+        from .. import fp8 as _fp8
+
+        _fp8.enable(fp8 if isinstance(fp8, _fp8.Fp8Recipe) else None)
+        maybe_print("fp8                    : {}".format(_fp8.state().recipe), True)
+    else:
+        from .. import fp8 as _fp8
+
+        if _fp8._GLOBAL:
+            _fp8.disable()
     return _initialize(models, optimizers, _amp_state.opt_properties, num_losses, cast_model_outputs)
 
 

@@ -1,0 +1,310 @@
+"""FP8 training for the dense GEMMs: per-tensor scaled OCP e4m3 / e5m2 on gfx950's block-scaled
+MFMA (``v_mfma_scale_f32_16x16x128_f8f6f4``, csrc/gemm.hip fp8 instantiation) — about 2x the
+bf16 MFMA rate on MI355X (tools/fp8_gemm_bench.py, profiles/r2_fp8_gemm.jsonl).
+
+The reference (apex) has no fp8 path; this is an MI355X-first extension of its amp O2 flow.
+
+What runs in fp8
+  forward   y = x W^T (+ bias / GELU / residual epilogue)    x: e4m3, W: e4m3
+  backward  dx = dy W (+ dGELU / residual epilogue)          dy: e5m2 ("hybrid"), W^T: e4m3
+  weight gradients stay in the activation dtype (bf16 via hipBLASLt split-K), as do attention,
+  normalisation and the optimizer. Outputs are bf16 / fp16, produced by the same fused
+  epilogues as the bf16 path.
+
+Scaling
+  * weights: current scaling — quantised (and transposed for the backward) once per optimizer
+    step from their exact amax, cached until the next ``step()``;
+  * activations and gradients: delayed scaling — each quantisation records max|x| on the device
+    (inside the quantise kernel); ``step()`` folds those into an ``amax_history_len`` window and
+    recomputes every scale (``scale = fmt_max * 2^-margin / max(window)``) in ONE kernel launch,
+    with an optional MAX all-reduce of the step's amaxes over ``amax_reduction_group`` (one
+    small RCCL call per step). A tensor's first quantisation uses current scaling.
+  Nothing here synchronises with the host.
+
+Use
+  amp:       ``amp.initialize(model, opt, opt_level="O2", fp8=True)`` (or an ``Fp8Recipe``) — the
+             patched ``optimizer.step()`` calls ``apex.fp8.step()``;
+  explicit:  ``with apex.fp8.fp8_autocast(recipe=Fp8Recipe()): loss = model(x)``; call
+             ``apex.fp8.step()`` after each optimizer step.
+  Which layers: the fused transformer blocks and dense ops of apex.ops (BERT / GPT / Megatron
+  model zoo, FusedDense, MLP) whenever their shapes fit the fp8 kernel (contraction % 128,
+  output width % 8, bf16/fp16 activations); others stay bf16.
+"""
+from __future__ import annotations
+
+import contextlib
+import dataclasses
+import weakref
+from typing import Optional
+
+import torch
+
+E4M3, E5M2 = 0, 1
+FMT_MAX = {E4M3: 448.0, E5M2: 57344.0}
+_FMT_NAMES = {"e4m3": E4M3, "e5m2": E5M2}
+
+__all__ = ["Fp8Recipe", "Fp8State", "fp8_autocast", "enable", "disable", "active", "step", "state",
+           "E4M3", "E5M2", "FMT_MAX"]
+
+
+@dataclasses.dataclass
+class Fp8Recipe:
+    """Delayed-scaling recipe. ``fwd_format`` for activations and weights, ``bwd_format`` for
+    output gradients ("hybrid" = e4m3 forward, e5m2 backward, the default)."""
+
+    margin: int = 0
+    amax_history_len: int = 16
+    fwd_format: str = "e4m3"
+    bwd_format: str = "e5m2"
+    amax_reduction_group: Optional[object] = None
+    reduce_amax: bool = True
+
+    def fmt(self, which):
+        name = self.fwd_format if which == "fwd" else self.bwd_format
+        if name not in _FMT_NAMES:
+            raise ValueError(f"fp8 format {name!r}: expected 'e4m3' or 'e5m2'")
+        return _FMT_NAMES[name]
+
+
+def _C():
+    from .. import _ext
+
+    return _ext.require()
+
+
+class Fp8State:
+    """Scaling metadata for every quantised tensor role, in device buffers indexed by slot:
+    ``hist [cap, L]``, ``amax [cap]`` (this step's running max), ``scale``, ``scale_inv``,
+    ``fmax``. Slots are keyed by (weight, role) with role in {"w", "x", "dy"}."""
+
+    def __init__(self, recipe: Fp8Recipe | None = None, device=None):
+        self.recipe = recipe or Fp8Recipe()
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
+        self.device = torch.device(device)
+        self.smax_scale = 2.0 ** (-self.recipe.margin)
+        self._cap = 0
+        self.n = 0
+        self.idx = 0
+        self.gen = 0
+        self.steps = 0
+        self.slots: dict = {}
+        self._fresh: set = set()
+        self._wcache: dict = {}
+        self._fwd = self.recipe.fmt("fwd")
+        self._bwd = self.recipe.fmt("bwd")
+        self._grow(128)
+
+    # ------------------------------------------------------------------ slots
+    def _grow(self, cap):
+        L = self.recipe.amax_history_len
+        dev = self.device
+        new = dict(hist=torch.zeros(cap, L, device=dev), amax=torch.zeros(cap, device=dev),
+                   scale=torch.ones(cap, device=dev), scale_inv=torch.ones(cap, device=dev),
+                   fmax=torch.ones(cap, device=dev))
+        if self._cap:
+            for k, t in new.items():
+                t[: self._cap].copy_(getattr(self, k))
+        for k, t in new.items():
+            setattr(self, k, t)
+        self._cap = cap
+
+    def slot(self, key, fmt) -> int:
+        s = self.slots.get(key)
+        if s is None:
+            if self.n == self._cap:
+                self._grow(2 * self._cap)
+            s = self.n
+            self.n += 1
+            self.slots[key] = s
+            self.fmax[s] = FMT_MAX[fmt]
+            self._fresh.add(s)
+        return s
+
+    def _view(self, name, s):
+        return getattr(self, name)[s:s + 1]
+
+    # ------------------------------------------------------------------ quantisers
+    def _current(self, x, s, fmt, transpose=False):
+        """Current scaling: exact amax of x, then quantise with smax / amax (scale written)."""
+        C = _C()
+        am = self._view("amax", s)
+        am.zero_()
+        C.fp8_amax(x, am)
+        q = C.fp8_quantize_t if transpose else C.fp8_quantize
+        return q(x, fmt, self._view("scale", s), None, am, self._view("scale_inv", s),
+                 FMT_MAX[fmt] * self.smax_scale)
+
+    def quantize(self, x, key, fmt):
+        """Delayed-scaled quantisation of an activation / gradient -> (codes uint8, scale_inv view)."""
+        C = _C()
+        x = x if x.is_contiguous() else x.contiguous()
+        s = self.slot(key, fmt)
+        if s in self._fresh:
+            self._fresh.discard(s)
+            y = self._current(x, s, fmt)  # amax stays recorded for the next update
+        else:
+            y = C.fp8_quantize(x, fmt, self._view("scale", s), self._view("amax", s))
+        return y, self._view("scale_inv", s)
+
+    def _weight_entry(self, w):
+        e = self._wcache.get(id(w))
+        if e is not None and e[0]() is w and e[1] == self.gen:
+            return e
+        s = self.slot((id(w), "w"), self._fwd)
+        self._fresh.discard(s)
+        w8 = self._current(w.detach().contiguous(), s, self._fwd)
+        e = [weakref.ref(w), self.gen, s, w8, None]
+        self._wcache[id(w)] = e
+        return e
+
+    def weight(self, w):
+        """W [N, K] -> (e4m3 codes [N, K], scale_inv), cached for this optimizer step."""
+        e = self._weight_entry(w)
+        return e[3], self._view("scale_inv", e[2])
+
+    def weight_t(self, w):
+        """W^T [K, N] codes (same scale as ``weight``), cached for this optimizer step."""
+        e = self._weight_entry(w)
+        if e[4] is None:
+            e[4] = _C().fp8_quantize_t(w.detach().contiguous(), self._fwd, self._view("scale", e[2]))
+        return e[4], self._view("scale_inv", e[2])
+
+    # ------------------------------------------------------------------ GEMMs
+    @staticmethod
+    def _fits(a, w, bias, aux, contraction, width):
+        if not (a.is_cuda and a.dtype in (torch.bfloat16, torch.float16) and a.dim() == 2):
+            return False
+        if contraction % 128 or width % 8 or w.dim() != 2:
+            return False
+        if bias is not None and bias.dtype != a.dtype:
+            return False
+        if aux is not None and (aux.dtype != a.dtype or not aux.is_contiguous()):
+            return False
+        return True
+
+    def forward_gemm(self, a, w, epi, bias=None, aux=None):
+        """a [M, K] @ w[N, K]^T with epilogue ``epi`` on the fp8 kernel -> (out, extra) or None."""
+        if not self._fits(a, w, bias, aux, w.shape[1], w.shape[0]):
+            return None
+        a8, ia = self.quantize(a, (id(w), "x"), self._fwd)
+        w8, iw = self.weight(w)
+        return _C().gemm_f8(a8, w8, ia, iw, self._fwd, epi, bias, aux, None, a.dtype)
+
+    def backward_gemm(self, dy, w, epi, aux=None, bias_grad_dtype=None):
+        """dy [M, N] @ w[N, K] with epilogue ``epi`` (dy e5m2 x W^T e4m3) -> (out, extra) or None."""
+        if not self._fits(dy, w, None, aux, w.shape[0], w.shape[1]):
+            return None
+        d8, id_ = self.quantize(dy, (id(w), "dy"), self._bwd)
+        wt8, iw = self.weight_t(w)
+        return _C().gemm_f8(d8, wt8, id_, iw, self._bwd, epi, None, aux, bias_grad_dtype, dy.dtype)
+
+    # ------------------------------------------------------------------ step
+    def step(self):
+        """Fold this step's amaxes into the history, recompute every scale, invalidate the
+        weight cache (the optimizer has changed the weights). One launch (+ one optional
+        all-reduce); no host synchronisation."""
+        self.gen += 1
+        self.steps += 1
+        self._wcache.clear()
+        if self.n == 0:
+            return
+        r = self.recipe
+        if r.reduce_amax and torch.distributed.is_available() and torch.distributed.is_initialized():
+            g = r.amax_reduction_group
+            if torch.distributed.get_world_size(g) > 1:
+                torch.distributed.all_reduce(self.amax[: self.n], op=torch.distributed.ReduceOp.MAX, group=g)
+        _C().fp8_update_scales(self.hist, self.amax, self.scale, self.scale_inv, self.fmax, self.n, self.idx,
+                               self.smax_scale)
+        self.idx = (self.idx + 1) % r.amax_history_len
+
+    # ------------------------------------------------------------------ checkpoint
+    def state_dict(self, model=None):
+        """Scaling state by parameter name (``model`` given) — restorable in another process."""
+        out = {"idx": self.idx, "steps": self.steps, "recipe": dataclasses.asdict(
+            dataclasses.replace(self.recipe, amax_reduction_group=None)), "slots": {}}
+        names = {id(p): n for n, p in model.named_parameters()} if model is not None else {}
+        for (pid, role), s in self.slots.items():
+            name = names.get(pid)
+            if model is not None and name is None:
+                continue
+            out["slots"][f"{name if name is not None else pid}:{role}"] = {
+                "hist": self.hist[s].cpu(), "scale": float(self.scale[s]), "scale_inv": float(self.scale_inv[s]),
+                "fmax": float(self.fmax[s]), "fresh": s in self._fresh}
+        return out
+
+    def load_state_dict(self, sd, model):
+        params = dict(model.named_parameters())
+        self.idx = int(sd["idx"])
+        self.steps = int(sd["steps"])
+        for k, v in sd["slots"].items():
+            name, role = k.rsplit(":", 1)
+            if name not in params:
+                continue
+            fmt = E4M3 if v["fmax"] == FMT_MAX[E4M3] else E5M2
+            s = self.slot((id(params[name]), role), fmt)
+            self.hist[s].copy_(v["hist"])
+            self.scale[s] = v["scale"]
+            self.scale_inv[s] = v["scale_inv"]
+            if not v["fresh"]:
+                self._fresh.discard(s)
+        self._wcache.clear()
+
+
+# ---------------------------------------------------------------------- global switch
+_STATE: Optional[Fp8State] = None
+_GLOBAL = False
+_DEPTH = 0
+
+
+def state(recipe: Fp8Recipe | None = None, device=None) -> Fp8State:
+    """The process's Fp8State (created on first use)."""
+    global _STATE
+    if _STATE is None:
+        _STATE = Fp8State(recipe, device)
+    elif recipe is not None and recipe != _STATE.recipe:
+        _STATE = Fp8State(recipe, device)  # a different recipe: fresh scaling state
+    return _STATE
+
+
+def active() -> Optional[Fp8State]:
+    """The state the fused ops should quantise with right now, or None (bf16 path)."""
+    if (_GLOBAL or _DEPTH) and _STATE is not None:
+        return _STATE
+    return None
+
+
+def enable(recipe: Fp8Recipe | None = None, device=None) -> Fp8State:
+    """Turn fp8 on for every subsequent forward (what amp.initialize(fp8=...) calls)."""
+    global _GLOBAL
+    st = state(recipe, device)
+    _GLOBAL = True
+    return st
+
+
+def disable():
+    global _GLOBAL, _STATE
+    _GLOBAL = False
+    _STATE = None
+
+
+def step():
+    """Per-optimizer-step scale update (no-op when fp8 was never used)."""
+    if _STATE is not None:
+        _STATE.step()
+
+
+@contextlib.contextmanager
+def fp8_autocast(enabled: bool = True, recipe: Fp8Recipe | None = None, device=None):
+    """Quantise the fused ops' GEMMs inside the block. The backward of a forward run here uses
+    fp8 too (the choice is recorded per autograd node). Scales update at ``step()``."""
+    global _DEPTH
+    if not enabled:
+        yield None
+        return
+    st = state(recipe, device)
+    _DEPTH += 1
+    try:
+        yield st
+    finally:
+        _DEPTH -= 1

@@ -43,15 +43,17 @@ class _AttnSublayer(torch.autograd.Function):
         d = E // heads
         scale = 1.0 / math.sqrt(d)
         x2 = _2d(x)
-        qkv = G.linear(x2, wqkv, bqkv)
+        f8 = G.fp8_state()
+        qkv = G.linear(x2, wqkv, bqkv, f8=f8)
         q, k, v = qkv.view(B, S, 3, heads, d).unbind(2)
         sa, oa = _seed(x.device) if p_attn > 0 else (0, 0)
         o, lse, dmask = C.flash_attn_fwd(q, k, v, bool(causal), scale, float(p_attn), sa, oa, k_lens)
         o2 = o.view(B * S, E)
-        t = G.linear(o2, wo)
+        t = G.linear(o2, wo, f8=f8)
         sh, oh = _seed(x.device) if p_hidden > 0 else (0, 0)
         y, s, mean, rstd = C.bdaln_fwd(t, bo, x2.contiguous(), gamma, beta, float(eps), float(p_hidden), sh, oh)
         ctx.save_for_backward(x2, wqkv, qkv, o, lse, k_lens, dmask, wo, s, gamma, mean, rstd)
+        ctx.f8 = f8
         ctx.cfg = (B, S, E, heads, d, scale, causal, p_attn, sa, oa, p_hidden, sh, oh, bqkv is not None,
                    bo is not None, bqkv.dtype if bqkv is not None else None)
         return y.view(B, S, E)
@@ -62,7 +64,8 @@ class _AttnSublayer(torch.autograd.Function):
         x2, wqkv, qkv, o, lse, k_lens, dmask, wo, s, gamma, mean, rstd = ctx.saved_tensors
         B, S, E, heads, d, scale, causal, p_attn, sa, oa, p_hidden, sh, oh, has_bqkv, has_bo, bdt = ctx.cfg
         dres, dt, dgamma, dbeta, dbo = C.bdaln_bwd(_2d(dy), s, gamma, mean, rstd, float(p_hidden), sh, oh, has_bo)
-        dctx = G.dgrad(dt, wo).view(B, S, heads, d)
+        f8 = ctx.f8
+        dctx = G.dgrad(dt, wo, f8=f8).view(B, S, heads, d)
         dwo = _wgrad(dt, o.view(B * S, E))
         q, k, v = qkv.view(B, S, 3, heads, d).unbind(2)
         dqkv = torch.empty_like(qkv)
@@ -73,7 +76,7 @@ class _AttnSublayer(torch.autograd.Function):
         C.flash_attn_bwd(dctx, q, k, v, o, lse, dq, dk, dv, bool(causal), scale, float(p_attn), sa, oa, k_lens,
                          dmask, dsum)
         dbqkv = C.partial_colsum(dsum, bdt) if has_bqkv else None
-        dx = G.dgrad_resid(dqkv, wqkv, dres)  # residual grad accumulated in the GEMM epilogue
+        dx = G.dgrad_resid(dqkv, wqkv, dres, f8=f8)  # residual grad accumulated in the GEMM epilogue
         dwqkv = _wgrad(dqkv, x2)
         return (dx.view(B, S, E), dwqkv, dbqkv, dwo, dbo if has_bo else None, dgamma, dbeta,
                 None, None, None, None, None, None)
@@ -84,16 +87,17 @@ class _FFNSublayer(torch.autograd.Function):
     def forward(ctx, x, w1, b1, w2, b2, gamma, beta, p, eps, act):
         C = _ext.require()
         x2 = _2d(x)
+        f8 = ctx.f8 = G.fp8_state()
         if act == ACT_GELU and b1 is not None:
             # g = gelu(h), h = x W1^T + b1; the backward keeps gelu'(h) (computed in this epilogue
             # from the same exp/erf) rather than h
-            g, h = G.linear_gelu_d(x2, w1, b1) if _STORE_DERIV else G.linear_gelu(x2, w1, b1)
+            g, h = G.linear_gelu_d(x2, w1, b1, f8=f8) if _STORE_DERIV else G.linear_gelu(x2, w1, b1, f8=f8)
             hb = None
         else:
             h = torch.mm(x2, w1.t())
             g = C.bias_act_fwd(h, b1, act)
             hb = b1
-        t = G.linear(g, w2)
+        t = G.linear(g, w2, f8=f8)
         seed, off = _seed(x.device) if p > 0 else (0, 0)
         y, s, mean, rstd = C.bdaln_fwd(t, b2, x2.contiguous(), gamma, beta, float(eps), float(p), seed, off)
         ctx.save_for_backward(x2, w1, hb, h, g, w2, s, gamma, mean, rstd)
@@ -105,16 +109,17 @@ class _FFNSublayer(torch.autograd.Function):
         C = _ext.require()
         x2, w1, hb, h, g, w2, s, gamma, mean, rstd = ctx.saved_tensors
         p, seed, off, act, has_b2, b1dt = ctx.cfg
+        f8 = ctx.f8
         dres, dt, dgamma, dbeta, db2 = C.bdaln_bwd(_2d(dy), s, gamma, mean, rstd, float(p), seed, off, has_b2)
         if hb is None and act == ACT_GELU and b1dt is not None:
             if _STORE_DERIV:
-                dh, db1 = G.dgrad_mul(dt, w2, h, b1dt)  # (dt W2) * gelu'(h) (stored) and its column sums
+                dh, db1 = G.dgrad_mul(dt, w2, h, b1dt, f8=f8)  # (dt W2) * gelu'(h) (stored) and its column sums
             else:
-                dh, db1 = G.dgrad_dgelu(dt, w2, h, b1dt)  # (dt W2) * gelu'(h) from h
+                dh, db1 = G.dgrad_dgelu(dt, w2, h, b1dt, f8=f8)  # (dt W2) * gelu'(h) from h
         else:
-            dh, db1 = C.bias_act_bwd(G.dgrad(dt, w2), h, hb, act)
+            dh, db1 = C.bias_act_bwd(G.dgrad(dt, w2, f8=f8), h, hb, act)
         dw2 = _wgrad(dt, g)
-        dx = G.dgrad_resid(dh, w1, dres)  # residual grad accumulated in the GEMM epilogue
+        dx = G.dgrad_resid(dh, w1, dres, f8=f8)  # residual grad accumulated in the GEMM epilogue
         dw1 = _wgrad(dh, x2)
         return (dx.view_as(dy), dw1, db1 if b1dt is not None else None, dw2, db2 if has_b2 else None, dgamma,
                 dbeta, None, None, None)
@@ -129,11 +134,12 @@ class _MLP(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w1, b1, w2, act):
         x2 = _2d(x)
+        f8 = ctx.f8 = G.fp8_state()
         if _STORE_DERIV:
-            g, gd = G.linear_gelu_d(x2, w1, b1, act)  # gelu(h) and gelu'(h)
+            g, gd = G.linear_gelu_d(x2, w1, b1, act, f8=f8)  # gelu(h) and gelu'(h)
         else:
-            g, gd = G.linear_gelu(x2, w1, b1, act)  # gelu(h) and h
-        t = G.linear(g, w2)
+            g, gd = G.linear_gelu(x2, w1, b1, act, f8=f8)  # gelu(h) and h
+        t = G.linear(g, w2, f8=f8)
         ctx.save_for_backward(x2, w1, gd, g, w2)
         ctx.act = act
         ctx.b1dt = b1.dtype
@@ -144,11 +150,11 @@ class _MLP(torch.autograd.Function):
         x2, w1, gd, g, w2 = ctx.saved_tensors
         dt2 = _2d(dt).contiguous()
         if _STORE_DERIV:
-            dh, db1 = G.dgrad_mul(dt2, w2, gd, ctx.b1dt)
+            dh, db1 = G.dgrad_mul(dt2, w2, gd, ctx.b1dt, f8=ctx.f8)
         else:
-            dh, db1 = G.dgrad_dgelu(dt2, w2, gd, ctx.b1dt, act=ctx.act)
+            dh, db1 = G.dgrad_dgelu(dt2, w2, gd, ctx.b1dt, act=ctx.act, f8=ctx.f8)
         dw2 = _wgrad(dt2, g)
-        dx = G.dgrad(dh, w1).view(*dt.shape[:-1], w1.shape[1])
+        dx = G.dgrad(dh, w1, f8=ctx.f8).view(*dt.shape[:-1], w1.shape[1])
         dw1 = _wgrad(dh, x2)
         return dx, dw1, db1, dw2, None
 

@@ -116,7 +116,8 @@ class _FusedDense(torch.autograd.Function):
         from . import gemm as G
 
         x2 = _2d(x)
-        y = G.linear(x2, w, b)
+        ctx.f8 = G.fp8_state()
+        y = G.linear(x2, w, b, f8=ctx.f8)
         ctx.save_for_backward(x2, w)
         ctx.has_b = b is not None
         ctx.bdtype = b.dtype if b is not None else None
@@ -130,7 +131,7 @@ class _FusedDense(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             from . import gemm as G
 
-            dx = G.dgrad(dy2, w).view(*dy.shape[:-1], w.shape[1])
+            dx = G.dgrad(dy2, w, f8=ctx.f8).view(*dy.shape[:-1], w.shape[1])
         if ctx.needs_input_grad[1]:
             dw = _wgrad(dy2, x2)
         if ctx.has_b and ctx.needs_input_grad[2]:
@@ -151,9 +152,11 @@ class _DenseAct(torch.autograd.Function):
 
         C = _ext.require()
         x2 = _2d(x)
-        if act in (ACT_GELU, ACT_GELU_TANH) and b is not None and G.use_mfma(x2, w) and b.dtype == x2.dtype:
+        f8 = ctx.f8 = G.fp8_state()
+        if act in (ACT_GELU, ACT_GELU_TANH) and b is not None and b.dtype == x2.dtype and \
+                (G.use_mfma(x2, w) or f8 is not None):
             # one MFMA GEMM with bias+GELU in the epilogue; h (with bias) kept for backward
-            y, h = G.linear_gelu(x2, w, b, act)
+            y, h = G.linear_gelu(x2, w, b, act, f8=f8)
             ctx.save_for_backward(x2, w, h, None)
             ctx.bdtype = b.dtype
         else:
@@ -176,7 +179,7 @@ class _DenseAct(torch.autograd.Function):
             b = db
         else:
             dh, db = C.bias_act_bwd(_2d(dy), h, b, ctx.act)
-        dx = G.dgrad(dh, w).view(*dy.shape[:-1], w.shape[1]) if ctx.needs_input_grad[0] else None
+        dx = G.dgrad(dh, w, f8=ctx.f8).view(*dy.shape[:-1], w.shape[1]) if ctx.needs_input_grad[0] else None
         dw = _wgrad(dh, x2) if ctx.needs_input_grad[1] else None
         return dx, dw, (db if b is not None else None), None
 
@@ -238,7 +241,8 @@ class _DenseBDALN(torch.autograd.Function):
 
         C = _ext.require()
         x2 = _2d(x)
-        t = G.linear(x2, w)
+        ctx.f8 = G.fp8_state()
+        t = G.linear(x2, w, f8=ctx.f8)
         seed, off = _seed(x.device) if p > 0 else (0, 0)
         y, s, mean, rstd = C.bdaln_fwd(t, b, _2d(res).contiguous(), gamma, beta, float(eps), float(p),
                                        seed, off)
@@ -254,7 +258,7 @@ class _DenseBDALN(torch.autograd.Function):
         dres, dt, dg, dbeta, db = C.bdaln_bwd(_2d(dy), s, gamma, mean, rstd, float(p), seed, off, has_b)
         from . import gemm as G
 
-        dx = G.dgrad(dt, w).view(*dy.shape[:-1], w.shape[1]) if ctx.needs_input_grad[0] else None
+        dx = G.dgrad(dt, w, f8=ctx.f8).view(*dy.shape[:-1], w.shape[1]) if ctx.needs_input_grad[0] else None
         dw = _wgrad(dt, x2) if ctx.needs_input_grad[1] else None
         return dx, dw, (db if has_b else None), dres.view_as(dy), dg, dbeta, None, None
 

@@ -31,6 +31,11 @@ Policy (``APEX_GEMM``):
 Each function falls back to the library path when the operands do not fit the MFMA kernel
 (K % 64, N % 8, dtype, alignment). Numerics follow the unfused composition: the GEMM result is
 rounded to the activation dtype before the bias/activation.
+
+FP8: every function takes ``f8`` (an apex.fp8.Fp8State, captured by the calling autograd
+Function's forward from ``fp8_state()``); when given and the shapes fit (contraction % 128), the
+product runs on the scaled-MFMA fp8 kernel with the same fused epilogue — forward operands e4m3,
+backward dy e5m2 x W^T e4m3 — and falls through to the bf16 paths otherwise.
 """
 from __future__ import annotations
 
@@ -62,6 +67,13 @@ def use_mfma(a, w, fused=True) -> bool:
     return _C().gemm_supported(a, w)
 
 
+def fp8_state():
+    """The active apex.fp8 state (None: bf16)."""
+    from .. import fp8
+
+    return fp8.active()
+
+
 def transpose(w):
     """W^T contiguous (HIP transpose kernel for 16-bit dtypes)."""
     if w.is_cuda and w.dtype in (torch.bfloat16, torch.float16) and w.dim() == 2:
@@ -69,9 +81,14 @@ def transpose(w):
     return w.t().contiguous()
 
 
-def linear(x, w, b=None):
+def linear(x, w, b=None, f8=None):
     """x [..., K] @ w[N, K]^T (+ b) in x's dtype."""
     a = _2d(x)
+    if f8 is not None:
+        C = _C()
+        r = f8.forward_gemm(a, w, C.EPI_BIAS if b is not None else C.EPI_NONE, b)
+        if r is not None:
+            return r[0].view(*x.shape[:-1], w.shape[0])
     if use_mfma(a, w, fused=False) and (b is None or b.dtype == x.dtype):
         C = _C()
         y, _ = C.gemm(a, w, C.EPI_BIAS if b is not None else C.EPI_NONE, b)
@@ -83,10 +100,15 @@ def linear(x, w, b=None):
 ACT_GELU, ACT_GELU_TANH = 0, 1  # apex.ops.fused activation codes
 
 
-def linear_gelu(x, w, b, act=ACT_GELU):
+def linear_gelu(x, w, b, act=ACT_GELU, f8=None):
     """(gelu(h), h) with h = x w^T + b (erf GELU, or tanh GELU for act=1); h kept for backward."""
     a = _2d(x)
     C = _C()
+    shp = (*x.shape[:-1], w.shape[0])
+    r = f8.forward_gemm(a, w, C.EPI_BIAS_GELU_TANH if act == ACT_GELU_TANH else C.EPI_BIAS_GELU, b) \
+        if f8 is not None and b is not None else None
+    if r is not None:
+        return r[0].view(shp), r[1].view(shp)
     if use_mfma(a, w) and b is not None and b.dtype == x.dtype:
         y, h = C.gemm(a, w, C.EPI_BIAS_GELU_TANH if act == ACT_GELU_TANH else C.EPI_BIAS_GELU, b)
     else:
@@ -97,12 +119,17 @@ def linear_gelu(x, w, b, act=ACT_GELU):
     return y.view(shp), h.view(shp)
 
 
-def linear_gelu_d(x, w, b, act=ACT_GELU):
+def linear_gelu_d(x, w, b, act=ACT_GELU, f8=None):
     """(gelu(h), gelu'(h)) with h = x w^T + b: the forward of an MLP whose backward multiplies by
     the stored derivative (dgrad_mul) instead of re-evaluating erf/exp from h. The derivative
     is taken at the rounded h, as the unfused composition's backward would."""
     a = _2d(x)
     C = _C()
+    shp = (*x.shape[:-1], w.shape[0])
+    r = f8.forward_gemm(a, w, C.EPI_BIAS_GELU_TANH_D if act == ACT_GELU_TANH else C.EPI_BIAS_GELU_D, b) \
+        if f8 is not None and b is not None else None
+    if r is not None:
+        return r[0].view(shp), r[1].view(shp)
     if use_mfma(a, w) and b is not None and b.dtype == x.dtype:
         y, gd = C.gemm(a, w, C.EPI_BIAS_GELU_TANH_D if act == ACT_GELU_TANH else C.EPI_BIAS_GELU_D, b)
     else:
@@ -113,11 +140,14 @@ def linear_gelu_d(x, w, b, act=ACT_GELU):
     return y.view(shp), gd.view(shp)
 
 
-def dgrad_mul(dy, w, gd, bias_dtype, wT=None):
+def dgrad_mul(dy, w, gd, bias_dtype, wT=None, f8=None):
     """(dh, db): dh = (dy @ w) * gd (gd = the stored activation derivative), db = column sums of dh."""
     a = _2d(dy)
     g2 = _2d(gd)
     C = _C()
+    r = f8.backward_gemm(a, w, C.EPI_MUL, g2, bias_dtype) if f8 is not None else None
+    if r is not None:
+        return r
     if _MODE != "blas" and a.is_cuda and g2.is_contiguous() and g2.dtype == a.dtype:
         wT = transpose(w) if wT is None else wT
         if use_mfma(a, wT):
@@ -128,9 +158,13 @@ def dgrad_mul(dy, w, gd, bias_dtype, wT=None):
     return dh, db
 
 
-def dgrad(dy, w, wT=None):
+def dgrad(dy, w, wT=None, f8=None):
     """dy [..., N] @ w [N, K] -> [..., K]."""
     a = _2d(dy)
+    if f8 is not None:
+        r = f8.backward_gemm(a, w, _C().EPI_NONE)
+        if r is not None:
+            return r[0].view(*dy.shape[:-1], w.shape[1])
     if _MODE == "mfma" and a.is_cuda:
         wT = transpose(w) if wT is None else wT
         if use_mfma(a, wT, fused=False):
@@ -140,10 +174,14 @@ def dgrad(dy, w, wT=None):
     return torch.mm(a, w).view(*dy.shape[:-1], w.shape[1])
 
 
-def dgrad_resid(dy, w, r, wT=None):
+def dgrad_resid(dy, w, r, wT=None, f8=None):
     """dy @ w + r (the residual-branch gradient accumulated in the epilogue)."""
     a = _2d(dy)
     r2 = _2d(r)
+    if f8 is not None:
+        res = f8.backward_gemm(a, w, _C().EPI_RESID, r2)
+        if res is not None:
+            return res[0].view(*dy.shape[:-1], w.shape[1])
     if _MODE != "blas" and a.is_cuda and r2.is_contiguous() and r2.dtype == a.dtype:
         wT = transpose(w) if wT is None else wT
         if use_mfma(a, wT):
@@ -153,11 +191,15 @@ def dgrad_resid(dy, w, r, wT=None):
     return torch.addmm(r2, a, w).view(*dy.shape[:-1], w.shape[1])
 
 
-def dgrad_dgelu(dy, w, h, bias_dtype, wT=None, act=ACT_GELU):
+def dgrad_dgelu(dy, w, h, bias_dtype, wT=None, act=ACT_GELU, f8=None):
     """(dh, db): dh = (dy @ w) * gelu'(h), db = column sums of dh (in bias_dtype)."""
     a = _2d(dy)
     h2 = _2d(h)
     C = _C()
+    r = f8.backward_gemm(a, w, C.EPI_DGELU_TANH if act == ACT_GELU_TANH else C.EPI_DGELU, h2, bias_dtype) \
+        if f8 is not None else None
+    if r is not None:
+        return r
     if _MODE != "blas" and a.is_cuda and h2.is_contiguous() and h2.dtype == a.dtype:
         wT = transpose(w) if wT is None else wT
         if use_mfma(a, wT):

@@ -48,11 +48,14 @@ def parse():
     ap.add_argument("--fp32-steps", type=int, default=2)
     ap.add_argument("--fp32-microbatch", type=int, default=256)
     ap.add_argument("--layers", type=int, default=24, help="(debug only; the metric needs 24)")
+    ap.add_argument("--fp8", action="store_true",
+                    help="extra pass: the same step with amp fp8=True (NOT the headline: reported under extra.fp8)")
+    ap.add_argument("--fp8-steps", type=int, default=10)
     ap.add_argument("--message-size", type=int, default=int(os.environ.get("APEX_DDP_MESSAGE_SIZE", 25_000_000)))
     return ap.parse_args()
 
 
-def build(env, cfg, fp32, message_size):
+def build(env, cfg, fp32, message_size, fp8=False):
     from apex import amp
     from apex.amp._amp_state import _amp_state
     from apex.models.bert import BertForPreTraining, param_groups_for_lamb
@@ -68,7 +71,7 @@ def build(env, cfg, fp32, message_size):
         model, opt = amp.initialize(model, opt, opt_level="O0", verbosity=0)
     else:
         model, opt = amp.initialize(model, opt, opt_level="O2", cast_model_type=torch.bfloat16,
-                                    verbosity=0)
+                                    verbosity=0, fp8=fp8)
     model = DDP(model, message_size=message_size, comm_timing=True)
     return model, opt
 
@@ -160,6 +163,22 @@ def main():
         extra["ddp"] = model.comm_stats()
         extra["peak_mem_gb"] = round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1)
         del model, opt, batches, loss
+        gc.collect()
+        torch.cuda.empty_cache()
+    if args.fp8 and not args.fp32_only:
+        # per-tensor scaled fp8 forward / input-gradient GEMMs (apex.fp8): an extension beyond the
+        # metric's amp O2 bf16 configuration, so it never replaces the headline value
+        model, opt = build(env, cfg, False, args.message_size, fp8=True)
+        batches = batches_for(args.batch)
+        f8_el, f8_loss = time_steps(env, make_step(model, opt, batches, 0), args.fp8_steps, 3)
+        f8_ms = max_over_ranks(env, f8_el / args.fp8_steps * 1000.0)
+        extra["fp8"] = {"ms_per_step": round(f8_ms, 2), "seq_per_s": round(args.batch * world / f8_ms * 1000.0, 2),
+                        "speedup_vs_bf16": round(ms / f8_ms, 3), "final_loss": round(float(f8_loss.float().item()), 4),
+                        "steps": args.fp8_steps, "recipe": "hybrid e4m3 fwd / e5m2 bwd, delayed scaling (history 16)"}
+        from apex import fp8 as _fp8
+
+        _fp8.disable()
+        del model, opt, batches, f8_loss
         gc.collect()
         torch.cuda.empty_cache()
     if world > 1 and not args.fp32_only:

@@ -865,6 +865,157 @@ std::vector<Tensor> k_gemm(Tensor a, Tensor b, int64_t epi, const c10::optional<
   return {c, extra};
 }
 
+// ---------------------------------------------------------------------------
+// FP8 (gemm.hip fp8 path + fp8.hip): a8 [..., K] / b8 [N, K] uint8 e4m3|e5m2 codes, alpha_a /
+// alpha_b fp32 device scalars (the inverse quantisation scales); output in out_dtype
+// ---------------------------------------------------------------------------
+void f8_check_scalar(const Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.numel() >= 1, what, " must be an fp32 device scalar");
+}
+
+bool k_gemm_f8_supported(Tensor a, Tensor b) {
+  if (!a.is_cuda() || a.dim() < 2 || b.dim() != 2 || a.scalar_type() != at::kByte || b.scalar_type() != at::kByte)
+    return false;
+  if (a.stride(-1) != 1 || b.stride(1) != 1) return false;
+  const int64_t K = a.size(-1), N = b.size(0);
+  const int64_t M = a.numel() / std::max<int64_t>(K, 1);
+  if (b.size(1) != K || M >= (1ll << 31) || N >= (1ll << 31)) return false;
+  if (a.dim() > 2 && !a.is_contiguous()) return false;
+  const int64_t lda = a.dim() == 2 ? a.stride(0) : K;
+  auto al = [](const Tensor& t) { return reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0; };
+  return al(a) && al(b) && apex::gemm_f8_supported((int)M, (int)N, (int)K, lda, b.stride(0), N);
+}
+
+std::vector<Tensor> k_gemm_f8(Tensor a, Tensor b, Tensor alpha_a, Tensor alpha_b, int64_t fmt_a, int64_t epi,
+                              const c10::optional<Tensor>& bias, const c10::optional<Tensor>& aux,
+                              c10::optional<at::ScalarType> bias_grad_dtype, at::ScalarType out_dtype) {
+  TORCH_CHECK(k_gemm_f8_supported(a, b), "gemm_f8: unsupported operands (uint8 codes, K % 128 == 0, N % 8 == 0, "
+              "16-byte aligned, unit inner stride)");
+  TORCH_CHECK(out_dtype == at::kBFloat16 || out_dtype == at::kHalf, "gemm_f8: bf16 / fp16 output");
+  f8_check_scalar(alpha_a, "alpha_a");
+  f8_check_scalar(alpha_b, "alpha_b");
+  const int64_t K = a.size(-1), N = b.size(0), M = a.numel() / K;
+  std::vector<int64_t> osz(a.sizes().begin(), a.sizes().end());
+  osz.back() = N;
+  auto oopt = a.options().dtype(out_dtype);
+  Tensor c = at::empty(osz, oopt);
+  apex::GemmArgs g{};
+  g.A = a.data_ptr();
+  g.B = b.data_ptr();
+  g.C = c.data_ptr();
+  g.M = (int)M;
+  g.N = (int)N;
+  g.K = (int)K;
+  g.lda = a.dim() == 2 ? a.stride(0) : K;
+  g.ldb = b.stride(0);
+  g.ldc = N;
+  g.epi = (int)epi;
+  g.alpha_a = alpha_a.data_ptr<float>();
+  g.alpha_b = alpha_b.data_ptr<float>();
+  Tensor extra, part;
+  const bool gelu_fwd = epi == apex::EPI_BIAS_GELU || epi == apex::EPI_BIAS_GELU_TANH ||
+                        epi == apex::EPI_BIAS_GELU_D || epi == apex::EPI_BIAS_GELU_TANH_D;
+  const bool mul = epi == apex::EPI_DGELU || epi == apex::EPI_DGELU_TANH || epi == apex::EPI_MUL;
+  TORCH_CHECK(epi >= 0 && epi <= apex::EPI_MUL && epi != apex::EPI_F32, "gemm_f8: bad epilogue ", epi);
+  if (epi == apex::EPI_BIAS || gelu_fwd) {
+    TORCH_CHECK(bias.has_value() && bias->defined() && bias->is_contiguous() && bias->numel() == N &&
+                    bias->scalar_type() == out_dtype, "gemm_f8: bias must be a contiguous [N] tensor of out_dtype");
+    g.bias = bias->data_ptr();
+  }
+  if (gelu_fwd) {
+    extra = at::empty(osz, oopt);
+    g.aux_out = extra.data_ptr();
+  }
+  if (mul || epi == apex::EPI_RESID) {
+    TORCH_CHECK(aux.has_value() && aux->defined() && aux->scalar_type() == out_dtype && aux->numel() == M * N &&
+                    aux->is_contiguous(), "gemm_f8: aux must be a contiguous [M, N] tensor of out_dtype");
+    g.aux = aux->data_ptr();
+    g.ldaux = N;
+  }
+  if (mul) {
+    part = at::empty({apex::gemm_part_rows((int)M), N}, a.options().dtype(at::kFloat));
+    g.part = part.data_ptr<float>();
+  }
+  check(apex::gemm_nt_f8(g, (int)fmt_a, 0, dt_code(out_dtype), cur_stream()), "gemm_f8");
+  if (mul && bias_grad_dtype.has_value()) {
+    extra = at::empty({N}, a.options().dtype(*bias_grad_dtype));
+    check(apex::gemm_bias_grad(part.data_ptr<float>(), (int)part.size(0), (int)N, extra.data_ptr(),
+                               dt_code(*bias_grad_dtype), cur_stream()), "gemm_bias_grad");
+  }
+  return {c, extra};
+}
+
+struct F8Opt {
+  float* amax = nullptr;
+  const float* cur = nullptr;
+  float* scale_inv = nullptr;
+};
+
+F8Opt f8_opts(const c10::optional<Tensor>& amax, const c10::optional<Tensor>& cur_amax,
+              const c10::optional<Tensor>& scale_inv, double smax) {
+  F8Opt o;
+  if (amax.has_value() && amax->defined()) {
+    f8_check_scalar(*amax, "amax");
+    o.amax = amax->data_ptr<float>();
+  }
+  if (cur_amax.has_value() && cur_amax->defined()) {
+    f8_check_scalar(*cur_amax, "cur_amax");
+    TORCH_CHECK(scale_inv.has_value() && scale_inv->defined() && smax > 0,
+                "fp8 current scaling needs scale_inv and smax > 0");
+    o.cur = cur_amax->data_ptr<float>();
+  }
+  if (scale_inv.has_value() && scale_inv->defined()) {
+    f8_check_scalar(*scale_inv, "scale_inv");
+    o.scale_inv = scale_inv->data_ptr<float>();
+  }
+  return o;
+}
+
+// delayed scaling: quantise with scale (and fold max|x| into amax); current scaling: cur_amax holds
+// max|x| already, scale / scale_inv are written (= smax / cur_amax and its inverse)
+Tensor k_fp8_quantize(Tensor x, int64_t fmt, Tensor scale, const c10::optional<Tensor>& amax,
+                      const c10::optional<Tensor>& cur_amax, const c10::optional<Tensor>& scale_inv, double smax) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous(), "fp8_quantize: contiguous device tensor");
+  f8_check_scalar(scale, "scale");
+  const F8Opt o = f8_opts(amax, cur_amax, scale_inv, smax);
+  Tensor y = at::empty(x.sizes(), x.options().dtype(at::kByte));
+  check(apex::fp8_quantize(x.data_ptr(), y.data_ptr<uint8_t>(), x.numel(), dt_code(x.scalar_type()), (int)fmt,
+                           scale.data_ptr<float>(), o.scale_inv, o.amax, o.cur, (float)smax, cur_stream()),
+        "fp8_quantize");
+  return y;
+}
+
+Tensor k_fp8_quantize_t(Tensor x, int64_t fmt, Tensor scale, const c10::optional<Tensor>& amax,
+                        const c10::optional<Tensor>& cur_amax, const c10::optional<Tensor>& scale_inv, double smax) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.dim() == 2, "fp8_quantize_t: contiguous 2-D device tensor");
+  f8_check_scalar(scale, "scale");
+  const F8Opt o = f8_opts(amax, cur_amax, scale_inv, smax);
+  Tensor y = at::empty({x.size(1), x.size(0)}, x.options().dtype(at::kByte));
+  check(apex::fp8_quantize_t(x.data_ptr(), y.data_ptr<uint8_t>(), (int)x.size(0), (int)x.size(1),
+                             dt_code(x.scalar_type()), (int)fmt, scale.data_ptr<float>(), o.scale_inv, o.amax, o.cur,
+                             (float)smax, cur_stream()),
+        "fp8_quantize_t");
+  return y;
+}
+
+void k_fp8_amax(Tensor x, Tensor amax) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous(), "fp8_amax: contiguous device tensor");
+  f8_check_scalar(amax, "amax");
+  check(apex::fp8_amax(x.data_ptr(), x.numel(), dt_code(x.scalar_type()), amax.data_ptr<float>(), cur_stream()),
+        "fp8_amax");
+}
+
+void k_fp8_update_scales(Tensor hist, Tensor amax_cur, Tensor scale, Tensor scale_inv, Tensor fmt_max, int64_t n_slots,
+                         int64_t idx, double margin_scale) {
+  TORCH_CHECK(hist.is_cuda() && hist.dim() == 2 && hist.is_contiguous() && hist.scalar_type() == at::kFloat,
+              "fp8_update_scales: hist fp32 [slots, history]");
+  TORCH_CHECK(n_slots <= hist.size(0) && idx >= 0 && idx < hist.size(1), "fp8_update_scales: bad slot count / index");
+  check(apex::fp8_update_scales(hist.data_ptr<float>(), amax_cur.data_ptr<float>(), scale.data_ptr<float>(),
+                                scale_inv.data_ptr<float>(), fmt_max.data_ptr<float>(), (int)n_slots,
+                                (int)hist.size(1), (int)idx, (float)margin_scale, cur_stream()),
+        "fp8_update_scales");
+}
+
 // weight gradient: out[P, Q] = a^T b for a [R, P], b [R, Q] (contraction over the R rows, split
 // into `splits` slices whose fp32 partials are combined by splitk_reduce)
 bool k_gemm_tt_supported(Tensor a, Tensor b, int64_t splits) {
@@ -950,6 +1101,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ln_bwd", &ln_bwd);
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd", &xent_bwd);
+  m.def("gemm_f8_supported", &k_gemm_f8_supported);
+  m.def("gemm_f8", &k_gemm_f8, py::arg("a"), py::arg("b"), py::arg("alpha_a"), py::arg("alpha_b"), py::arg("fmt_a"),
+        py::arg("epi"), py::arg("bias") = py::none(), py::arg("aux") = py::none(),
+        py::arg("bias_grad_dtype") = py::none(), py::arg("out_dtype") = at::kBFloat16);
+  m.def("fp8_quantize", &k_fp8_quantize, py::arg("x"), py::arg("fmt"), py::arg("scale"), py::arg("amax") = py::none(),
+        py::arg("cur_amax") = py::none(), py::arg("scale_inv") = py::none(), py::arg("smax") = 0.0);
+  m.def("fp8_quantize_t", &k_fp8_quantize_t, py::arg("x"), py::arg("fmt"), py::arg("scale"),
+        py::arg("amax") = py::none(), py::arg("cur_amax") = py::none(), py::arg("scale_inv") = py::none(),
+        py::arg("smax") = 0.0);
+  m.def("fp8_amax", &k_fp8_amax);
+  m.def("fp8_update_scales", &k_fp8_update_scales);
   m.def("flash_attn_fwd", &flash_attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("causal"),
         py::arg("scale"), py::arg("p_drop"), py::arg("seed"), py::arg("offset"), py::arg("k_lens"),
         py::arg("bias") = py::none());

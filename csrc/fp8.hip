@@ -1,0 +1,245 @@
+// FP8 support kernels for the fp8 GEMM path (amp fp8 option, apex/fp8): per-tensor scaled
+// quantisation to OCP e4m3 / e5m2 (gfx950's native FP8 encodings) and the delayed-scaling
+// bookkeeping — every quantisation records the amax of its input on the device, and one launch
+// per step folds those amaxes into a rolling history and recomputes every scale. No host sync.
+//
+//   quantize      y8 = sat(x * scale[slot])           + amax_cur[slot] = max |x|
+//                 (current scaling: scale = fmt_max * 2^-margin / amax measured just before)
+//   quantize_t    y8[c][r] = sat(x[r][c] * scale)     (weights for the dgrad GEMM: W^T, K-contiguous)
+//   amax          amax_cur[slot] = max |x|             (first use of a slot: current scaling)
+//   update        hist[slot][idx] = amax_cur; a = max(hist[slot]); scale = fmt_max / a / 2^margin;
+//                 scale_inv = 1 / scale; amax_cur = 0
+// The conversions are the hardware v_cvt_pk_fp8_f32 / v_cvt_pk_bf8_f32 (round to nearest even); x
+// is clamped to the format's finite range first (e4m3fn has no infinity).
+#include "common.h"
+#include "kernels.h"
+
+namespace apex {
+
+namespace {
+
+constexpr float kE4M3Max = 448.f;
+constexpr float kE5M2Max = 57344.f;
+
+// non-negative floats order like their bit patterns: max via integer atomics
+__device__ __forceinline__ void atomic_max_pos(float* p, float v) {
+  atomicMax(reinterpret_cast<unsigned int*>(p), __float_as_uint(v));
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// block max -> ONE atomic per 256-thread block (thousands of same-address atomics serialise in
+// L2: one per wave made the quantiser atomic-bound at ~0.19 ms regardless of size). The plain
+// pre-read is only a filter: amax only grows, so a stale value costs an extra atomic, never a
+// missed one.
+__device__ __forceinline__ void block_amax(float mx, float* amax) {
+  __shared__ float red[4];
+  mx = wave_max(mx);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    if (m > 0.f && m > *(volatile float*)amax) atomic_max_pos(amax, m);
+  }
+}
+
+template <int FMT>
+__device__ __forceinline__ uint32_t pack4(float a, float b, float c, float d) {
+  const float m = FMT == 0 ? kE4M3Max : kE5M2Max;
+  a = fminf(fmaxf(a, -m), m);
+  b = fminf(fmaxf(b, -m), m);
+  c = fminf(fmaxf(c, -m), m);
+  d = fminf(fmaxf(d, -m), m);
+  int w = 0;
+  if constexpr (FMT == 0) {
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, w, false);
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+  } else {
+    w = __builtin_amdgcn_cvt_pk_bf8_f32(a, b, w, false);
+    w = __builtin_amdgcn_cvt_pk_bf8_f32(c, d, w, true);
+  }
+  return (uint32_t)w;
+}
+
+// Scale source of one quantisation. Delayed: s = scale[0] (from the history), the input's amax
+// is folded into amax[0] for the next update. Current (cur != null, amax already measured by
+// amax_kernel): s = smax / cur[0], written back to scale[0] / scale_inv[0] by the first block.
+struct QScale {
+  float* scale;
+  float* scale_inv;
+  float* amax;
+  const float* cur;
+  float smax;
+};
+
+__device__ __forceinline__ float q_scale(const QScale& q, bool first_block) {
+  if (!q.cur) return q.scale[0];
+  const float a = q.cur[0];
+  const float s = (a > 0.f && isfinite(a)) ? q.smax / a : 1.f;
+  if (first_block && threadIdx.x == 0) {
+    q.scale[0] = s;
+    q.scale_inv[0] = 1.f / s;
+  }
+  return s;
+}
+
+// 8 elements per lane per iteration (16-byte loads of 16-bit inputs, 8-byte stores)
+template <typename T, int FMT>
+__global__ void __launch_bounds__(256) quantize_kernel(const T* __restrict__ x, uint8_t* __restrict__ y, int64_t n,
+                                                       QScale q) {
+  const float s = q_scale(q, blockIdx.x == 0);
+  float* amax = q.amax;
+  float mx = 0.f;
+  const int64_t nv = n / 8;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += (int64_t)gridDim.x * 256) {
+    float v[8];
+    load_f<T, 8>(x + i * 8, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) mx = fmaxf(mx, fabsf(v[k]));
+    uint2 w;
+    w.x = pack4<FMT>(v[0] * s, v[1] * s, v[2] * s, v[3] * s);
+    w.y = pack4<FMT>(v[4] * s, v[5] * s, v[6] * s, v[7] * s);
+    *reinterpret_cast<uint2*>(y + i * 8) = w;
+  }
+  for (int64_t i = nv * 8 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float v = to_f(x[i]);
+    mx = fmaxf(mx, fabsf(v));
+    y[i] = (uint8_t)(pack4<FMT>(v * s, 0.f, 0.f, 0.f) & 0xff);
+  }
+  if (amax) block_amax(mx, amax);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) amax_kernel(const T* __restrict__ x, int64_t n, float* __restrict__ amax) {
+  float mx = 0.f;
+  const int64_t nv = n / 8;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += (int64_t)gridDim.x * 256) {
+    float v[8];
+    load_f<T, 8>(x + i * 8, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) mx = fmaxf(mx, fabsf(v[k]));
+  }
+  for (int64_t i = nv * 8 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    mx = fmaxf(mx, fabsf(to_f(x[i])));
+  block_amax(mx, amax);
+}
+
+// y[C][R] = quant(x[R][C]): 64 x 64 tiles through LDS, 8 elements (one 8-byte store) per lane
+template <typename T, int FMT>
+__global__ void __launch_bounds__(256) quantize_t_kernel(const T* __restrict__ x, uint8_t* __restrict__ y, int R,
+                                                         int C, QScale q) {
+  __shared__ float tile[64][65];
+  const float s = q_scale(q, blockIdx.x == 0 && blockIdx.y == 0);
+  float* amax = q.amax;
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  float mx = 0.f;
+  for (int idx = threadIdx.x; idx < 64 * 64; idx += 256) {
+    const int rr = idx / 64, cc = idx % 64;
+    const int r = r0 + rr, c = c0 + cc;
+    const float v = (r < R && c < C) ? to_f(x[(int64_t)r * C + c]) : 0.f;
+    mx = fmaxf(mx, fabsf(v));
+    tile[rr][cc] = v * s;
+  }
+  __syncthreads();
+  // thread -> (output row c, 8 consecutive r)
+  for (int idx = threadIdx.x; idx < 64 * 8; idx += 256) {
+    const int cc = idx / 8, rg = (idx % 8) * 8;
+    const int c = c0 + cc, r = r0 + rg;
+    if (c >= C) continue;
+    const float* t = &tile[0][0];
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = t[(rg + k) * 65 + cc];
+    if (r + 8 <= R) {
+      uint2 w;
+      w.x = pack4<FMT>(v[0], v[1], v[2], v[3]);
+      w.y = pack4<FMT>(v[4], v[5], v[6], v[7]);
+      *reinterpret_cast<uint2*>(y + (int64_t)c * R + r) = w;
+    } else {
+      for (int k = 0; k < 8 && r + k < R; ++k) y[(int64_t)c * R + r + k] = (uint8_t)(pack4<FMT>(v[k], 0.f, 0.f, 0.f) & 0xff);
+    }
+  }
+  if (amax) block_amax(mx, amax);
+}
+
+// one thread per slot
+__global__ void update_scales_kernel(float* __restrict__ hist, float* __restrict__ amax_cur, float* __restrict__ scale,
+                                     float* __restrict__ scale_inv, const float* __restrict__ fmt_max, int n_slots,
+                                     int hist_len, int idx, float margin_scale) {
+  const int sl = blockIdx.x * blockDim.x + threadIdx.x;
+  if (sl >= n_slots) return;
+  float* h = hist + (int64_t)sl * hist_len;
+  const float cur = amax_cur[sl];
+  h[idx] = isfinite(cur) ? cur : 0.f;  // an overflowed (skipped) step does not poison the window
+  float a = 0.f;
+  for (int k = 0; k < hist_len; ++k) a = fmaxf(a, h[k]);
+  if (a > 0.f && isfinite(a)) {
+    const float sc = fmt_max[sl] / a * margin_scale;
+    scale[sl] = sc;
+    scale_inv[sl] = 1.f / sc;
+  }
+  amax_cur[sl] = 0.f;
+}
+
+inline int grid_for(int64_t n8) {
+  int64_t g = (n8 + 255) / 256;
+  return (int)(g < 1 ? 1 : g > 1024 ? 1024 : g);  // 4 blocks / CU, grid-stride beyond
+}
+
+}  // namespace
+
+#define FP8_DT(DT, T, ...)                                  \
+  switch (DT) {                                             \
+    case kF32: { using T = float; __VA_ARGS__; } break;     \
+    case kF16: { using T = f16; __VA_ARGS__; } break;       \
+    case kBF16: { using T = bf16; __VA_ARGS__; } break;     \
+    default: return -1;                                     \
+  }
+
+int fp8_quantize(const void* x, uint8_t* y, int64_t n, int dt, int fmt, float* scale, float* scale_inv, float* amax,
+                 const float* cur, float smax, hipStream_t s) {
+  if (n == 0) return 0;
+  if (cur && (!scale_inv || smax <= 0.f)) return -2;
+  const QScale q{scale, scale_inv, amax, cur, smax};
+  const int g = grid_for((n + 7) / 8);
+  if (fmt == 0) {
+    FP8_DT(dt, T, hipLaunchKernelGGL((quantize_kernel<T, 0>), dim3(g), dim3(256), 0, s, (const T*)x, y, n, q));
+  } else {
+    FP8_DT(dt, T, hipLaunchKernelGGL((quantize_kernel<T, 1>), dim3(g), dim3(256), 0, s, (const T*)x, y, n, q));
+  }
+  return (int)hipGetLastError();
+}
+
+int fp8_quantize_t(const void* x, uint8_t* y, int R, int C, int dt, int fmt, float* scale, float* scale_inv,
+                   float* amax, const float* cur, float smax, hipStream_t s) {
+  if (R == 0 || C == 0) return 0;
+  if (cur && (!scale_inv || smax <= 0.f)) return -2;
+  const QScale q{scale, scale_inv, amax, cur, smax};
+  dim3 grid((C + 63) / 64, (R + 63) / 64);
+  if (fmt == 0) {
+    FP8_DT(dt, T, hipLaunchKernelGGL((quantize_t_kernel<T, 0>), grid, dim3(256), 0, s, (const T*)x, y, R, C, q));
+  } else {
+    FP8_DT(dt, T, hipLaunchKernelGGL((quantize_t_kernel<T, 1>), grid, dim3(256), 0, s, (const T*)x, y, R, C, q));
+  }
+  return (int)hipGetLastError();
+}
+
+int fp8_amax(const void* x, int64_t n, int dt, float* amax, hipStream_t s) {
+  if (n == 0) return 0;
+  FP8_DT(dt, T, hipLaunchKernelGGL((amax_kernel<T>), dim3(grid_for((n + 7) / 8)), dim3(256), 0, s, (const T*)x, n, amax));
+  return (int)hipGetLastError();
+}
+
+int fp8_update_scales(float* hist, float* amax_cur, float* scale, float* scale_inv, const float* fmt_max,
+                      int n_slots, int hist_len, int idx, float margin_scale, hipStream_t s) {
+  if (n_slots == 0) return 0;
+  hipLaunchKernelGGL(update_scales_kernel, dim3((n_slots + 255) / 256), dim3(256), 0, s, hist, amax_cur, scale,
+                     scale_inv, fmt_max, n_slots, hist_len, idx, margin_scale);
+  return (int)hipGetLastError();
+}
+
+}  // namespace apex

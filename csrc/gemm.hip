@@ -61,6 +61,24 @@ template <> __device__ __forceinline__ f32x4 mfma16<f16>(const s16x8& a, const s
   return __builtin_amdgcn_mfma_f32_16x16x32_f16((h8)a, (h8)b, c, 0, 0, 0);
 }
 
+// FP8 (gfx950 f8f6f4 block-scaled MFMA, 16x16x128, 2x the bf16 rate): the 32 bytes of a lane's
+// operand are the SAME two 16-byte LDS chunks the bf16 path reads for its two 16x16x32 K-steps
+// (chunks lk and lk + 4 of the 128-byte K-tile row). The K order inside the instruction is thus a
+// permutation of the tile's K, identical for both operands, so the dot products are unchanged and
+// the LDS reads stay conflict-free. Block scales are all 2^0 (E8M0 127): the per-tensor scales
+// are applied in the epilogue (alpha). Formats: 0 = e4m3 (OCP fn), 1 = e5m2.
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+template <int FMT_A, int FMT_B>
+__device__ __forceinline__ f32x4 mfma_f8(const s16x8& a0, const s16x8& a1, const s16x8& b0, const s16x8& b1,
+                                         const f32x4& c) {
+  const i32x4 xa0 = __builtin_bit_cast(i32x4, a0), xa1 = __builtin_bit_cast(i32x4, a1);
+  const i32x4 xb0 = __builtin_bit_cast(i32x4, b0), xb1 = __builtin_bit_cast(i32x4, b1);
+  const i32x8 a = __builtin_shufflevector(xa0, xa1, 0, 1, 2, 3, 4, 5, 6, 7);
+  const i32x8 b = __builtin_shufflevector(xb0, xb1, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, FMT_A, FMT_B, 0, 0x7F7F7F7F, 0, 0x7F7F7F7F);
+}
+
 __device__ __forceinline__ void glds16(const void* g, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
@@ -170,13 +188,13 @@ __device__ __forceinline__ void stage_pieces(const T* __restrict__ g, int64_t ld
     if constexpr (TR) {
       const int r = piece * 2 + (lane >> 5);
       const int chunk = (lane & 31) ^ ftr(r);
-      glds16(g + (int64_t)(k0 + r) * ld + row0 + chunk * 8, lds_tile + piece * 1024);
+      glds16(g + (int64_t)(k0 + r) * ld + row0 + chunk * (16 / (int)sizeof(T)), lds_tile + piece * 1024);
     } else {
       const int r = piece * 8 + (lane >> 3);
       const int chunk = (lane & 7) ^ ((r >> 1) & 7);
       int gr = row0 + r;
       gr = gr < rows ? gr : rows - 1;
-      glds16(g + (int64_t)gr * ld + k0 + chunk * 8, lds_tile + piece * 1024);
+      glds16(g + (int64_t)gr * ld + k0 + chunk * (16 / (int)sizeof(T)), lds_tile + piece * 1024);
     }
   }
 }
@@ -232,11 +250,15 @@ __device__ __forceinline__ s16x8 frag(const char* tile, int rb, int s, int lr, i
 // software-pipelined under 64-MFMA halves) makes hipcc shuffle ~220 accumulator copies
 // (v_accvgpr_read/write) per K-tile through the loop-carried phis, so it is not used. rocprof on the 32768x1024x4096 case: MFMA busy 65 %
 // of SIMD cycles at 1.98 GHz, zero LDS bank conflicts.
-template <typename T, bool TR>
+template <typename T, bool TR, int FA = -1, int FB = -1>
 __device__ __forceinline__ void mainloop_bk64(const T* __restrict__ A, const T* __restrict__ B, int M, int N, int K,
                                               int64_t lda, int64_t ldb, int m0, int n0, char* smem, int wid, int wr,
                                               int wc, int lane, f32x4 (&acc)[4][8]) {
-  const int nt = K / GB_K;
+  // one K-tile = 128 bytes of every row: 64 bf16/f16 elements or 128 fp8 ones
+  constexpr bool F8 = FA >= 0;
+  static_assert(!F8 || (!TR && sizeof(T) == 1), "fp8: NT operands only");
+  constexpr int BKE = 128 / (int)sizeof(T);
+  const int nt = K / BKE;
   const int lr = lane & 15, lk = lane >> 4;
   // prologue: A(0), B(0) -> buf0, B(1) -> buf1; retire tile 0
   stage_pieces<T, TR>(A, lda, m0, M, 0, smem, wid, lane, 0);
@@ -244,8 +266,8 @@ __device__ __forceinline__ void mainloop_bk64(const T* __restrict__ A, const T* 
   stage_pieces<T, TR>(B, ldb, n0, N, 0, smem + G_TILE_BYTES, wid, lane, 0);
   stage_pieces<T, TR>(B, ldb, n0, N, 0, smem + G_TILE_BYTES, wid, lane, 2);
   if (nt > 1) {
-    stage_pieces<T, TR>(B, ldb, n0, N, GB_K, smem + G_BUF_BYTES + G_TILE_BYTES, wid, lane, 0);
-    stage_pieces<T, TR>(B, ldb, n0, N, GB_K, smem + G_BUF_BYTES + G_TILE_BYTES, wid, lane, 2);
+    stage_pieces<T, TR>(B, ldb, n0, N, BKE, smem + G_BUF_BYTES + G_TILE_BYTES, wid, lane, 0);
+    stage_pieces<T, TR>(B, ldb, n0, N, BKE, smem + G_BUF_BYTES + G_TILE_BYTES, wid, lane, 2);
     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -269,16 +291,23 @@ __device__ __forceinline__ void mainloop_bk64(const T* __restrict__ A, const T* 
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int s = 0; s < 2; ++s) fa[i][s] = frag<TR>(ta, wr * 128 + i * 16, s, lr, lk);
-    if (ld_a) stage_pieces<T, TR>(A, lda, m0, M, (t + 1) * GB_K, oth, wid, lane, 0);
+    if (ld_a) stage_pieces<T, TR>(A, lda, m0, M, (t + 1) * BKE, oth, wid, lane, 0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     bar();
     __builtin_amdgcn_s_setprio(1);
+    if constexpr (F8) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[j][i] = mfma_f8<FB, FA>(fb0[j][0], fb0[j][1], fa[i][0], fa[i][1], acc[j][i]);
+    } else {
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc[j][i] = mfma16<T>(fb0[j][s], fa[i][s], acc[j][i]);
+    }
     __builtin_amdgcn_s_setprio(0);
     bar();
     // ---------------- p2: B nh=1; stage A(t+1) pieces 2,3 ----------------
@@ -286,16 +315,23 @@ __device__ __forceinline__ void mainloop_bk64(const T* __restrict__ A, const T* 
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int s = 0; s < 2; ++s) fb1[j][s] = frag<TR>(tb, wc * 64 + 32 + j * 16, s, lr, lk);
-    if (ld_a) stage_pieces<T, TR>(A, lda, m0, M, (t + 1) * GB_K, oth, wid, lane, 2);
+    if (ld_a) stage_pieces<T, TR>(A, lda, m0, M, (t + 1) * BKE, oth, wid, lane, 2);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     bar();
     __builtin_amdgcn_s_setprio(1);
+    if constexpr (F8) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[2 + j][i] = mfma_f8<FB, FA>(fb1[j][0], fb1[j][1], fa[i][0], fa[i][1], acc[2 + j][i]);
+    } else {
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc[2 + j][i] = mfma16<T>(fb1[j][s], fa[i][s], acc[2 + j][i]);
+    }
     __builtin_amdgcn_s_setprio(0);
     bar();
     // ---------------- p3: A mh=1; stage B(t+2) pieces 0,1 into this buffer ----------------
@@ -303,33 +339,47 @@ __device__ __forceinline__ void mainloop_bk64(const T* __restrict__ A, const T* 
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int s = 0; s < 2; ++s) fa[i][s] = frag<TR>(ta, wr * 128 + 64 + i * 16, s, lr, lk);
-    if (ld_b) stage_pieces<T, TR>(B, ldb, n0, N, (t + 2) * GB_K, cur + G_TILE_BYTES, wid, lane, 0);
+    if (ld_b) stage_pieces<T, TR>(B, ldb, n0, N, (t + 2) * BKE, cur + G_TILE_BYTES, wid, lane, 0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     bar();
     __builtin_amdgcn_s_setprio(1);
+    if constexpr (F8) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[2 + j][4 + i] = mfma_f8<FB, FA>(fb1[j][0], fb1[j][1], fa[i][0], fa[i][1], acc[2 + j][4 + i]);
+    } else {
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc[2 + j][4 + i] = mfma16<T>(fb1[j][s], fa[i][s], acc[2 + j][4 + i]);
+    }
     __builtin_amdgcn_s_setprio(0);
     bar();
     // ---------------- p4: stage B(t+2) pieces 2,3; retire A(t+1), B(t+1) ----------------
     if (ld_b) {
-      stage_pieces<T, TR>(B, ldb, n0, N, (t + 2) * GB_K, cur + G_TILE_BYTES, wid, lane, 2);
+      stage_pieces<T, TR>(B, ldb, n0, N, (t + 2) * BKE, cur + G_TILE_BYTES, wid, lane, 2);
       asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     bar();
     __builtin_amdgcn_s_setprio(1);
+    if constexpr (F8) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[j][4 + i] = mfma_f8<FB, FA>(fb0[j][0], fb0[j][1], fa[i][0], fa[i][1], acc[j][4 + i]);
+    } else {
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc[j][4 + i] = mfma16<T>(fb0[j][s], fa[i][s], acc[j][4 + i]);
+    }
     __builtin_amdgcn_s_setprio(0);
     bar();
   }
@@ -340,7 +390,7 @@ template <typename T, int EPI, int TBM, int TBN>
 __device__ __forceinline__ void epilogue(const f32x4 (&acc)[4][8], char* reg, T* __restrict__ C, int M, int N,
                                          int64_t ldc, const T* __restrict__ bias, const T* __restrict__ aux,
                                          int64_t ldaux, T* __restrict__ aux_out, float* __restrict__ part, int m0,
-                                         int n0, int tm, int wr, int wc, int lane) {
+                                         int n0, int tm, int wr, int wc, int lane, float alpha = 1.f) {
   const int lr = lane & 15, lk = lane >> 4;
   // ---- epilogue ----
   // acc[j][i] holds rows wr*128 + i*16 + lr, cols wc*64 + j*16 + 4*lk .. +3 of the tile. The fp32
@@ -362,7 +412,7 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[4][8], char* reg, T*
       const int half = (lk & 1) ^ ((row >> 3) & 1);
       Pack<T, 4> pk;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) pk.v[e] = from_f<T>(acc[j][i][e]);
+      for (int e = 0; e < 4; ++e) pk.v[e] = from_f<T>(acc[j][i][e] * alpha);
       *reinterpret_cast<Pack<T, 4>*>(reg + row * 128 + chunk * 16 + half * 8) = pk;
     }
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
@@ -536,13 +586,16 @@ __device__ int g_gemm_dbg = 0;
 // profiles/r1_gemm_stagger.json), so the launchers pass 0.
 __device__ int g_gemm_stagger = 0;
 
-template <typename T, int EPI, bool TR>
-__global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(const T* __restrict__ A, const T* __restrict__ B,
+// T: output / epilogue dtype; TI: operand dtype (T, or uint8_t fp8 with formats FA (A) / FB (B) and
+// the dequantisation alpha = alpha_a[0] * alpha_b[0] read on the device)
+template <typename T, int EPI, bool TR, typename TI = T, int FA = -1, int FB = -1>
+__global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(const TI* __restrict__ A, const TI* __restrict__ B,
                                                             T* __restrict__ C, int M, int N, int K, int64_t lda,
                                                             int64_t ldb, int64_t ldc, const T* __restrict__ bias,
                                                             const T* __restrict__ aux, int64_t ldaux,
                                                             T* __restrict__ aux_out, float* __restrict__ part,
-                                                            int stagger) {
+                                                            int stagger, const float* __restrict__ alpha_a = nullptr,
+                                                            const float* __restrict__ alpha_b = nullptr) {
   __shared__ __attribute__((aligned(16))) char smem[G_LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -578,7 +631,7 @@ __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(const T* __restrict_
     A += (int64_t)blockIdx.y * K * lda;
     B += (int64_t)blockIdx.y * K * ldb;
   }
-  mainloop_bk64<T, TR>(A, B, M, N, K, lda, ldb, m0, n0, smem, wid, wr, wc, lane, acc);
+  mainloop_bk64<TI, TR, FA, FB>(A, B, M, N, K, lda, ldb, m0, n0, smem, wid, wr, wc, lane, acc);
   if (wr == 0) bar();  // re-align the groups
   bar();               // every wave is past its last ds_read: LDS is free for the epilogue
   if constexpr (EPI == EPI_F32) {
@@ -605,8 +658,10 @@ __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(const T* __restrict_
     if (t == 1.2345e-30f) C[0] = from_f<T>(t);
     return;
   }
+  float alpha = 1.f;
+  if constexpr (FA >= 0) alpha = alpha_a[0] * alpha_b[0];
   epilogue<T, EPI, GB_M, GB_N>(acc, smem + wid * 16384, C, M, N, ldc, bias, aux, ldaux, aux_out, part, m0, n0, tm, wr,
-                                wc, lane);
+                                wc, lane, alpha);
 }
 
 
@@ -646,6 +701,32 @@ void launch_gemm(const GemmArgs& g, hipStream_t s) {
   hipLaunchKernelGGL((gemm_nt_kernel<T, EPI, TR>), dim3(tiles, TR ? g.splits : 1), dim3(G_THREADS), 0, s, (const T*)g.A, (const T*)g.B,
                      (T*)g.C, g.M, g.N, g.K, g.lda, g.ldb, g.ldc, (const T*)g.bias, (const T*)g.aux, g.ldaux,
                      (T*)g.aux_out, g.part, stagger);
+}
+
+template <typename T, int EPI, int FA, int FB>
+void launch_gemm_f8(const GemmArgs& g, hipStream_t s) {
+  const int tiles = ((g.M + GB_M - 1) / GB_M) * ((g.N + GB_N - 1) / GB_N);
+  hipLaunchKernelGGL((gemm_nt_kernel<T, EPI, false, uint8_t, FA, FB>), dim3(tiles), dim3(G_THREADS), 0, s,
+                     (const uint8_t*)g.A, (const uint8_t*)g.B, (T*)g.C, g.M, g.N, g.K, g.lda, g.ldb, g.ldc,
+                     (const T*)g.bias, (const T*)g.aux, g.ldaux, (T*)g.aux_out, g.part, 0, g.alpha_a, g.alpha_b);
+}
+
+template <typename T, int FA, int FB>
+int gemm_dispatch_f8(const GemmArgs& g, hipStream_t s) {
+  switch (g.epi) {
+    case EPI_NONE: launch_gemm_f8<T, EPI_NONE, FA, FB>(g, s); break;
+    case EPI_BIAS: launch_gemm_f8<T, EPI_BIAS, FA, FB>(g, s); break;
+    case EPI_RESID: launch_gemm_f8<T, EPI_RESID, FA, FB>(g, s); break;
+    case EPI_BIAS_GELU: launch_gemm_f8<T, EPI_BIAS_GELU, FA, FB>(g, s); break;
+    case EPI_BIAS_GELU_TANH: launch_gemm_f8<T, EPI_BIAS_GELU_TANH, FA, FB>(g, s); break;
+    case EPI_DGELU: launch_gemm_f8<T, EPI_DGELU, FA, FB>(g, s); break;
+    case EPI_DGELU_TANH: launch_gemm_f8<T, EPI_DGELU_TANH, FA, FB>(g, s); break;
+    case EPI_BIAS_GELU_D: launch_gemm_f8<T, EPI_BIAS_GELU_D, FA, FB>(g, s); break;
+    case EPI_BIAS_GELU_TANH_D: launch_gemm_f8<T, EPI_BIAS_GELU_TANH_D, FA, FB>(g, s); break;
+    case EPI_MUL: launch_gemm_f8<T, EPI_MUL, FA, FB>(g, s); break;
+    default: return -3;
+  }
+  return (int)hipGetLastError();
 }
 
 template <typename T>
@@ -688,6 +769,24 @@ int gemm_nt(const GemmArgs& g, int dt, hipStream_t s) {
   if (!gemm_supported(g.M, g.N, g.K, g.lda, g.ldb, g.ldc)) return -2;
   if (dt == kBF16Code) return gemm_dispatch<bf16>(g, s);
   if (dt == kF16Code) return gemm_dispatch<f16>(g, s);
+  return -1;
+}
+
+bool gemm_f8_supported(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc) {
+  return M > 0 && N > 0 && K > 0 && K % 128 == 0 && N % 8 == 0 && lda % 16 == 0 && ldb % 16 == 0 && ldc % 8 == 0 &&
+         (int64_t)M * lda < (1ll << 40);
+}
+
+int gemm_nt_f8(const GemmArgs& g, int fmt_a, int fmt_b, int out_dt, hipStream_t s) {
+  // A (activations / gradients): e4m3 (0) or e5m2 (1); B (weights): e4m3
+  if (!gemm_f8_supported(g.M, g.N, g.K, g.lda, g.ldb, g.ldc) || fmt_b != 0 || !g.alpha_a || !g.alpha_b) return -2;
+  if (out_dt == kBF16Code) {
+    if (fmt_a == 0) return gemm_dispatch_f8<bf16, 0, 0>(g, s);
+    if (fmt_a == 1) return gemm_dispatch_f8<bf16, 1, 0>(g, s);
+  } else if (out_dt == kF16Code) {
+    if (fmt_a == 0) return gemm_dispatch_f8<f16, 0, 0>(g, s);
+    if (fmt_a == 1) return gemm_dispatch_f8<f16, 1, 0>(g, s);
+  }
   return -1;
 }
 

@@ -200,10 +200,25 @@ struct GemmArgs {
   float* part;       // [gemm_part_rows(M), N] fp32  EPI_DGELU / EPI_MUL (bias-grad partials)
   int epi;
   int splits;        // gemm_tt: split-K slices (blockIdx.y)
+  const float* alpha_a = nullptr;  // fp8: dequantisation scales (1 / quantisation scale) of A and B,
+  const float* alpha_b = nullptr;  // device scalars; C = epi(alpha_a * alpha_b * A8 . B8^T)
 };
 bool gemm_supported(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc);
 int64_t gemm_part_rows(int M);
 int gemm_nt(const GemmArgs& g, int dt, hipStream_t s);
+// FP8 operands (uint8 storage; fmt 0 = e4m3, 1 = e5m2; B must be e4m3): K % 128 == 0
+bool gemm_f8_supported(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc);
+int gemm_nt_f8(const GemmArgs& g, int fmt_a, int fmt_b, int out_dt, hipStream_t s);
+// fp8.hip: per-tensor scaled quantisation + delayed-scaling bookkeeping (fmt 0 = e4m3, 1 = e5m2)
+// delayed scaling: scale read, amax (optional) accumulated; current scaling (cur != null): scale /
+// scale_inv WRITTEN from smax / cur[0]
+int fp8_quantize(const void* x, uint8_t* y, int64_t n, int dt, int fmt, float* scale, float* scale_inv, float* amax,
+                 const float* cur, float smax, hipStream_t s);
+int fp8_quantize_t(const void* x, uint8_t* y, int R, int C, int dt, int fmt, float* scale, float* scale_inv,
+                   float* amax, const float* cur, float smax, hipStream_t s);
+int fp8_amax(const void* x, int64_t n, int dt, float* amax, hipStream_t s);
+int fp8_update_scales(float* hist, float* amax_cur, float* scale, float* scale_inv, const float* fmt_max,
+                      int n_slots, int hist_len, int idx, float margin_scale, hipStream_t s);
 int gemm_set_dbg(int v);  // diagnostics: 2 = skip the epilogue
 // weight-gradient form: C[P, Q] = A^T B with A [R, P], B [R, Q] row-major (contraction over rows)
 bool gemm_tt_supported(int P, int Q, int R, int splits, int64_t lda, int64_t ldb);

@@ -1,0 +1,361 @@
+"""FP8 kernels on the GPU (csrc/fp8.hip, the fp8 instantiation of csrc/gemm.hip), each against a
+plain PyTorch fp32 reference:
+
+* quantisation: the hardware RNE conversions (after saturation to the format's range) must equal
+  torch's own float8_e4m3fn / float8_e5m2 casts bit for bit; amax is the exact max |x|; the
+  transposing quantiser equals quantise-then-transpose;
+* the scaled-MFMA GEMM (e4m3 x e4m3, e5m2 x e4m3): against the fp32 product of the DEQUANTISED
+  operands (so only accumulation order and the bf16 output rounding differ: tolerance 1e-2 rel),
+  an identity-A layout probe, M / N tails, and every fused epilogue the fp8 path instantiates;
+* delayed scaling: history roll, max over the window, margin, first-use current scaling.
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+F8 = {0: torch.float8_e4m3fn, 1: torch.float8_e5m2}
+FMAX = {0: 448.0, 1: 57344.0}
+
+
+def _C():
+    import apex._ext as e
+
+    return e.require()
+
+
+def _scalar(v):
+    return torch.tensor([v], dtype=torch.float32, device=DEV)
+
+
+def _ref_q(x, s, fmt):
+    m = FMAX[fmt]
+    return (x.float() * s).clamp(-m, m).to(F8[fmt])
+
+
+@pytest.mark.parametrize("fmt", [0, 1])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize("n", [8 * 4096 + 5, 1000, 3])
+def test_quantize_bits_match_torch(fmt, dt, n):
+    C = _C()
+    torch.manual_seed(n)
+    x = (torch.randn(n, device=DEV) * 3).to(dt)
+    x[: min(n, 2)] = torch.tensor([1e4, -7e-4][: min(n, 2)], device=DEV).to(dt)  # saturation + subnormal
+    s = 37.5
+    amax = torch.zeros(1, device=DEV)
+    y = C.fp8_quantize(x, fmt, _scalar(s), amax)
+    assert y.dtype == torch.uint8 and y.shape == x.shape
+    ref = _ref_q(x, s, fmt).view(torch.uint8)
+    assert torch.equal(y, ref), (y != ref).nonzero()[:5]
+    assert float(amax) == float(x.float().abs().max())
+
+
+@pytest.mark.parametrize("R,Cc", [(256, 512), (300, 200), (64, 8)])
+def test_quantize_transposed(R, Cc):
+    C = _C()
+    torch.manual_seed(R)
+    x = torch.randn(R, Cc, device=DEV).bfloat16()
+    amax = torch.zeros(1, device=DEV)
+    yt = C.fp8_quantize_t(x, 0, _scalar(11.0), amax)
+    assert yt.shape == (Cc, R)
+    assert torch.equal(yt, C.fp8_quantize(x, 0, _scalar(11.0)).t().contiguous())
+    assert float(amax) == float(x.float().abs().max())
+
+
+@pytest.mark.parametrize("transpose", [False, True])
+def test_quantize_current_scaling_writes_scale(transpose):
+    """Current scaling: amax measured first, the quantiser derives scale = smax / amax and
+    writes scale and scale_inv (the GEMM's alpha) itself."""
+    C = _C()
+    x = torch.randn(192, 320, device=DEV).bfloat16() * 5
+    amax = torch.zeros(1, device=DEV)
+    C.fp8_amax(x, amax)
+    a = float(x.float().abs().max())
+    assert float(amax) == a
+    scale, sinv = torch.zeros(1, device=DEV), torch.zeros(1, device=DEV)
+    q = C.fp8_quantize_t if transpose else C.fp8_quantize
+    y = q(x, 0, scale, None, amax, sinv, 448.0 * 0.5)
+    assert abs(float(scale) - 224.0 / a) <= 1e-6 * 224.0 / a
+    assert abs(float(sinv) * float(scale) - 1.0) < 1e-6
+    ref = _ref_q(x, float(scale), 0).view(torch.uint8)
+    assert torch.equal(y, ref.t().contiguous() if transpose else ref)
+
+
+def _deq(y8, fmt, inv):
+    return y8.view(F8[fmt]).float() * inv
+
+
+def _operands(M, N, K, fmt_a, seed=0):
+    C = _C()
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    a = torch.randn(M, K, device=DEV, generator=g).bfloat16()
+    b = (torch.randn(N, K, device=DEV, generator=g) * 0.05).bfloat16()
+    sa, sb = FMAX[fmt_a] / float(a.float().abs().max()), 448.0 / float(b.float().abs().max())
+    a8 = C.fp8_quantize(a, fmt_a, _scalar(sa))
+    b8 = C.fp8_quantize(b, 0, _scalar(sb))
+    ia, ib = _scalar(1.0 / sa), _scalar(1.0 / sb)
+    return a8, b8, ia, ib, _deq(a8, fmt_a, 1.0 / sa), _deq(b8, 0, 1.0 / sb)
+
+
+@pytest.mark.parametrize("fmt_a", [0, 1])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 768, 1024), (300, 392, 384), (1000, 1024, 4096)])
+def test_gemm_f8_matches_dequantised_fp32(fmt_a, M, N, K):
+    C = _C()
+    a8, b8, ia, ib, af, bf = _operands(M, N, K, fmt_a, seed=M + N)
+    assert C.gemm_f8_supported(a8, b8)
+    out, _ = C.gemm_f8(a8, b8, ia, ib, fmt_a, C.EPI_NONE)
+    ref = af @ bf.t()
+    assert out.dtype == torch.bfloat16 and out.shape == (M, N)
+    tol = 1e-2 * float(ref.abs().max())
+    torch.testing.assert_close(out.float(), ref, rtol=1e-2, atol=tol)
+
+
+def test_gemm_f8_identity_layout():
+    """A = I picks rows of B: out[m, n] = B[n, m] — pins the operand order and the K packing of
+    the 128-deep scaled MFMA (a swapped or mis-packed operand fails this exactly)."""
+    C = _C()
+    K = 256
+    eye = torch.eye(K, device=DEV).bfloat16()
+    b = torch.randn(384, K, device=DEV).bfloat16()
+    b8 = C.fp8_quantize(b, 0, _scalar(64.0))
+    a8 = C.fp8_quantize(eye, 0, _scalar(1.0))
+    out, _ = C.gemm_f8(a8, b8, _scalar(1.0), _scalar(1.0 / 64.0), 0, C.EPI_NONE)
+    ref = _deq(b8, 0, 1.0 / 64.0).t()
+    torch.testing.assert_close(out.float(), ref, rtol=4e-3, atol=1e-6)
+
+
+def _gelu(h):
+    return 0.5 * h * (1.0 + torch.erf(h / math.sqrt(2.0)))
+
+
+def _dgelu(h):
+    return 0.5 * (1.0 + torch.erf(h / math.sqrt(2.0))) + h * torch.exp(-0.5 * h * h) / math.sqrt(2 * math.pi)
+
+
+def _tanh_gelu(h):
+    c = math.sqrt(2.0 / math.pi)
+    return 0.5 * h * (1.0 + torch.tanh(c * (h + 0.044715 * h ** 3)))
+
+
+@pytest.mark.parametrize("epi", ["bias", "resid", "gelu", "dgelu", "gelu_d", "gelu_tanh_d", "mul"])
+def test_gemm_f8_epilogues(epi):
+    C = _C()
+    M, N, K = 320, 512, 768
+    a8, b8, ia, ib, af, bf = _operands(M, N, K, 0, seed=3)
+    acc = af @ bf.t()
+    bias = (torch.randn(N, device=DEV) * 0.1).bfloat16()
+    aux = torch.randn(M, N, device=DEV).bfloat16()
+    tol = dict(rtol=2e-2, atol=2e-2 * float(acc.abs().max()))
+    if epi == "bias":
+        out, _ = C.gemm_f8(a8, b8, ia, ib, 0, C.EPI_BIAS, bias)
+        torch.testing.assert_close(out.float(), acc + bias.float(), **tol)
+    elif epi == "resid":
+        out, _ = C.gemm_f8(a8, b8, ia, ib, 0, C.EPI_RESID, None, aux)
+        torch.testing.assert_close(out.float(), acc + aux.float(), **tol)
+    elif epi == "gelu":
+        y, h = C.gemm_f8(a8, b8, ia, ib, 0, C.EPI_BIAS_GELU, bias)
+        hr = acc + bias.float()
+        torch.testing.assert_close(h.float(), hr, **tol)
+        torch.testing.assert_close(y.float(), _gelu(hr), **tol)
+    elif epi == "dgelu":
+        dh, db = C.gemm_f8(a8, b8, ia, ib, 0, C.EPI_DGELU, None, aux, torch.float32)
+        ref = acc * _dgelu(aux.float())
+        torch.testing.assert_close(dh.float(), ref, rtol=2e-2, atol=2e-2 * float(ref.abs().max()))
+        torch.testing.assert_close(db, ref.sum(0), rtol=2e-2, atol=2e-2 * float(ref.sum(0).abs().max()))
+    elif epi == "gelu_d":
+        y, g = C.gemm_f8(a8, b8, ia, ib, 0, C.EPI_BIAS_GELU_D, bias)
+        h = acc + bias.float()
+        torch.testing.assert_close(y.float(), _gelu(h), **tol)
+        torch.testing.assert_close(g.float(), _dgelu(h), rtol=2e-2, atol=3e-2)
+    elif epi == "gelu_tanh_d":
+        y, g = C.gemm_f8(a8, b8, ia, ib, 0, C.EPI_BIAS_GELU_TANH_D, bias)
+        h = (acc + bias.float()).requires_grad_(True)
+        yr = _tanh_gelu(h)
+        (gr,) = torch.autograd.grad(yr.sum(), h)
+        torch.testing.assert_close(y.float(), yr.detach(), **tol)
+        torch.testing.assert_close(g.float(), gr, rtol=2e-2, atol=3e-2)
+    else:
+        dh, db = C.gemm_f8(a8, b8, ia, ib, 0, C.EPI_MUL, None, aux, torch.float32)
+        ref = acc * aux.float()
+        torch.testing.assert_close(dh.float(), ref, rtol=2e-2, atol=2e-2 * float(ref.abs().max()))
+        torch.testing.assert_close(db, ref.sum(0), rtol=2e-2, atol=2e-2 * float(ref.sum(0).abs().max()))
+
+
+def test_gemm_f8_batched_activation_and_fp16_out():
+    C = _C()
+    a = torch.randn(4, 96, 256, device=DEV).half()
+    w = (torch.randn(264, 256, device=DEV) * 0.1).half()
+    a8, w8 = C.fp8_quantize(a, 0, _scalar(50.0)), C.fp8_quantize(w, 0, _scalar(1000.0))
+    out, _ = C.gemm_f8(a8, w8, _scalar(1 / 50.0), _scalar(1 / 1000.0), 0, C.EPI_NONE, out_dtype=torch.float16)
+    assert out.shape == (4, 96, 264) and out.dtype == torch.float16
+    ref = _deq(a8, 0, 1 / 50.0) @ _deq(w8, 0, 1 / 1000.0).t()
+    torch.testing.assert_close(out.float(), ref, rtol=1e-2, atol=1e-2 * float(ref.abs().max()))
+
+
+def test_gemm_f8_rejects_unsupported():
+    C = _C()
+    a8 = torch.zeros(64, 100, dtype=torch.uint8, device=DEV)  # K % 128 != 0
+    b8 = torch.zeros(64, 100, dtype=torch.uint8, device=DEV)
+    assert not C.gemm_f8_supported(a8, b8)
+    with pytest.raises(RuntimeError):
+        C.gemm_f8(a8, b8, _scalar(1.0), _scalar(1.0), 0, C.EPI_NONE)
+
+
+def test_update_scales_history_and_margin():
+    C = _C()
+    n, L = 3, 4
+    hist = torch.zeros(n, L, device=DEV)
+    amax = torch.tensor([2.0, 0.0, 8.0], device=DEV)
+    scale = torch.ones(n, device=DEV)
+    sinv = torch.ones(n, device=DEV)
+    fmax = torch.tensor([448.0, 448.0, 57344.0], device=DEV)
+    C.fp8_update_scales(hist, amax, scale, sinv, fmax, n, 0, 0.5)
+    torch.cuda.synchronize()
+    assert torch.allclose(scale, torch.tensor([448.0 / 2 * 0.5, 1.0, 57344.0 / 8 * 0.5], device=DEV))
+    assert torch.allclose(sinv * scale, torch.ones(n, device=DEV))
+    assert float(amax.abs().sum()) == 0.0  # consumed
+    # the window keeps the max of the last L steps
+    amax.copy_(torch.tensor([1.0, 4.0, 1.0], device=DEV))
+    C.fp8_update_scales(hist, amax, scale, sinv, fmax, n, 1, 1.0)
+    assert torch.allclose(scale, torch.tensor([448.0 / 2, 448.0 / 4, 57344.0 / 8], device=DEV))
+    assert torch.equal(hist[:, :2].cpu(), torch.tensor([[2.0, 1.0], [0.0, 4.0], [8.0, 1.0]]))
+
+
+# ----------------------------------------------------------------------------------- training path
+def _rel(a, b):
+    return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12))
+
+
+@pytest.fixture
+def fp8_off():
+    from apex import fp8
+
+    fp8.disable()
+    yield fp8
+    fp8.disable()
+
+
+def test_blocks_fp8_track_bf16(fp8_off):
+    """The BERT sublayers (attention, FFN) with every dense GEMM in fp8 against the same layers in
+    bf16: relative Frobenius error of the outputs below 6% (e4m3 carries 3 mantissa bits: ~3%
+    per-element rounding, averaged down by the K-long sums) and of every gradient below 15% (the
+    output gradient is e5m2 — 2 mantissa bits — and passes through up to three fp8 GEMMs before
+    a weight gradient: 9.4% measured for dWqkv). Training-level agreement is the tiny-BERT
+    loss-curve test below."""
+    from apex.ops import blocks
+
+    fp8 = fp8_off
+    torch.manual_seed(0)
+    B, S, E, H, F = 4, 128, 256, 4, 1024
+    dt = torch.bfloat16
+    x = torch.randn(B, S, E, device=DEV, dtype=dt)
+    mk = lambda *s, sc=0.05: (torch.randn(*s, device=DEV) * sc).to(dt).requires_grad_(True)
+    wqkv, bqkv, wo, bo = mk(3 * E, E), mk(3 * E), mk(E, E), mk(E)
+    w1, b1, w2, b2 = mk(F, E), mk(F), mk(E, F), mk(E)
+    g1, be1 = (torch.ones(E, device=DEV, dtype=dt).requires_grad_(True), torch.zeros(E, device=DEV, dtype=dt).requires_grad_(True))
+    g2, be2 = (torch.ones(E, device=DEV, dtype=dt).requires_grad_(True), torch.zeros(E, device=DEV, dtype=dt).requires_grad_(True))
+    params = [wqkv, bqkv, wo, bo, w1, b1, w2, b2, g1, be1, g2, be2]
+
+    def run():
+        xi = x.clone().requires_grad_(True)
+        h = blocks.attention_sublayer(xi, wqkv, bqkv, wo, bo, g1, be1, H)
+        y = blocks.ffn_sublayer(h, w1, b1, w2, b2, g2, be2)
+        assert y is not None
+        dy = torch.randn(y.shape, device=DEV, generator=torch.Generator(device=DEV).manual_seed(3)).to(dt)
+        grads = torch.autograd.grad(y, [xi] + params, dy)
+        return y.detach(), grads
+
+    y_ref, g_ref = run()
+    with fp8.fp8_autocast():
+        y8, g8 = run()
+    st = fp8.state()
+    assert st.n >= 4 * 3 - 1, st.slots  # four weights: w, x, dy slots each (the first layer's dy too)
+    assert _rel(y8, y_ref) < 0.06
+    for i, (a, b) in enumerate(zip(g8, g_ref)):
+        assert _rel(a, b) < 0.15, (i, _rel(a, b))
+    # delayed scaling: after an update the second pass uses history scales, same accuracy
+    fp8.step()
+    with fp8.fp8_autocast():
+        y8b, g8b = run()
+    assert _rel(y8b, y_ref) < 0.06
+    assert _rel(g8b[0], g_ref[0]) < 0.15
+
+
+def test_weight_cache_invalidated_by_step(fp8_off):
+    from apex.ops import fused
+
+    fp8 = fp8_off
+    torch.manual_seed(1)
+    x = torch.randn(256, 256, device=DEV).bfloat16()
+    w = (torch.randn(512, 256, device=DEV) * 0.05).bfloat16()
+    with fp8.fp8_autocast():
+        y0 = fused.fused_dense(x, w)
+        w.mul_(2.0)  # an in-place optimizer update between steps (no version bump seen by us)
+        y_stale = fused.fused_dense(x, w)  # same step: cached codes (documented contract)
+        fp8.step()
+        y1 = fused.fused_dense(x, w)
+    torch.testing.assert_close(y_stale, y0)
+    assert _rel(y1, 2 * y0.float()) < 0.02
+
+
+def _tiny_bert_losses(use_fp8, steps=40):
+    from apex import amp, fp8
+    from apex.amp._amp_state import _amp_state
+    from apex.models.bert import BertConfig, BertForPreTraining, synthetic_batch
+    from apex.optimizers import FusedAdam
+
+    _amp_state.optimizers, _amp_state.loss_scalers = [], []
+    fp8.disable()
+    torch.manual_seed(5)
+    cfg = BertConfig(vocab_size=1000, hidden_size=256, num_hidden_layers=2, num_attention_heads=4,
+                     intermediate_size=1024, max_position_embeddings=128, hidden_dropout_prob=0.0,
+                     attention_probs_dropout_prob=0.0)
+    model = BertForPreTraining(cfg).to(DEV)
+    opt = FusedAdam(model.parameters(), lr=1e-3)
+    model, opt = amp.initialize(model, opt, opt_level="O2", cast_model_type=torch.bfloat16, verbosity=0,
+                                fp8=use_fp8)
+    g = torch.Generator(device=DEV).manual_seed(9)
+    batch = synthetic_batch(cfg, 32, 128, device=DEV, generator=g)
+    losses = []
+    for _ in range(steps):
+        loss = model(**batch)
+        with amp.scale_loss(loss, opt) as sl:
+            sl.backward()
+        opt.step()
+        opt.zero_grad()
+        losses.append(float(loss))
+    n_slots = fp8.state().n if use_fp8 else 0
+    fp8.disable()
+    return losses, n_slots
+
+
+def test_tiny_bert_fp8_loss_tracks_bf16():
+    """amp O2 + fp8=True: the loss curve of a 2-layer BERT (hidden 256, FFN 1024) memorising one
+    batch follows the bf16 curve within 5% at every step after the first few, and falls."""
+    ref, _ = _tiny_bert_losses(False)
+    got, n_slots = _tiny_bert_losses(True)
+    assert n_slots >= 2 * 4 * 3  # 2 layers x 4 dense weights x (w, x, dy)
+    assert got[-1] < 0.7 * got[0]
+    for i in range(5, len(ref)):
+        assert abs(got[i] - ref[i]) <= 0.05 * ref[i] + 0.05, (i, got[i], ref[i])
+
+
+def test_state_dict_roundtrip(fp8_off):
+    from apex.ops import fused
+
+    fp8 = fp8_off
+    lin = torch.nn.Linear(256, 512).to(DEV).bfloat16()
+    x = torch.randn(128, 256, device=DEV).bfloat16().requires_grad_(True)
+    with fp8.fp8_autocast():
+        fused.fused_dense(x, lin.weight, lin.bias).sum().backward()
+    fp8.step()
+    sd = fp8.state().state_dict(lin)
+    assert {"weight:w", "weight:x", "weight:dy"} <= set(sd["slots"])
+    scale_x = sd["slots"]["weight:x"]["scale"]
+    fp8.disable()
+    st = fp8.state()
+    st.load_state_dict(sd, lin)
+    s = st.slots[(id(lin.weight), "x")]
+    assert float(st.scale[s]) == scale_x and s not in st._fresh

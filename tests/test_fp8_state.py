@@ -1,0 +1,97 @@
+"""apex.fp8 bookkeeping on the CPU (no kernels): recipe validation, slot allocation and growth,
+the autocast / global switches, amp.initialize(fp8=...) wiring and the checkpoint format.
+The kernels and the training path are covered on the GPU by tests/test_fp8_gpu.py."""
+import pytest
+import torch
+
+from apex import fp8
+
+
+@pytest.fixture(autouse=True)
+def _reset():
+    fp8.disable()
+    yield
+    fp8.disable()
+
+
+def test_recipe_formats():
+    r = fp8.Fp8Recipe()
+    assert (r.fmt("fwd"), r.fmt("bwd")) == (fp8.E4M3, fp8.E5M2)
+    with pytest.raises(ValueError):
+        fp8.Fp8Recipe(fwd_format="e3m4").fmt("fwd")
+
+
+def test_slots_grow_and_keep_values():
+    st = fp8.Fp8State(fp8.Fp8Recipe(amax_history_len=4), device="cpu")
+    keys = [(i, "x") for i in range(300)]
+    for i, k in enumerate(keys):
+        s = st.slot(k, fp8.E4M3 if i % 2 == 0 else fp8.E5M2)
+        st.scale[s] = float(i + 1)
+    assert st.n == 300 and st._cap >= 300 and st.hist.shape == (st._cap, 4)
+    for i, k in enumerate(keys):
+        s = st.slots[k]
+        assert float(st.scale[s]) == i + 1
+        assert float(st.fmax[s]) == (448.0 if i % 2 == 0 else 57344.0)
+    assert st.slot(keys[5], fp8.E4M3) == st.slots[keys[5]]  # stable
+
+
+def test_autocast_and_global_switch():
+    assert fp8.active() is None
+    with fp8.fp8_autocast(device="cpu") as st:
+        assert fp8.active() is st
+        with fp8.fp8_autocast(device="cpu"):
+            assert fp8.active() is st  # same recipe: same state
+        assert fp8.active() is st
+    assert fp8.active() is None
+    with fp8.fp8_autocast(enabled=False):
+        assert fp8.active() is None
+    st = fp8.enable(device="cpu")
+    assert fp8.active() is st
+    fp8.disable()
+    assert fp8.active() is None
+
+
+def test_new_recipe_resets_state():
+    a = fp8.state(fp8.Fp8Recipe(), device="cpu")
+    assert fp8.state(fp8.Fp8Recipe(), device="cpu") is a  # equal recipe
+    b = fp8.state(fp8.Fp8Recipe(margin=1), device="cpu")
+    assert b is not a and b.smax_scale == 0.5
+
+
+def test_amp_initialize_fp8_flag_and_step_hook():
+    from apex import amp
+    from apex.amp._amp_state import _amp_state
+
+    _amp_state.optimizers, _amp_state.loss_scalers = [], []
+    model = torch.nn.Linear(8, 8)
+    opt = torch.optim.SGD(model.parameters(), lr=0.1)
+    model, opt = amp.initialize(model, opt, opt_level="O0", verbosity=0, fp8=True)
+    st = fp8.active()
+    assert st is not None and _amp_state.fp8
+    model(torch.randn(2, 8)).sum().backward()
+    opt.step()
+    assert st.steps == 1 and st.gen == 1  # the patched step ran apex.fp8.step()
+    _amp_state.optimizers, _amp_state.loss_scalers = [], []
+    model2 = torch.nn.Linear(8, 8)
+    opt2 = torch.optim.SGD(model2.parameters(), lr=0.1)
+    amp.initialize(model2, opt2, opt_level="O0", verbosity=0)
+    assert fp8.active() is None  # re-initialising without fp8 turns it off
+
+
+def test_state_dict_by_parameter_name():
+    lin = torch.nn.Linear(4, 4)
+    st = fp8.Fp8State(device="cpu")
+    sw = st.slot((id(lin.weight), "w"), fp8.E4M3)
+    sx = st.slot((id(lin.weight), "x"), fp8.E4M3)
+    st.slot((12345, "x"), fp8.E4M3)  # not a parameter of lin: dropped from the named dict
+    st.scale[sx] = 3.0
+    st.hist[sx, 0] = 7.0
+    st._fresh.discard(sx)
+    sd = st.state_dict(lin)
+    assert set(sd["slots"]) == {"weight:w", "weight:x"}
+    st2 = fp8.Fp8State(device="cpu")
+    st2.load_state_dict(sd, lin)
+    s2 = st2.slots[(id(lin.weight), "x")]
+    assert float(st2.scale[s2]) == 3.0 and float(st2.hist[s2, 0]) == 7.0
+    assert s2 not in st2._fresh and st2.slots[(id(lin.weight), "w")] in st2._fresh
+    del sw
