@@ -643,7 +643,7 @@ std::vector<int64_t> bn_dims(const Tensor& x, bool nhwc) {
 Tensor k_bn_local_stats(Tensor x, bool nhwc) {
   TORCH_CHECK(x.is_contiguous(), "syncbn: input must be contiguous in its layout");
   auto d = bn_dims(x, nhwc);
-  const int sp = apex::bn_splits_for(d[0], d[1], d[2]);
+  const int sp = apex::bn_splits_for(d[0], d[1], d[2], nhwc, dt_code(x.scalar_type()));
   auto fo = x.options().dtype(at::kFloat);
   Tensor part = at::empty({d[1] * sp * 3}, fo);
   int spo = 0;
@@ -677,8 +677,10 @@ Tensor k_bn_elemt(Tensor x, Tensor mean, Tensor invstd, const c10::optional<Tens
   auto d = bn_dims(x, nhwc);
   Tensor y = at::empty_like(x);
   const int wdt = w.has_value() && w->defined() ? dt_code(w->scalar_type()) : apex::kF32Code;
+  Tensor coef = at::empty({2 * d[1] + 4}, x.options().dtype(at::kFloat));
   check(apex::bn_elemt(x.data_ptr(), mean.data_ptr<float>(), invstd.data_ptr<float>(), opt_vptr(w), opt_vptr(b),
-                       y.data_ptr(), d[0], d[1], d[2], nhwc, relu, dt_code(x.scalar_type()), wdt, cur_stream()),
+                       y.data_ptr(), d[0], d[1], d[2], nhwc, relu, dt_code(x.scalar_type()), wdt,
+                       coef.data_ptr<float>(), cur_stream()),
         "bn_elemt");
   return y;
 }
@@ -687,7 +689,7 @@ Tensor k_bn_elemt(Tensor x, Tensor mean, Tensor invstd, const c10::optional<Tens
 Tensor k_bn_bwd_reduce(Tensor dy, Tensor x, Tensor mean, bool nhwc) {
   auto d = bn_dims(x, nhwc);
   Tensor dyc = dy.contiguous();
-  const int sp = apex::bn_splits_for(d[0], d[1], d[2]);
+  const int sp = apex::bn_splits_for(d[0], d[1], d[2], nhwc, dt_code(x.scalar_type()));
   auto fo = x.options().dtype(at::kFloat);
   Tensor part = at::empty({d[1] * sp * 2}, fo);
   Tensor out = at::empty({2, d[1]}, fo);
@@ -706,11 +708,12 @@ Tensor k_bn_bwd_elemt(Tensor dy, Tensor x, Tensor mean, Tensor invstd, const c10
   Tensor dyc = dy.contiguous();
   Tensor dx = at::empty_like(x);
   Tensor sc = sums.contiguous();
+  Tensor coef = at::empty({3 * d[1] + 4}, x.options().dtype(at::kFloat));
   const int wdt = w.has_value() && w->defined() ? dt_code(w->scalar_type()) : apex::kF32Code;
   check(apex::bn_bwd_elemt(dyc.data_ptr(), x.data_ptr(), mean.data_ptr<float>(), invstd.data_ptr<float>(),
                            opt_vptr(w), sc.data_ptr<float>(), sc.data_ptr<float>() + d[1],
                            count.data_ptr<float>(), dx.data_ptr(), d[0], d[1], d[2], nhwc,
-                           dt_code(x.scalar_type()), wdt, cur_stream()),
+                           dt_code(x.scalar_type()), wdt, coef.data_ptr<float>(), cur_stream()),
         "bn_bwd_elemt");
   return dx;
 }

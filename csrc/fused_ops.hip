@@ -268,7 +268,11 @@ __global__ void __launch_bounds__(kEwBlock) bdaln_fwd_kernel(const T* __restrict
   }
 }
 
-// part rows: [dgamma | dbeta | dbias] (3*cols floats) per block
+// part rows: [dgamma | dbeta | dbias] (3*cols floats) per block.
+// Each wave walks `rows_per_wave` rows (4 waves interleaved per block); the NEXT row's s / dy are
+// loaded into registers (raw 16-byte packs) before the current row's reduction and stores, so every
+// wave keeps two rows of loads in flight — with one row per wave the kernel was latency-bound at
+// ~4.2 TB/s (rocprofv3 FETCH/WRITE_SIZE, profiles/r2_pmc_bw_kernels.json).
 template <typename T, typename W, int VPT, bool DROP>
 __global__ void __launch_bounds__(kEwBlock) bdaln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ s,
                                                             const W* __restrict__ gamma,
@@ -293,18 +297,37 @@ __global__ void __launch_bounds__(kEwBlock) bdaln_bwd_kernel(const T* __restrict
     if (j * 64 + lane < nvec) load_f<W, 8>(gamma + (j * 64 + lane) * 8, g[j]);
   }
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_wave * 4;
+  typedef Pack<T, 8> P8;
+  P8 ns[VPT], nd[VPT];
+  auto fetch = [&](int64_t row) {
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int vi = j * 64 + lane;
+      if (vi < nvec && row < rows) {
+        ns[j] = *reinterpret_cast<const P8*>(s + row * cols + vi * 8);
+        nd[j] = *reinterpret_cast<const P8*>(dy + row * cols + vi * 8);
+      }
+    }
+  };
+  fetch(r0 + wid);
   for (int rr = 0; rr < rows_per_wave; ++rr) {
     const int64_t row = r0 + (int64_t)rr * 4 + wid;
     if (row >= rows) break;
-    const float mu = mean[row], rs = rstd[row];
     float xh[VPT][8], dv[VPT][8];
+#pragma unroll
+    for (int j = 0; j < VPT; ++j)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        xh[j][k] = to_f(ns[j].v[k]);
+        dv[j][k] = to_f(nd[j].v[k]);
+      }
+    if (rr + 1 < rows_per_wave) fetch(row + 4);
+    const float mu = mean[row], rs = rstd[row];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int j = 0; j < VPT; ++j) {
       const int vi = j * 64 + lane;
       if (vi < nvec) {
-        load_f<T, 8>(s + row * cols + vi * 8, xh[j]);
-        load_f<T, 8>(dy + row * cols + vi * 8, dv[j]);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           xh[j][k] = (xh[j][k] - mu) * rs;
@@ -556,7 +579,9 @@ int bdaln_fwd(const void* x, const void* b, const void* res, const void* gamma, 
   return (int)hipGetLastError();
 }
 
-constexpr int kBdalnMaxParts = 512;
+// 768 blocks = 3 per CU (the 48 KB combine buffer at cols 1024 allows 3): 12 waves per CU, each
+// with two rows of loads in flight
+constexpr int kBdalnMaxParts = 768;
 static inline int bdaln_rpw(int64_t rows) {
   const int64_t r = (rows + 4 * kBdalnMaxParts - 1) / (4 * kBdalnMaxParts);
   return r < 1 ? 1 : (int)r;

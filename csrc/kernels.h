@@ -154,18 +154,18 @@ int gru_cell_fwd(const void* ig, const void* hg, const void* bih, const void* bh
                  float* ws, int64_t B, int64_t H, int dt, hipStream_t s);
 int gru_cell_bwd(const void* dhy, const void* hx, const float* ws, void* dig, void* dhg, void* dhx, int64_t B,
                  int64_t H, int dt, hipStream_t s);
-int bn_splits_for(int64_t N, int64_t C, int64_t S);
+int bn_splits_for(int64_t N, int64_t C, int64_t S, int nhwc, int dt);
 int bn_stats(const void* x, float* part, int64_t N, int64_t C, int64_t S, int nhwc, int dt, int* splits_out,
              hipStream_t s);
 int bn_combine(const float* in, int groups, int64_t C, int gmajor, float* mean, float* var, float* count,
                hipStream_t s);
 int bn_elemt(const void* x, const float* mean, const float* invstd, const void* w, const void* b, void* y,
-             int64_t N, int64_t C, int64_t S, int nhwc, int relu, int dt, int wdt, hipStream_t s);
+             int64_t N, int64_t C, int64_t S, int nhwc, int relu, int dt, int wdt, float* coef, hipStream_t s);
 int bn_bwd_reduce(const void* dy, const void* x, const float* mean, float* part, float* sum_dy,
                   float* sum_dy_xmu, int64_t N, int64_t C, int64_t S, int nhwc, int dt, hipStream_t s);
 int bn_bwd_elemt(const void* dy, const void* x, const float* mean, const float* invstd, const void* w,
                  const float* sum_dy, const float* sum_dy_xmu, const float* count, void* dx, int64_t N, int64_t C,
-                 int64_t S, int nhwc, int dt, int wdt, hipStream_t s);
+                 int64_t S, int nhwc, int dt, int wdt, float* coef, hipStream_t s);
 
 // ----------------------------- fused scale-mask softmax --------------------
 // mode 0: scale only, 1: byte mask [B, mask_heads, sq, cols] (nonzero masked), 2: causal

@@ -14,7 +14,7 @@
 namespace apex {
 
 constexpr int kLnBlock = 256;
-constexpr int kMaxBwdParts = 512;  // ~2 blocks per CU; rows per wave adapts to reach it
+constexpr int kMaxBwdParts = 768;  // 3 blocks per CU; rows per wave adapts to reach it
 
 template <typename T, typename W, int VPT, bool RMS>
 __global__ void __launch_bounds__(kLnBlock) ln_fwd_fast(const T* __restrict__ x,
@@ -112,21 +112,41 @@ __global__ void __launch_bounds__(kLnBlock) ln_bwd_fast(const T* __restrict__ dy
   }
   const int64_t rows_per_block = (int64_t)rpw * (kLnBlock / 64);
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  // the next row's x / dy are loaded (raw 16-byte packs) before this row's reduction and stores:
+  // two rows of loads in flight per wave (one row per wave left the kernel latency-bound at
+  // ~3.9 TB/s, profiles/r2_pmc_bw_kernels.json)
+  typedef Pack<T, 8> P8;
+  P8 nx[VPT], nd[VPT];
+  auto fetch = [&](int64_t row) {
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int vi = j * 64 + lane;
+      if (vi < nvec && row < rows) {
+        nx[j] = *reinterpret_cast<const P8*>(x + row * cols + vi * 8);
+        nd[j] = *reinterpret_cast<const P8*>(dy + row * cols + vi * 8);
+      }
+    }
+  };
+  fetch(r0 + wid);
   for (int rr = 0; rr < rpw; ++rr) {
     const int64_t row = r0 + (int64_t)rr * (kLnBlock / 64) + wid;
     if (row >= rows) break;
+    float xh[VPT][8], dv[VPT][8];
+#pragma unroll
+    for (int j = 0; j < VPT; ++j)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        xh[j][k] = to_f(nx[j].v[k]);
+        dv[j][k] = to_f(nd[j].v[k]);
+      }
+    if (rr + 1 < rpw) fetch(row + (kLnBlock / 64));
     const float mu = RMS ? 0.f : mean[row];
     const float rs = rstd[row];
-    const T* xr = x + row * cols;
-    const T* dyr = dy + row * cols;
-    float xh[VPT][8], dv[VPT][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int j = 0; j < VPT; ++j) {
       const int vi = j * 64 + lane;
       if (vi < nvec) {
-        load_f<T, 8>(xr + vi * 8, xh[j]);
-        load_f<T, 8>(dyr + vi * 8, dv[j]);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           xh[j][k] = (xh[j][k] - mu) * rs;

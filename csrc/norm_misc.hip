@@ -425,7 +425,427 @@ __global__ void __launch_bounds__(256) bn_bwd_elemt_kernel(const T* __restrict__
   }
 }
 
-static inline int bn_splits(int64_t N, int64_t S, int64_t C) {
+// ---------------------------------------------------------------------------
+// Vectorised SyncBN kernels (16-byte accesses: VEC = 8 for 16-bit data, 4 for fp32). The scalar
+// kernels above (one 2-byte element per thread, 64-bit div/mod per element) ran at 1.1-2.7 TB/s
+// by rocprofv3 FETCH/WRITE_SIZE (profiles/r2_pmc_bw_kernels.json) and NHWC's per-channel strided
+// gather was worse; they remain for shapes these do not take (plane or channel count not a
+// multiple of VEC, misaligned views).
+//
+//  NCHW: a vector = VEC consecutive elements of one channel plane (needs S % VEC == 0).
+//  NHWC: a vector = VEC consecutive channels of one row (needs C % VEC == 0); a block covers
+//        cvb channel vectors x rpb row lanes and combines its row lanes through LDS.
+// Partials keep the layouts of the scalar kernels: Welford triples part[(c*splits + y)*3] for
+// bn_combine, (sum_dy, sum_dy_xmu) pairs part[(c*splits + y)*2] for bn_bwd_finalize.
+// ---------------------------------------------------------------------------
+template <typename T>
+struct BnVec {
+  static constexpr int V = 16 / (int)sizeof(T);
+  typedef Pack<T, V> P;
+};
+
+// Welford merge of a VEC-element chunk given its sum / sum of squared deviations
+__device__ __forceinline__ void wf_add_chunk(Welford& w, float csum, float cm2, float cn) {
+  w = wf_merge(w, Welford{csum / cn, cm2, cn});
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) bn_stats_nchw_vec(const T* __restrict__ x, float* __restrict__ part,
+                                                        int N, int C, int S) {
+  constexpr int V = BnVec<T>::V;
+  typedef typename BnVec<T>::P P;
+  __shared__ float sm[3][4];
+  const int c = blockIdx.x;
+  const int SV = S / V;
+  const int total = N * SV;
+  const int per = (total + gridDim.y - 1) / gridDim.y;
+  const int e0 = blockIdx.y * per, e1 = min(e0 + per, total);
+  Welford w{0.f, 0.f, 0.f};
+  for (int e = e0 + threadIdx.x; e < e1; e += 256) {
+    const int n = e / SV, sv = e - n * SV;
+    const P pk = *reinterpret_cast<const P*>(x + ((int64_t)n * C + c) * S + (int64_t)sv * V);
+    float v[V], cs = 0.f;
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      v[k] = to_f(pk.v[k]);
+      cs += v[k];
+    }
+    const float cm = cs * (1.f / V);
+    float m2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < V; ++k) m2 += (v[k] - cm) * (v[k] - cm);
+    wf_add_chunk(w, cs, m2, (float)V);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    Welford b{__shfl_xor(w.mean, o, 64), __shfl_xor(w.m2, o, 64), __shfl_xor(w.n, o, 64)};
+    w = wf_merge(w, b);
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) {
+    sm[0][wid] = w.mean;
+    sm[1][wid] = w.m2;
+    sm[2][wid] = w.n;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    Welford t{sm[0][0], sm[1][0], sm[2][0]};
+    for (int k = 1; k < 4; ++k) t = wf_merge(t, Welford{sm[0][k], sm[1][k], sm[2][k]});
+    float* p = part + ((int64_t)c * gridDim.y + blockIdx.y) * 3;
+    p[0] = t.mean;
+    p[1] = t.m2;
+    p[2] = t.n;
+  }
+}
+
+// NHWC: rows R = N*S of C channels. Thread (cv, rl): channel vector cv, rows rl, rl + rpb*splits, ...
+template <typename T>
+__global__ void __launch_bounds__(256) bn_stats_nhwc_vec(const T* __restrict__ x, float* __restrict__ part,
+                                                        int64_t R, int C, int cvb, int rpb) {
+  constexpr int V = BnVec<T>::V;
+  typedef typename BnVec<T>::P P;
+  __shared__ float sm[256 * V * 2 + 256];
+  const int CV = C / V;
+  const int tc = threadIdx.x % cvb, tr = threadIdx.x / cvb;
+  const int cv = blockIdx.x * cvb + tc;
+  const bool act = tr < rpb && cv < CV;
+  float mean[V], m2[V], n = 0.f;
+#pragma unroll
+  for (int k = 0; k < V; ++k) mean[k] = m2[k] = 0.f;
+  if (act) {
+    const int64_t step = (int64_t)rpb * gridDim.y;
+    int64_t r = (int64_t)blockIdx.y * rpb + tr;
+    // two rows per iteration: two independent 16-byte loads in flight per thread
+    for (; r + step < R; r += 2 * step) {
+      const P a = *reinterpret_cast<const P*>(x + r * C + (int64_t)cv * V);
+      const P b = *reinterpret_cast<const P*>(x + (r + step) * C + (int64_t)cv * V);
+      n += 1.f;
+      float inv = 1.f / n;
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        const float v = to_f(a.v[k]), d = v - mean[k];
+        mean[k] += d * inv;
+        m2[k] += d * (v - mean[k]);
+      }
+      n += 1.f;
+      inv = 1.f / n;
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        const float v = to_f(b.v[k]), d = v - mean[k];
+        mean[k] += d * inv;
+        m2[k] += d * (v - mean[k]);
+      }
+    }
+    if (r < R) {
+      const P a = *reinterpret_cast<const P*>(x + r * C + (int64_t)cv * V);
+      n += 1.f;
+      const float inv = 1.f / n;
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        const float v = to_f(a.v[k]), d = v - mean[k];
+        mean[k] += d * inv;
+        m2[k] += d * (v - mean[k]);
+      }
+    }
+  }
+  // combine the rpb row lanes of every channel vector
+  float* smean = sm;
+  float* sm2 = sm + 256 * V;
+  float* sn = sm + 512 * V;
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    smean[threadIdx.x * V + k] = mean[k];
+    sm2[threadIdx.x * V + k] = m2[k];
+  }
+  sn[threadIdx.x] = n;
+  __syncthreads();
+  if (tr == 0 && cv < CV) {
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      Welford t{smean[tc * V + k], sm2[tc * V + k], sn[tc]};
+      for (int q = 1; q < rpb; ++q) {
+        const int id = q * cvb + tc;
+        t = wf_merge(t, Welford{smean[id * V + k], sm2[id * V + k], sn[id]});
+      }
+      float* p = part + ((int64_t)(cv * V + k) * gridDim.y + blockIdx.y) * 3;
+      p[0] = t.mean;
+      p[1] = t.m2;
+      p[2] = t.n;
+    }
+  }
+}
+
+// per-channel affine coefficients of the elementwise passes (one thread per channel):
+//   forward   y  = x * k0 + k1                     k0 = w * invstd, k1 = b - mean * k0
+//   backward  dx = dy * k0 + x * k1 + k2           k0 = w * invstd, k1 = -k0 * invstd^2 * mdx,
+//                                                  k2 = k0 * (mean * invstd^2 * mdx - mdy)
+// so the vector kernels load 2-3 floats per channel instead of recomputing from 4-7 inputs.
+template <typename W>
+__global__ void bn_coef_fwd_kernel(const float* __restrict__ mean, const float* __restrict__ invstd,
+                                   const W* __restrict__ w, const W* __restrict__ b, float* __restrict__ k, int C) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  const float k0 = (w ? to_f(w[c]) : 1.f) * invstd[c];
+  k[c] = k0;
+  k[C + c] = (b ? to_f(b[c]) : 0.f) - mean[c] * k0;
+}
+
+template <typename W>
+__global__ void bn_coef_bwd_kernel(const float* __restrict__ mean, const float* __restrict__ invstd,
+                                   const W* __restrict__ w, const float* __restrict__ sum_dy,
+                                   const float* __restrict__ sum_dy_xmu, const float* __restrict__ count,
+                                   float* __restrict__ k, int C) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  const float is = invstd[c], ic = 1.f / fmaxf(count[c], 1.f);
+  const float mdy = sum_dy[c] * ic, mdx = sum_dy_xmu[c] * ic;
+  const float k0 = (w ? to_f(w[c]) : 1.f) * is;
+  const float q = is * is * mdx;
+  k[c] = k0;
+  k[C + c] = -k0 * q;
+  k[2 * C + c] = k0 * (mean[c] * q - mdy);
+}
+
+template <int V>
+__device__ __forceinline__ void load_coef(const float* __restrict__ k, int c0, float (&o)[V]) {
+  if constexpr (V == 8) {
+    const float4 a = *reinterpret_cast<const float4*>(k + c0);
+    const float4 b = *reinterpret_cast<const float4*>(k + c0 + 4);
+    o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+  } else {
+    const float4 a = *reinterpret_cast<const float4*>(k + c0);
+    o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w;
+  }
+}
+
+// nvec < 2^31 (checked by the launcher): 32-bit index math
+template <typename T>
+__global__ void __launch_bounds__(256) bn_elemt_vec(const T* __restrict__ x, const float* __restrict__ k,
+                                                   T* __restrict__ y, int nvec, int C, int S, int nhwc, int relu) {
+  constexpr int V = BnVec<T>::V;
+  typedef typename BnVec<T>::P P;
+  const int SV = S / V, CV = C / V;
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < nvec; e += gridDim.x * 256) {
+    const P pk = *reinterpret_cast<const P*>(x + (int64_t)e * V);
+    P o;
+    if (nhwc) {
+      const int c0 = (e % CV) * V;
+      float k0[V], k1[V];
+      load_coef<V>(k, c0, k0);
+      load_coef<V>(k + C, c0, k1);
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        float v = to_f(pk.v[i]) * k0[i] + k1[i];
+        if (relu) v = fmaxf(v, 0.f);
+        o.v[i] = from_f<T>(v);
+      }
+    } else {
+      const int c = (e / SV) % C;
+      const float k0 = k[c], k1 = k[C + c];
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        float v = to_f(pk.v[i]) * k0 + k1;
+        if (relu) v = fmaxf(v, 0.f);
+        o.v[i] = from_f<T>(v);
+      }
+    }
+    *reinterpret_cast<P*>(y + (int64_t)e * V) = o;
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) bn_bwd_reduce_nchw_vec(const T* __restrict__ dy, const T* __restrict__ x,
+                                                             const float* __restrict__ mean,
+                                                             float* __restrict__ part, int N, int C, int S) {
+  constexpr int V = BnVec<T>::V;
+  typedef typename BnVec<T>::P P;
+  __shared__ float red[4];
+  const int c = blockIdx.x;
+  const int SV = S / V;
+  const int total = N * SV;
+  const int per = (total + gridDim.y - 1) / gridDim.y;
+  const int e0 = blockIdx.y * per, e1 = min(e0 + per, total);
+  const float mu = mean[c];
+  float s1 = 0.f, s2 = 0.f;
+  for (int e = e0 + threadIdx.x; e < e1; e += 256) {
+    const int n = e / SV, sv = e - n * SV;
+    const int64_t off = ((int64_t)n * C + c) * S + (int64_t)sv * V;
+    const P d = *reinterpret_cast<const P*>(dy + off);
+    const P xv = *reinterpret_cast<const P*>(x + off);
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      const float g = to_f(d.v[k]);
+      s1 += g;
+      s2 += g * (to_f(xv.v[k]) - mu);
+    }
+  }
+  s1 = block_sum(s1, red);
+  s2 = block_sum(s2, red);
+  if (threadIdx.x == 0) {
+    part[((int64_t)c * gridDim.y + blockIdx.y) * 2] = s1;
+    part[((int64_t)c * gridDim.y + blockIdx.y) * 2 + 1] = s2;
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) bn_bwd_reduce_nhwc_vec(const T* __restrict__ dy, const T* __restrict__ x,
+                                                             const float* __restrict__ mean,
+                                                             float* __restrict__ part, int64_t R, int C, int cvb,
+                                                             int rpb) {
+  constexpr int V = BnVec<T>::V;
+  typedef typename BnVec<T>::P P;
+  __shared__ float sm[256 * V * 2];
+  const int CV = C / V;
+  const int tc = threadIdx.x % cvb, tr = threadIdx.x / cvb;
+  const int cv = blockIdx.x * cvb + tc;
+  float s1[V], s2[V], mu[V];
+#pragma unroll
+  for (int k = 0; k < V; ++k) s1[k] = s2[k] = 0.f;
+  if (tr < rpb && cv < CV) {
+#pragma unroll
+    for (int k = 0; k < V; ++k) mu[k] = mean[cv * V + k];
+    const int64_t step = (int64_t)rpb * gridDim.y;
+    for (int64_t r = (int64_t)blockIdx.y * rpb + tr; r < R; r += step) {
+      const P d = *reinterpret_cast<const P*>(dy + r * C + (int64_t)cv * V);
+      const P xv = *reinterpret_cast<const P*>(x + r * C + (int64_t)cv * V);
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        const float g = to_f(d.v[k]);
+        s1[k] += g;
+        s2[k] += g * (to_f(xv.v[k]) - mu[k]);
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    sm[threadIdx.x * V + k] = s1[k];
+    sm[256 * V + threadIdx.x * V + k] = s2[k];
+  }
+  __syncthreads();
+  if (tr == 0 && cv < CV) {
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      float a = 0.f, bb = 0.f;
+      for (int q = 0; q < rpb; ++q) {
+        const int id = q * cvb + tc;
+        a += sm[id * V + k];
+        bb += sm[256 * V + id * V + k];
+      }
+      float* p = part + ((int64_t)(cv * V + k) * gridDim.y + blockIdx.y) * 2;
+      p[0] = a;
+      p[1] = bb;
+    }
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) bn_bwd_elemt_vec(const T* __restrict__ dy, const T* __restrict__ x,
+                                                       const float* __restrict__ k, T* __restrict__ dx, int nvec,
+                                                       int C, int S, int nhwc) {
+  constexpr int V = BnVec<T>::V;
+  typedef typename BnVec<T>::P P;
+  const int SV = S / V, CV = C / V;
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < nvec; e += gridDim.x * 256) {
+    const P d = *reinterpret_cast<const P*>(dy + (int64_t)e * V);
+    const P xv = *reinterpret_cast<const P*>(x + (int64_t)e * V);
+    P o;
+    if (nhwc) {
+      const int c0 = (e % CV) * V;
+      float k0[V], k1[V], k2[V];
+      load_coef<V>(k, c0, k0);
+      load_coef<V>(k + C, c0, k1);
+      load_coef<V>(k + 2 * C, c0, k2);
+#pragma unroll
+      for (int i = 0; i < V; ++i) o.v[i] = from_f<T>(to_f(d.v[i]) * k0[i] + to_f(xv.v[i]) * k1[i] + k2[i]);
+    } else {
+      const int c = (e / SV) % C;
+      const float k0 = k[c], k1 = k[C + c], k2 = k[2 * C + c];
+#pragma unroll
+      for (int i = 0; i < V; ++i) o.v[i] = from_f<T>(to_f(d.v[i]) * k0 + to_f(xv.v[i]) * k1 + k2);
+    }
+    *reinterpret_cast<P*>(dx + (int64_t)e * V) = o;
+  }
+}
+
+// parallel (sum_dy, sum_dy_xmu) finalize for many splits: one block per channel
+__global__ void __launch_bounds__(256) bn_bwd_finalize_par_kernel(const float* __restrict__ part, int splits,
+                                                                 float* __restrict__ sum_dy,
+                                                                 float* __restrict__ sum_dy_xmu) {
+  __shared__ float red[4];
+  const int64_t c = blockIdx.x;
+  float a = 0.f, b = 0.f;
+  for (int k = threadIdx.x; k < splits; k += 256) {
+    a += part[(c * splits + k) * 2];
+    b += part[(c * splits + k) * 2 + 1];
+  }
+  a = block_sum(a, red);
+  b = block_sum(b, red);
+  if (threadIdx.x == 0) {
+    sum_dy[c] = a;
+    sum_dy_xmu[c] = b;
+  }
+}
+
+// parallel combine of c-major local partials (groups >= 64): one block per channel
+__global__ void __launch_bounds__(256) bn_combine_par_kernel(const float* __restrict__ in, int groups,
+                                                            float* __restrict__ mean, float* __restrict__ var,
+                                                            float* __restrict__ count) {
+  __shared__ float sm[3][4];
+  const int64_t c = blockIdx.x;
+  Welford t{0.f, 0.f, 0.f};
+  for (int g = threadIdx.x; g < groups; g += 256) {
+    const float* p = in + (c * groups + g) * 3;
+    t = wf_merge(t, Welford{p[0], p[1], p[2]});
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    Welford b{__shfl_xor(t.mean, o, 64), __shfl_xor(t.m2, o, 64), __shfl_xor(t.n, o, 64)};
+    t = wf_merge(t, b);
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) {
+    sm[0][wid] = t.mean;
+    sm[1][wid] = t.m2;
+    sm[2][wid] = t.n;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    Welford r{sm[0][0], sm[1][0], sm[2][0]};
+    for (int k = 1; k < 4; ++k) r = wf_merge(r, Welford{sm[0][k], sm[1][k], sm[2][k]});
+    mean[c] = r.mean;
+    var[c] = r.n > 0.f ? r.m2 / r.n : 0.f;
+    if (count) count[c] = r.n;
+  }
+}
+
+static inline int bn_vec(int dt) { return dt == kF32 ? 4 : 8; }
+
+// NHWC block geometry: cvb channel vectors x rpb row lanes (cvb * rpb <= 256)
+static inline void bn_nhwc_geom(int64_t C, int V, int& cvb, int& rpb, int& gx) {
+  const int CV = (int)(C / V);
+  cvb = CV < 64 ? CV : 64;
+  rpb = 256 / cvb;
+  gx = (CV + cvb - 1) / cvb;
+}
+
+static inline bool bn_vec_ok(const void* p, int64_t N, int64_t C, int64_t S, int nhwc, int V) {
+  if (((uintptr_t)p & 15) || N * C * S / V >= (1ll << 31) || C >= (1 << 30)) return false;
+  return nhwc ? (C % V == 0 && C / V <= 256 * 64) : (S % V == 0 && N * (S / V) < (1ll << 31));
+}
+
+static inline int bn_splits(int64_t N, int64_t S, int64_t C, int nhwc, int V) {
+  if (nhwc) {
+    // ~1024 blocks over the channel-vector groups, >= 8 rows per row lane
+    int cvb, rpb, gx;
+    bn_nhwc_geom(C, V, cvb, rpb, gx);
+    const int64_t R = N * S;
+    int64_t sp = (1024 + gx - 1) / gx;
+    const int64_t cap = R / (8 * (int64_t)rpb);
+    if (sp > cap) sp = cap;
+    if (sp < 1) sp = 1;
+    if (sp > 512) sp = 512;
+    return (int)sp;
+  }
   // enough blocks to fill the chip: ~2048 blocks total, each >= 1024 elements
   int64_t per_c = (N * S + 1023) / 1024;
   int64_t want = (2048 + C - 1) / C;
@@ -435,33 +855,66 @@ static inline int bn_splits(int64_t N, int64_t S, int64_t C) {
   return (int)sp;
 }
 
-int bn_stats(const void* x, float* part, int64_t N, int64_t C, int64_t S, int nhwc, int dt, int* splits_out,
-             hipStream_t s) {
-  const int sp = bn_splits(N, S, C);
-  *splits_out = sp;
-  if (C == 0) return 0;
-  NM_DISPATCH(dt, T,
-      hipLaunchKernelGGL((bn_stats_kernel<T>), dim3((unsigned)C, sp), dim3(256), 0, s, (const T*)x, part, N, C,
-                         S, nhwc));
-  return (int)hipGetLastError();
+int bn_splits_for(int64_t N, int64_t C, int64_t S, int nhwc, int dt) {
+  return bn_splits(N, S, C, nhwc, bn_vec(dt));
 }
 
-int bn_splits_for(int64_t N, int64_t C, int64_t S) { return bn_splits(N, S, C); }
+int bn_stats(const void* x, float* part, int64_t N, int64_t C, int64_t S, int nhwc, int dt, int* splits_out,
+             hipStream_t s) {
+  const int V = bn_vec(dt);
+  const int sp = bn_splits(N, S, C, nhwc, V);
+  *splits_out = sp;
+  if (C == 0) return 0;
+  if (bn_vec_ok(x, N, C, S, nhwc, V)) {
+    if (nhwc) {
+      int cvb, rpb, gx;
+      bn_nhwc_geom(C, V, cvb, rpb, gx);
+      NM_DISPATCH(dt, T,
+          hipLaunchKernelGGL((bn_stats_nhwc_vec<T>), dim3(gx, sp), dim3(256), 0, s, (const T*)x, part, N * S,
+                             (int)C, cvb, rpb));
+    } else {
+      NM_DISPATCH(dt, T,
+          hipLaunchKernelGGL((bn_stats_nchw_vec<T>), dim3((unsigned)C, sp), dim3(256), 0, s, (const T*)x, part,
+                             (int)N, (int)C, (int)S));
+    }
+  } else {
+    NM_DISPATCH(dt, T,
+        hipLaunchKernelGGL((bn_stats_kernel<T>), dim3((unsigned)C, sp), dim3(256), 0, s, (const T*)x, part, N, C,
+                           S, nhwc));
+  }
+  return (int)hipGetLastError();
+}
 
 int bn_combine(const float* in, int groups, int64_t C, int gmajor, float* mean, float* var, float* count,
                hipStream_t s) {
   if (C == 0) return 0;
-  hipLaunchKernelGGL(bn_combine_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, in, groups, C,
-                     gmajor, mean, var, count);
+  if (!gmajor && groups >= 64) {
+    hipLaunchKernelGGL(bn_combine_par_kernel, dim3((unsigned)C), dim3(256), 0, s, in, groups, mean, var, count);
+  } else {
+    hipLaunchKernelGGL(bn_combine_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, in, groups, C,
+                       gmajor, mean, var, count);
+  }
   return (int)hipGetLastError();
 }
 
 int bn_elemt(const void* x, const float* mean, const float* invstd, const void* w, const void* b, void* y,
-             int64_t N, int64_t C, int64_t S, int nhwc, int relu, int dt, int wdt, hipStream_t s) {
+             int64_t N, int64_t C, int64_t S, int nhwc, int relu, int dt, int wdt, float* coef, hipStream_t s) {
   const int64_t total = N * C * S;
   if (total == 0) return 0;
-  const int64_t grid = min((total + 255) / 256, (int64_t)8192);
   if (!w && !b) wdt = kF32;
+  const int V = bn_vec(dt);
+  if (coef && bn_vec_ok(x, N, C, S, nhwc, V) && ((uintptr_t)y & 15) == 0 && ((uintptr_t)coef & 15) == 0) {
+    NM_DISPATCH(wdt, W,
+        hipLaunchKernelGGL((bn_coef_fwd_kernel<W>), dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, mean, invstd,
+                           (const W*)w, (const W*)b, coef, (int)C));
+    const int64_t nvec = total / V;
+    const int64_t grid = min((nvec + 255) / 256, (int64_t)4096);
+    NM_DISPATCH(dt, T,
+        hipLaunchKernelGGL((bn_elemt_vec<T>), dim3((unsigned)grid), dim3(256), 0, s, (const T*)x, coef, (T*)y,
+                           (int)nvec, (int)C, (int)S, nhwc, relu));
+    return (int)hipGetLastError();
+  }
+  const int64_t grid = min((total + 255) / 256, (int64_t)8192);
   NM_DISPATCH(dt, T, NM_DISPATCH(wdt, W,
       hipLaunchKernelGGL((bn_elemt_kernel<T, W>), dim3((unsigned)grid), dim3(256), 0, s, (const T*)x, mean,
                          invstd, (const W*)w, (const W*)b, (T*)y, N, C, S, nhwc, relu)));
@@ -471,22 +924,53 @@ int bn_elemt(const void* x, const float* mean, const float* invstd, const void* 
 int bn_bwd_reduce(const void* dy, const void* x, const float* mean, float* part, float* sum_dy,
                   float* sum_dy_xmu, int64_t N, int64_t C, int64_t S, int nhwc, int dt, hipStream_t s) {
   if (C == 0) return 0;
-  const int sp = bn_splits(N, S, C);
-  NM_DISPATCH(dt, T,
-      hipLaunchKernelGGL((bn_bwd_reduce_kernel<T>), dim3((unsigned)C, sp), dim3(256), 0, s, (const T*)dy,
-                         (const T*)x, mean, part, N, C, S, nhwc));
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, part, sp, C,
-                     sum_dy, sum_dy_xmu);
+  const int V = bn_vec(dt);
+  const int sp = bn_splits(N, S, C, nhwc, V);
+  if (bn_vec_ok(x, N, C, S, nhwc, V) && ((uintptr_t)dy & 15) == 0) {
+    if (nhwc) {
+      int cvb, rpb, gx;
+      bn_nhwc_geom(C, V, cvb, rpb, gx);
+      NM_DISPATCH(dt, T,
+          hipLaunchKernelGGL((bn_bwd_reduce_nhwc_vec<T>), dim3(gx, sp), dim3(256), 0, s, (const T*)dy,
+                             (const T*)x, mean, part, N * S, (int)C, cvb, rpb));
+    } else {
+      NM_DISPATCH(dt, T,
+          hipLaunchKernelGGL((bn_bwd_reduce_nchw_vec<T>), dim3((unsigned)C, sp), dim3(256), 0, s, (const T*)dy,
+                             (const T*)x, mean, part, (int)N, (int)C, (int)S));
+    }
+  } else {
+    NM_DISPATCH(dt, T,
+        hipLaunchKernelGGL((bn_bwd_reduce_kernel<T>), dim3((unsigned)C, sp), dim3(256), 0, s, (const T*)dy,
+                           (const T*)x, mean, part, N, C, S, nhwc));
+  }
+  if (sp >= 64)
+    hipLaunchKernelGGL(bn_bwd_finalize_par_kernel, dim3((unsigned)C), dim3(256), 0, s, part, sp, sum_dy, sum_dy_xmu);
+  else
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, part, sp, C,
+                       sum_dy, sum_dy_xmu);
   return (int)hipGetLastError();
 }
 
 int bn_bwd_elemt(const void* dy, const void* x, const float* mean, const float* invstd, const void* w,
                  const float* sum_dy, const float* sum_dy_xmu, const float* count, void* dx, int64_t N, int64_t C,
-                 int64_t S, int nhwc, int dt, int wdt, hipStream_t s) {
+                 int64_t S, int nhwc, int dt, int wdt, float* coef, hipStream_t s) {
   const int64_t total = N * C * S;
   if (total == 0) return 0;
-  const int64_t grid = min((total + 255) / 256, (int64_t)8192);
   if (!w) wdt = kF32;
+  const int V = bn_vec(dt);
+  if (coef && bn_vec_ok(x, N, C, S, nhwc, V) && ((uintptr_t)dy & 15) == 0 && ((uintptr_t)dx & 15) == 0 &&
+      ((uintptr_t)coef & 15) == 0) {
+    NM_DISPATCH(wdt, W,
+        hipLaunchKernelGGL((bn_coef_bwd_kernel<W>), dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, mean, invstd,
+                           (const W*)w, sum_dy, sum_dy_xmu, count, coef, (int)C));
+    const int64_t nvec = total / V;
+    const int64_t grid = min((nvec + 255) / 256, (int64_t)4096);
+    NM_DISPATCH(dt, T,
+        hipLaunchKernelGGL((bn_bwd_elemt_vec<T>), dim3((unsigned)grid), dim3(256), 0, s, (const T*)dy, (const T*)x,
+                           coef, (T*)dx, (int)nvec, (int)C, (int)S, nhwc));
+    return (int)hipGetLastError();
+  }
+  const int64_t grid = min((total + 255) / 256, (int64_t)8192);
   NM_DISPATCH(dt, T, NM_DISPATCH(wdt, W,
       hipLaunchKernelGGL((bn_bwd_elemt_kernel<T, W>), dim3((unsigned)grid), dim3(256), 0, s, (const T*)dy,
                          (const T*)x, mean, invstd, (const W*)w, sum_dy, sum_dy_xmu, count, (T*)dx, N, C,

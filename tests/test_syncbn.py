@@ -78,7 +78,11 @@ def test_syncbn_matches_full_batch_bn():
 @pytest.mark.gpu
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("shape,channel_last", [((8, 16, 7, 7), False), ((4, 64, 20, 9), False),
-                                                ((6, 5, 3, 32), True), ((33, 12), False)])
+                                                ((6, 5, 3, 32), True), ((33, 12), False),
+                                                # vectorised paths: NCHW planes % 8, NHWC channels % 8
+                                                ((4, 64, 16, 8), False), ((2, 32, 56, 56), False),
+                                                ((4, 7, 9, 64), True), ((8, 14, 14, 256), True),
+                                                ((2, 7, 7, 2048), True), ((3, 24), False)])
 def test_syncbn_kernels_single_process(dt, shape, channel_last):
     from apex.parallel import SyncBatchNorm
 
@@ -107,3 +111,30 @@ def test_syncbn_kernels_single_process(dt, shape, channel_last):
     torch.testing.assert_close(x.grad.float(), xr.grad, rtol=tol * 2, atol=tol * 2)
     torch.testing.assert_close(m.weight.grad.float(), ref.weight.grad, rtol=tol * 4, atol=tol * 20)
     torch.testing.assert_close(m.running_mean, ref.running_mean, rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_syncbn_channels_last_memory_format_and_large_mean(dt):
+    """A torch channels_last NCHW tensor takes the NHWC kernels on the zero-copy view; inputs with
+    a mean far from zero check the Welford partial merges (a sum / sum-of-squares reduction would
+    lose the variance to cancellation at mean 100, std 1)."""
+    from apex.parallel import SyncBatchNorm
+
+    torch.manual_seed(2)
+    N, C, H, W = 16, 128, 28, 28
+    x = (torch.randn(N, C, H, W, device="cuda") + 100.0).to(dt).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    m = SyncBatchNorm(C).cuda()
+    y = m(x)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    # fp64 reference: an fp32 library BatchNorm itself loses ~1e-3 at mean 100
+    xr = x.detach().double().requires_grad_(True)
+    ref = nn.BatchNorm2d(C).cuda().double()
+    yr = ref(xr)
+    yr.backward(dy.double())
+    tol = 3e-2 if dt == torch.bfloat16 else 1e-3
+    torch.testing.assert_close(y.float(), yr.float(), rtol=tol, atol=tol)
+    torch.testing.assert_close(x.grad.float(), xr.grad.float(), rtol=2 * tol, atol=2 * tol)
+    torch.testing.assert_close(m.running_var, ref.running_var.float(), rtol=1e-2, atol=1e-2)

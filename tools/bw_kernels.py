@@ -107,20 +107,24 @@ def op_xent(iters):
             dict(op="softmax_xentropy_bwd", us=bwd, bytes=2 * n + R * 16, kernels="xent_bwd_kernel")]
 
 
-def op_syncbn(iters):
+def op_syncbn(iters, channels_last=False):
     from apex.parallel import SyncBatchNorm
 
     N, Cc, H, W = 64, 256, 56, 56
     bn = SyncBatchNorm(Cc).to(DEV)
-    x = torch.randn(N, Cc, H, W, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    x = torch.randn(N, Cc, H, W, device=DEV, dtype=torch.bfloat16)
+    if channels_last:
+        x = x.contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
     dy = torch.randn_like(x)
     y = bn(x)
     fwd = _time(lambda: bn(x), iters)
     bwd = _time(lambda: torch.autograd.grad(y, [x] + list(bn.parameters()), dy, retain_graph=True), iters)
     n = x.numel() * 2
     # fwd: stats pass reads x, elementwise pass reads x writes y; bwd: reduce reads dy, x; elemt reads dy, x, writes dx
-    return [dict(op="syncbn_fwd", us=fwd, bytes=3 * n, kernels="bn_local_stats + bn_combine + bn_elemt"),
-            dict(op="syncbn_bwd", us=bwd, bytes=5 * n, kernels="bn_bwd_reduce + bn_bwd_elemt")]
+    tag = "syncbn_nhwc" if channels_last else "syncbn_nchw"
+    return [dict(op=tag + "_fwd", us=fwd, bytes=3 * n, kernels="bn_local_stats + bn_combine + bn_elemt"),
+            dict(op=tag + "_bwd", us=bwd, bytes=5 * n, kernels="bn_bwd_reduce + bn_bwd_elemt")]
 
 
 def op_scale(iters):
@@ -136,7 +140,8 @@ def op_scale(iters):
     return [dict(op="multi_tensor_scale_bf16_to_fp32", us=us, bytes=n * 6, params=n, kernels="mt scale")]
 
 
-OPS = dict(ln=op_ln, bdaln=op_bdaln, lamb=op_lamb, xent=op_xent, syncbn=op_syncbn, scale=op_scale)
+OPS = dict(ln=op_ln, bdaln=op_bdaln, lamb=op_lamb, xent=op_xent, syncbn=op_syncbn,
+           syncbn_nhwc=lambda it: op_syncbn(it, True), scale=op_scale)
 
 
 def main():

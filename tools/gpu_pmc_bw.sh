@@ -4,7 +4,7 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/${OUT:-pmc_bw}
-OPS=${OPS:-ln,bdaln,lamb,xent,syncbn,scale}
+OPS=${OPS:-ln,bdaln,lamb,xent,syncbn,syncbn_nhwc,scale}
 mkdir -p $O
 timeout -k 10 300 python tools/bw_kernels.py --ops $OPS --iters 10 > $O/timing.jsonl 2> $O/timing.err || exit $?
 i=0
