@@ -322,7 +322,7 @@ __global__ void __launch_bounds__(kBlock) lamb_stage1_kernel(MTMeta m, LambArgs 
     float* mm = (float*)m.ptr(2, cv.t) + cv.start;
     float* vv = (float*)m.ptr(3, cv.t) + cv.start;
     float sp = 0.f, su = 0.f;
-    chunk_for(m, cv.n, [&](auto NC, int64_t i) {
+    auto body = [&](auto NC, int64_t i) {
       constexpr int N = decltype(NC)::value;
       float gv[N], pv[N], mv[N], vv2[N], u[N];
       load_f<G, N>(g + i, gv);
@@ -341,7 +341,43 @@ __global__ void __launch_bounds__(kBlock) lamb_stage1_kernel(MTMeta m, LambArgs 
       }
       store_f<float, N>(mm + i, mv);
       store_f<float, N>(vv + i, vv2);
-    });
+    };
+    // two vector groups per iteration with every load issued before the first store: the
+    // compiler cannot move the next group's loads above this group's stores (possible aliasing),
+    // so one group per iteration kept only one set of loads in flight per thread
+    const int64_t nv = m.aligned ? (cv.n & ~int64_t(7)) : 0;
+    const int64_t stride = (int64_t)blockDim.x * 8;
+    int64_t i = threadIdx.x * 8;
+    for (; i + stride < nv; i += 2 * stride) {
+      const int64_t j = i + stride;
+      float gv[2][8], pv[2][8], mv[2][8], vq[2][8];
+      load_f<G, 8>(g + i, gv[0]);
+      load_f<G, 8>(g + j, gv[1]);
+      load_f<P, 8>(p + i, pv[0]);
+      load_f<P, 8>(p + j, pv[1]);
+      load_f<float, 8>(mm + i, mv[0]);
+      load_f<float, 8>(mm + j, mv[1]);
+      load_f<float, 8>(vv + i, vq[0]);
+      load_f<float, 8>(vv + j, vq[1]);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          float gg = gv[h][k] * gs;
+          if (!a.adamw && a.wd != 0.f) gg += a.wd * pv[h][k];
+          mv[h][k] = b1 * mv[h][k] + b3 * gg;
+          vq[h][k] = b2 * vq[h][k] + (1.f - b2) * gg * gg;
+          const float u = lamb_u(mv[h][k], vq[h][k], pv[h][k], rbc1, rbc2, a);
+          sp += pv[h][k] * pv[h][k];
+          su += u * u;
+        }
+      store_f<float, 8>(mm + i, mv[0]);
+      store_f<float, 8>(mm + j, mv[1]);
+      store_f<float, 8>(vv + i, vq[0]);
+      store_f<float, 8>(vv + j, vq[1]);
+    }
+    for (; i < nv; i += stride) body(I8{}, i);
+    for (int64_t t = nv + threadIdx.x; t < cv.n; t += blockDim.x) body(I1{}, t);
     sp = block_sum(sp, red);
     su = block_sum(su, red);
     if (threadIdx.x == 0) {
@@ -368,7 +404,7 @@ __global__ void __launch_bounds__(kBlock) lamb_stage2_kernel(MTMeta m, LambArgs 
       const float pn = pnorm[cv.t], un = unorm[cv.t];
       if (pn != 0.f && un != 0.f) ratio = a.lr * (pn / un);
     }
-    chunk_for(m, cv.n, [&](auto NC, int64_t i) {
+    auto body = [&](auto NC, int64_t i) {
       constexpr int N = decltype(NC)::value;
       float pv[N], mv[N], vv2[N];
       load_f<P, N>(p + i, pv);
@@ -378,7 +414,33 @@ __global__ void __launch_bounds__(kBlock) lamb_stage2_kernel(MTMeta m, LambArgs 
       for (int k = 0; k < N; ++k) pv[k] -= ratio * lamb_u(mv[k], vv2[k], pv[k], rbc1, rbc2, a);
       store_f<P, N>(p + i, pv);
       if (cp) store_f<C, N>(cp + i, pv);
-    });
+    };
+    // two vector groups per iteration, loads before stores (see stage 1)
+    const int64_t nv = m.aligned ? (cv.n & ~int64_t(7)) : 0;
+    const int64_t stride = (int64_t)blockDim.x * 8;
+    int64_t i = threadIdx.x * 8;
+    for (; i + stride < nv; i += 2 * stride) {
+      const int64_t j = i + stride;
+      float pv[2][8], mv[2][8], vq[2][8];
+      load_f<P, 8>(p + i, pv[0]);
+      load_f<P, 8>(p + j, pv[1]);
+      load_f<float, 8>(mm + i, mv[0]);
+      load_f<float, 8>(mm + j, mv[1]);
+      load_f<float, 8>(vv + i, vq[0]);
+      load_f<float, 8>(vv + j, vq[1]);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) pv[h][k] -= ratio * lamb_u(mv[h][k], vq[h][k], pv[h][k], rbc1, rbc2, a);
+      store_f<P, 8>(p + i, pv[0]);
+      store_f<P, 8>(p + j, pv[1]);
+      if (cp) {
+        store_f<C, 8>(cp + i, pv[0]);
+        store_f<C, 8>(cp + j, pv[1]);
+      }
+    }
+    for (; i < nv; i += stride) body(I8{}, i);
+    for (int64_t t = nv + threadIdx.x; t < cv.n; t += blockDim.x) body(I1{}, t);
   }
 }
 
