@@ -63,6 +63,10 @@ class BertConfig:
 
 
 class BertEmbeddings(nn.Module):
+    # one fused kernel each way (apex.ops.fused.bert_embeddings); APEX_BERT_EMBED_FUSION=0 selects
+    # the op-by-op composition
+    use_fused = os.environ.get("APEX_BERT_EMBED_FUSION", "1") == "1"
+
     def __init__(self, c: BertConfig):
         super().__init__()
         self.word_embeddings = nn.Embedding(c.padded_vocab, c.hidden_size)
@@ -76,6 +80,11 @@ class BertEmbeddings(nn.Module):
         if S > self.position_embeddings.num_embeddings:  # host-side check (a bad gather faults the GPU)
             raise ValueError(f"sequence length {S} exceeds max_position_embeddings="
                              f"{self.position_embeddings.num_embeddings}")
+        if self.use_fused:
+            return fops.bert_embeddings(input_ids, token_type_ids, self.word_embeddings.weight,
+                                        self.position_embeddings.weight, self.token_type_embeddings.weight,
+                                        self.LayerNorm.weight, self.LayerNorm.bias, self.p, self.LayerNorm.eps,
+                                        training=self.training)
         pos = torch.arange(S, device=input_ids.device)
         x = self.word_embeddings(input_ids) + self.position_embeddings(pos)[None] + \
             self.token_type_embeddings(token_type_ids)

@@ -6,6 +6,8 @@ the PyTorch reference formulation on CPU (also the numerics reference for the te
   fused_dense(x, W, b)                      y = x W^T + b            (bias grad: HIP colsum)
   dense_gelu(x, W, b)                       y = gelu(x W^T + b)      (bias+GELU fwd/bwd fused,
                                                                      bias grad folded in)
+  bert_embeddings(ids, types, Ww, Wp, Wt, gamma, beta, p, eps)
+                                            y = dropout(LN(Ww[ids] + Wp[pos] + Wt[types]))
   dense_bias_dropout_add_ln(x, W, b, res, gamma, beta, p, eps)
                                             y = LN(res + dropout(x W^T + b))  (one fused
                                                                      kernel each way)
@@ -231,6 +233,60 @@ def bias_gelu(h, bias):
     if _native(h) and h.shape[-1] % 8 == 0:
         return _BiasAct.apply(h, bias, ACT_GELU)
     return F.gelu(h + bias)
+
+
+# ---------------------------------------------------------------------------
+class _BertEmbeddings(torch.autograd.Function):
+    """y = dropout(LN(Ww[ids] + Wp[pos] + Wt[types])), pos = arange(S): one HIP kernel each way
+    (csrc/fused_ops.hip embed_ln_*) instead of three gathers, two broadcast adds, LayerNorm and
+    dropout; the word-table gradient is a deterministic segment sum over the id-sorted tokens (no
+    atomics), the position / type / gamma / beta gradients come out of the backward kernel's
+    registers as partial rows."""
+
+    @staticmethod
+    def forward(ctx, ids, tids, Ww, Wp, Wt, gamma, beta, p, eps):
+        C = _ext.require()
+        V, TV = Ww.shape[0], Wt.shape[0]
+        # out-of-range ids are clamped (a bad gather would fault the GPU); nn.Embedding raises
+        ids32 = ids.clamp(0, V - 1).to(torch.int32).contiguous()
+        t32 = tids.clamp(0, TV - 1).to(torch.int32).contiguous() if tids is not None else None
+        seed, off = _seed(ids.device) if p > 0 else (0, 0)
+        y, sv, mean, rstd = C.embed_ln_fwd(ids32, t32, Ww, Wp, Wt, gamma, beta, float(eps), float(p), seed, off)
+        ctx.save_for_backward(ids32, t32, sv, gamma, mean, rstd)
+        ctx.cfg = (float(p), seed, off, V, Wp.shape[0], TV)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = _ext.require()
+        ids32, t32, sv, gamma, mean, rstd = ctx.saved_tensors
+        p, seed, off, V, npos, TV = ctx.cfg
+        ds, dWp, dWt, dg, db = C.embed_ln_bwd(dy, sv, gamma, mean, rstd, t32, TV, npos, p, seed, off)
+        sorted_ids, perm = torch.sort(ids32.view(-1), stable=True)
+        dWw = C.embed_segsum(ds, sorted_ids, perm, V)
+        return None, None, dWw, dWp, dWt, dg, db, None, None
+
+
+def bert_embeddings(input_ids, token_type_ids, word, position, token_type, gamma, beta, p=0.0, eps=1e-12,
+                    training=True):
+    """BERT's embedding block: dropout(LayerNorm(word[ids] + position[arange(S)] + type[types]))."""
+    p = p if training else 0.0
+    H = word.shape[1]
+    if (_native(input_ids) and input_ids.dim() == 2 and token_type.shape[0] <= 2 and
+            word.dtype in (torch.float16, torch.bfloat16) and position.dtype == word.dtype and
+            token_type.dtype == word.dtype and gamma is not None and beta is not None and
+            _ext.require().bdaln_supported(H) and input_ids.shape[1] <= position.shape[0]):
+        return _BertEmbeddings.apply(input_ids, token_type_ids, word, position, token_type, gamma, beta, float(p),
+                                     float(eps))
+    S = input_ids.shape[1]
+    pos = torch.arange(S, device=input_ids.device)
+    x = F.embedding(input_ids, word) + F.embedding(pos, position)[None]
+    if token_type_ids is not None:
+        x = x + F.embedding(token_type_ids, token_type)
+    else:
+        x = x + token_type[0]
+    x = F.layer_norm(x, (H,), gamma, beta, eps)
+    return F.dropout(x, p, True) if p > 0 else x
 
 
 # ---------------------------------------------------------------------------

@@ -549,6 +549,79 @@ std::vector<Tensor> k_bdaln_bwd(Tensor dy, Tensor s, Tensor gamma, Tensor mean, 
 }
 
 // --------------------------------------------------------------------------
+// BERT embeddings (fused_ops.hip): ids / tids int32 [B, S] (clamped by the caller)
+// --------------------------------------------------------------------------
+std::vector<Tensor> k_embed_ln_fwd(Tensor ids, const c10::optional<Tensor>& tids, Tensor Ww, Tensor Wp, Tensor Wt,
+                                   Tensor gamma, Tensor beta, double eps, double p, int64_t seed, int64_t offset) {
+  TORCH_CHECK(ids.is_cuda() && ids.dim() == 2 && ids.is_contiguous() && ids.scalar_type() == at::kInt,
+              "embed_ln_fwd: ids int32 [B, S]");
+  TORCH_CHECK(Ww.is_contiguous() && Wp.is_contiguous() && Wt.is_contiguous() && Ww.dim() == 2 &&
+                  Wp.size(1) == Ww.size(1) && Wt.size(1) == Ww.size(1) && Wp.scalar_type() == Ww.scalar_type() &&
+                  Wt.scalar_type() == Ww.scalar_type() && Wp.size(0) >= ids.size(1),
+              "embed_ln_fwd: tables");
+  const int* tp = nullptr;
+  if (tids.has_value() && tids->defined()) {
+    TORCH_CHECK(tids->sizes() == ids.sizes() && tids->is_contiguous() && tids->scalar_type() == at::kInt,
+                "embed_ln_fwd: type ids int32 [B, S]");
+    tp = tids->data_ptr<int>();
+  }
+  const int64_t B = ids.size(0), S = ids.size(1), H = Ww.size(1), rows = B * S;
+  auto xo = Ww.options();
+  Tensor y = at::empty({B, S, H}, xo), sv = at::empty({B, S, H}, xo);
+  auto fo = xo.dtype(at::kFloat);
+  Tensor mean = at::empty({rows}, fo), rstd = at::empty({rows}, fo);
+  auto dp = drop_params(p);
+  check(apex::embed_ln_fwd(ids.data_ptr<int>(), tp, Ww.data_ptr(), Wp.data_ptr(), Wt.data_ptr(), gamma.data_ptr(),
+                           beta.data_ptr(), y.data_ptr(), sv.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
+                           rows, (int)H, (int)S, (float)eps, (uint64_t)seed, (uint64_t)offset, dp.first, dp.second,
+                           dt_code(Ww.scalar_type()), dt_code(gamma.scalar_type()), cur_stream()),
+        "embed_ln_fwd");
+  return {y, sv, mean, rstd};
+}
+
+// -> {ds [B, S, H], dWp [npos, H] (rows >= S zero), dWt [tvocab, H], dgamma, dbeta}
+std::vector<Tensor> k_embed_ln_bwd(Tensor dy, Tensor sv, Tensor gamma, Tensor mean, Tensor rstd,
+                                   const c10::optional<Tensor>& tids, int64_t tvocab, int64_t npos, double p,
+                                   int64_t seed, int64_t offset) {
+  Tensor dyc = dy.contiguous();
+  TORCH_CHECK(sv.dim() == 3 && dyc.sizes() == sv.sizes(), "embed_ln_bwd: shapes");
+  const int64_t B = sv.size(0), S = sv.size(1), H = sv.size(2);
+  TORCH_CHECK(npos >= S && tvocab >= 1 && tvocab <= 2, "embed_ln_bwd: table sizes");
+  const int* tp = nullptr;
+  if (tids.has_value() && tids->defined()) tp = tids->data_ptr<int>();
+  Tensor ds = at::empty_like(sv);
+  Tensor dWp = at::zeros({npos, H}, sv.options());
+  Tensor dWt = at::empty({tvocab, H}, sv.options());
+  Tensor dgamma = at::empty_like(gamma), dbeta = at::empty_like(gamma);
+  const int nwt = apex::embed_nwt(B);
+  auto fo = sv.options().dtype(at::kFloat);
+  Tensor part_pos = at::empty({(int64_t)nwt * S * H}, fo);
+  Tensor part_tg = at::empty({S * nwt * 4 * H}, fo);
+  auto dp = drop_params(p);
+  check(apex::embed_ln_bwd(dyc.data_ptr(), sv.data_ptr(), gamma.data_ptr(), mean.data_ptr<float>(),
+                           rstd.data_ptr<float>(), tp, (int)tvocab, ds.data_ptr(), part_pos.data_ptr<float>(),
+                           part_tg.data_ptr<float>(), dWp.data_ptr(), dWt.data_ptr(), dgamma.data_ptr(),
+                           dbeta.data_ptr(), B, (int)H, (int)S, (uint64_t)seed, (uint64_t)offset, dp.first, dp.second,
+                           dt_code(sv.scalar_type()), dt_code(gamma.scalar_type()), cur_stream()),
+        "embed_ln_bwd");
+  return {ds, dWp, dWt, dgamma, dbeta};
+}
+
+// dW [vocab, H]: zero rows, plus the ds rows of every token summed into its id's row
+Tensor k_embed_segsum(Tensor ds, Tensor sorted_ids, Tensor perm, int64_t vocab) {
+  TORCH_CHECK(ds.is_contiguous() && sorted_ids.scalar_type() == at::kInt && perm.scalar_type() == at::kLong &&
+                  sorted_ids.is_contiguous() && perm.is_contiguous() && sorted_ids.numel() == perm.numel(),
+              "embed_segsum: int32 sorted ids, int64 permutation");
+  const int64_t H = ds.size(-1), R = ds.numel() / H;
+  TORCH_CHECK(sorted_ids.numel() == R, "embed_segsum: one id per ds row");
+  Tensor dW = at::zeros({vocab, H}, ds.options());
+  check(apex::embed_segsum(ds.data_ptr(), sorted_ids.data_ptr<int>(), perm.data_ptr<int64_t>(), dW.data_ptr(), R,
+                           (int)H, dt_code(ds.scalar_type()), cur_stream()),
+        "embed_segsum");
+  return dW;
+}
+
+// --------------------------------------------------------------------------
 // weight norm: v viewed as [R, C]; row_mode: one norm per row (dim=0), else per column
 // --------------------------------------------------------------------------
 std::vector<Tensor> k_wn_fwd(Tensor v, Tensor g, bool row_mode) {
@@ -1147,6 +1220,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("splitk_reduce", &k_splitk_reduce);
   m.def("bdaln_supported", &k_bdaln_supported);
   m.def("bdaln_fwd", &k_bdaln_fwd);
+  m.def("embed_ln_fwd", &k_embed_ln_fwd);
+  m.def("embed_ln_bwd", &k_embed_ln_bwd);
+  m.def("embed_segsum", &k_embed_segsum);
   m.def("bdaln_bwd", &k_bdaln_bwd);
   m.def("input_normalize", &k_input_normalize);
   m.def("gemm_supported", &k_gemm_supported);

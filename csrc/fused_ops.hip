@@ -380,6 +380,227 @@ __global__ void __launch_bounds__(kEwBlock) bdaln_bwd_kernel(const T* __restrict
     out[c] = lds[c] + lds[3 * cols + c] + lds[6 * cols + c] + lds[9 * cols + c];
 }
 
+// ------------------------- BERT embeddings (gather-sum + LayerNorm + dropout) -------------
+// forward, one wave per token row (row = b*S + pos):
+//   s = Ww[id] + Wp[pos] + Wt[type]; y = dropout(LN(s))     (s stored for the backward)
+// The word / type ids are int32, clamped to the table by the caller (apex.ops.fused).
+template <typename T, typename W, int VPT, bool DROP>
+__global__ void __launch_bounds__(kEwBlock) embed_ln_fwd_kernel(const int* __restrict__ ids, const int* __restrict__ tids,
+                                                               const T* __restrict__ Ww, const T* __restrict__ Wp,
+                                                               const T* __restrict__ Wt, const W* __restrict__ gamma,
+                                                               const W* __restrict__ beta, T* __restrict__ y,
+                                                               T* __restrict__ s_out, float* __restrict__ mean,
+                                                               float* __restrict__ rstd, int64_t rows, int cols, int S,
+                                                               float eps, uint64_t seed, uint64_t offset,
+                                                               uint32_t thresh, float scale) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nvec = cols >> 3;
+  const int pos = (int)(row % S);
+  const T* wr = Ww + (int64_t)ids[row] * cols;
+  const T* pr = Wp + (int64_t)pos * cols;
+  const T* tr = tids ? Wt + (int64_t)tids[row] * cols : Wt;
+  float v[VPT][8];
+  float sum = 0.f;
+#pragma unroll
+  for (int j = 0; j < VPT; ++j) {
+    const int vi = j * 64 + lane;
+    if (vi < nvec) {
+      float a[8], b[8], c[8];
+      load_f<T, 8>(wr + vi * 8, a);
+      load_f<T, 8>(pr + vi * 8, b);
+      load_f<T, 8>(tr + vi * 8, c);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[j][k] = a[k] + b[k] + c[k];
+      store_f<T, 8>(s_out + row * cols + vi * 8, v[j]);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        v[j][k] = to_f(from_f<T>(v[j][k]));  // normalise exactly what the backward reads
+        sum += v[j][k];
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[j][k] = 0.f;
+    }
+  }
+  const float inv_n = 1.f / (float)cols;
+  const float mu = wave_sum(sum) * inv_n;
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < VPT; ++j)
+    if (j * 64 + lane < nvec)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) ss += (v[j][k] - mu) * (v[j][k] - mu);
+  const float rs = rsqrtf(wave_sum(ss) * inv_n + eps);
+  if (lane == 0) {
+    mean[row] = mu;
+    rstd[row] = rs;
+  }
+#pragma unroll
+  for (int j = 0; j < VPT; ++j) {
+    const int vi = j * 64 + lane;
+    if (vi < nvec) {
+      const int64_t e = row * cols + vi * 8;
+      float gv[8], bb[8], o[8];
+      load_f<W, 8>(gamma + vi * 8, gv);
+      load_f<W, 8>(beta + vi * 8, bb);
+      bool keep[8];
+      if (DROP) drop_mask8(seed, offset, e >> 3, thresh, keep);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        o[k] = (v[j][k] - mu) * rs * gv[k] + bb[k];
+        if (DROP) o[k] = keep[k] ? o[k] * scale : 0.f;
+      }
+      store_f<T, 8>(y + e, o);
+    }
+  }
+}
+
+// backward: grid (S, NWT / 4); wave (pos = blockIdx.x, w) walks the batch rows b = w, w + NWT, ...
+// of one position: dropout-backward + LayerNorm-backward -> ds (the gradient of the sum, stored for
+// the word-embedding segment sum), and in registers the position row's gradient, the type rows'
+// (type vocab <= 2) and dgamma / dbeta, written as fp32 partial rows:
+//   part_pos [NWT][S][cols], part_tg [S * NWT][4][cols] = {dgamma, dbeta, dtype0, dtype1}
+template <typename T, typename W, int VPT, bool DROP>
+__global__ void __launch_bounds__(kEwBlock) embed_ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ s,
+                                                               const W* __restrict__ gamma, const float* __restrict__ mean,
+                                                               const float* __restrict__ rstd, const int* __restrict__ tids,
+                                                               T* __restrict__ ds_out, float* __restrict__ part_pos,
+                                                               float* __restrict__ part_tg, int64_t B, int cols, int S,
+                                                               int nwt, uint64_t seed, uint64_t offset, uint32_t thresh,
+                                                               float scale) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int pos = blockIdx.x;
+  const int w = blockIdx.y * 4 + wid;
+  const int nvec = cols >> 3;
+  const float inv_n = 1.f / (float)cols;
+  float g[VPT][8], dgm[VPT][8], dbt[VPT][8], dps[VPT][8], dt0[VPT][8], dt1[VPT][8];
+#pragma unroll
+  for (int j = 0; j < VPT; ++j) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) g[j][k] = dgm[j][k] = dbt[j][k] = dps[j][k] = dt0[j][k] = dt1[j][k] = 0.f;
+    if (j * 64 + lane < nvec) load_f<W, 8>(gamma + (j * 64 + lane) * 8, g[j]);
+  }
+  typedef Pack<T, 8> P8;
+  P8 ns[VPT], nd[VPT];
+  auto fetch = [&](int64_t b) {
+    const int64_t row = b * S + pos;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int vi = j * 64 + lane;
+      if (vi < nvec && b < B) {
+        ns[j] = *reinterpret_cast<const P8*>(s + row * cols + vi * 8);
+        nd[j] = *reinterpret_cast<const P8*>(dy + row * cols + vi * 8);
+      }
+    }
+  };
+  if (w < nwt) {
+    fetch(w);
+    for (int64_t b = w; b < B; b += nwt) {
+      const int64_t row = b * S + pos;
+      float xh[VPT][8], dv[VPT][8];
+#pragma unroll
+      for (int j = 0; j < VPT; ++j)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          xh[j][k] = to_f(ns[j].v[k]);
+          dv[j][k] = to_f(nd[j].v[k]);
+        }
+      if (b + nwt < B) fetch(b + nwt);
+      const float mu = mean[row], rs = rstd[row];
+      const int tt = tids ? tids[row] : 0;
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int j = 0; j < VPT; ++j) {
+        const int vi = j * 64 + lane;
+        if (vi < nvec) {
+          bool keep[8];
+          if (DROP) drop_mask8(seed, offset, (row * cols + vi * 8) >> 3, thresh, keep);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            if (DROP) dv[j][k] = keep[k] ? dv[j][k] * scale : 0.f;
+            xh[j][k] = (xh[j][k] - mu) * rs;
+            const float dyg = dv[j][k] * g[j][k];
+            s1 += dyg;
+            s2 += dyg * xh[j][k];
+            dgm[j][k] += dv[j][k] * xh[j][k];
+            dbt[j][k] += dv[j][k];
+          }
+        }
+      }
+      s1 = wave_sum(s1) * inv_n;
+      s2 = wave_sum(s2) * inv_n;
+#pragma unroll
+      for (int j = 0; j < VPT; ++j) {
+        const int vi = j * 64 + lane;
+        if (vi < nvec) {
+          float d[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            d[k] = rs * (dv[j][k] * g[j][k] - s1 - xh[j][k] * s2);
+            dps[j][k] += d[k];
+            if (tt == 0) dt0[j][k] += d[k];
+            else dt1[j][k] += d[k];
+          }
+          store_f<T, 8>(ds_out + row * cols + vi * 8, d);
+        }
+      }
+    }
+  }
+  if (w >= nwt) return;
+  float* pp = part_pos + ((int64_t)w * S + pos) * cols;
+  float* pt = part_tg + ((int64_t)pos * nwt + w) * 4 * cols;
+#pragma unroll
+  for (int j = 0; j < VPT; ++j) {
+    const int vi = j * 64 + lane;
+    if (vi < nvec) {
+      store_f<float, 8>(pp + vi * 8, dps[j]);
+      store_f<float, 8>(pt + vi * 8, dgm[j]);
+      store_f<float, 8>(pt + cols + vi * 8, dbt[j]);
+      store_f<float, 8>(pt + 2 * cols + vi * 8, dt0[j]);
+      store_f<float, 8>(pt + 3 * cols + vi * 8, dt1[j]);
+    }
+  }
+}
+
+// word-embedding gradient: one wave per position of the id-sorted token list; the head of each
+// run of equal ids sums the ds rows of that run (fixed order: deterministic) into dW[id]
+template <typename T, int VPT>
+__global__ void __launch_bounds__(kEwBlock) embed_segsum_kernel(const T* __restrict__ ds, const int* __restrict__ sorted,
+                                                               const int64_t* __restrict__ perm, T* __restrict__ dW,
+                                                               int64_t R, int cols) {
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= R) return;
+  const int id = sorted[i];
+  if (i > 0 && sorted[i - 1] == id) return;
+  const int nvec = cols >> 3;
+  float acc[VPT][8];
+#pragma unroll
+  for (int j = 0; j < VPT; ++j)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[j][k] = 0.f;
+  for (int64_t t = i; t < R && sorted[t] == id; ++t) {
+    const T* r = ds + perm[t] * cols;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int vi = j * 64 + lane;
+      if (vi < nvec) {
+        float v[8];
+        load_f<T, 8>(r + vi * 8, v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[j][k] += v[k];
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < VPT; ++j) {
+    const int vi = j * 64 + lane;
+    if (vi < nvec) store_f<T, 8>(dW + (int64_t)id * cols + vi * 8, acc[j]);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
@@ -613,6 +834,66 @@ int bdaln_bwd(const void* dy, const void* s_in, const void* gamma, const float* 
     const int64_t ld = 3 * (int64_t)cols;
     launch_partial_colsum3<W>(ws, parts, ld, cols, (W*)dgamma, (W*)dbeta, (W*)dbias, s);
   })));
+  return (int)hipGetLastError();
+}
+
+int embed_ln_fwd(const int* ids, const int* tids, const void* Ww, const void* Wp, const void* Wt, const void* gamma,
+                 const void* beta, void* y, void* s_out, float* mean, float* rstd, int64_t rows, int cols, int S,
+                 float eps, uint64_t seed, uint64_t offset, uint32_t thresh, float scale, int xdt, int wdt,
+                 hipStream_t s) {
+  if (rows == 0) return 0;
+  const int vpt = bdaln_vpt(cols);
+  const dim3 grid((unsigned)((rows + 3) / 4));
+  EW_DISPATCH(xdt, T, EW_DISPATCH(wdt, W, EW_VPT(vpt, VPT, {
+    if (thresh)
+      hipLaunchKernelGGL((embed_ln_fwd_kernel<T, W, VPT, true>), grid, dim3(kEwBlock), 0, s, ids, tids, (const T*)Ww,
+                         (const T*)Wp, (const T*)Wt, (const W*)gamma, (const W*)beta, (T*)y, (T*)s_out, mean, rstd,
+                         rows, cols, S, eps, seed, offset, thresh, scale);
+    else
+      hipLaunchKernelGGL((embed_ln_fwd_kernel<T, W, VPT, false>), grid, dim3(kEwBlock), 0, s, ids, tids, (const T*)Ww,
+                         (const T*)Wp, (const T*)Wt, (const W*)gamma, (const W*)beta, (T*)y, (T*)s_out, mean, rstd,
+                         rows, cols, S, eps, seed, offset, thresh, scale);
+  })));
+  return (int)hipGetLastError();
+}
+
+int embed_nwt(int64_t B) { return B >= 16 ? 16 : (int)((B + 3) / 4 * 4); }
+
+int embed_ln_bwd(const void* dy, const void* s_in, const void* gamma, const float* mean, const float* rstd,
+                 const int* tids, int tvocab, void* ds_out, float* part_pos, float* part_tg, void* dWp, void* dWt,
+                 void* dgamma, void* dbeta, int64_t B, int cols, int S, uint64_t seed, uint64_t offset,
+                 uint32_t thresh, float scale, int xdt, int wdt, hipStream_t s) {
+  if (B == 0) return 0;
+  if (tvocab < 1 || tvocab > 2) return -3;
+  const int vpt = bdaln_vpt(cols);
+  const int nwt = embed_nwt(B);
+  const dim3 grid((unsigned)S, (unsigned)(nwt / 4));
+  EW_DISPATCH(xdt, T, EW_DISPATCH(wdt, W, EW_VPT(vpt, VPT, {
+    if (thresh)
+      hipLaunchKernelGGL((embed_ln_bwd_kernel<T, W, VPT, true>), grid, dim3(kEwBlock), 0, s, (const T*)dy,
+                         (const T*)s_in, (const W*)gamma, mean, rstd, tids, (T*)ds_out, part_pos, part_tg, B, cols, S,
+                         nwt, seed, offset, thresh, scale);
+    else
+      hipLaunchKernelGGL((embed_ln_bwd_kernel<T, W, VPT, false>), grid, dim3(kEwBlock), 0, s, (const T*)dy,
+                         (const T*)s_in, (const W*)gamma, mean, rstd, tids, (T*)ds_out, part_pos, part_tg, B, cols, S,
+                         nwt, seed, offset, thresh, scale);
+    // position rows: sum over the nwt wave partials; gamma / beta and the two type rows over S * nwt
+    launch_partial_colsum3<T>(part_pos, nwt, (int64_t)S * cols, S * cols, (T*)dWp, (T*)nullptr, (T*)nullptr, s);
+    launch_partial_colsum3<W>(part_tg, S * nwt, 4 * (int64_t)cols, cols, (W*)dgamma, (W*)dbeta, (W*)nullptr, s);
+    launch_partial_colsum3<T>(part_tg + 2 * cols, S * nwt, 4 * (int64_t)cols, tvocab * cols, (T*)dWt, (T*)nullptr,
+                              (T*)nullptr, s);
+  })));
+  return (int)hipGetLastError();
+}
+
+int embed_segsum(const void* ds, const int* sorted, const int64_t* perm, void* dW, int64_t R, int cols, int xdt,
+                 hipStream_t s) {
+  if (R == 0) return 0;
+  const int vpt = bdaln_vpt(cols);
+  const dim3 grid((unsigned)((R + 3) / 4));
+  EW_DISPATCH(xdt, T, EW_VPT(vpt, VPT,
+      hipLaunchKernelGGL((embed_segsum_kernel<T, VPT>), grid, dim3(kEwBlock), 0, s, (const T*)ds, sorted, perm, (T*)dW,
+                         R, cols)));
   return (int)hipGetLastError();
 }
 

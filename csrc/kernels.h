@@ -135,6 +135,19 @@ int bdaln_supported(int cols);
 int bdaln_fwd(const void* x, const void* b, const void* res, const void* gamma, const void* beta, void* y,
               void* s_out, float* mean, float* rstd, int64_t rows, int cols, float eps, uint64_t seed,
               uint64_t offset, uint32_t thresh, float scale, int xdt, int wdt, hipStream_t s);
+// BERT embeddings: s = Ww[id] + Wp[row % S] + Wt[type]; y = dropout(LN(s)); backward -> ds, dWp, dWt
+// (type vocab <= 2), dgamma, dbeta; embed_segsum: word rows from the id-sorted token list
+int embed_ln_fwd(const int* ids, const int* tids, const void* Ww, const void* Wp, const void* Wt, const void* gamma,
+                 const void* beta, void* y, void* s_out, float* mean, float* rstd, int64_t rows, int cols, int S,
+                 float eps, uint64_t seed, uint64_t offset, uint32_t thresh, float scale, int xdt, int wdt,
+                 hipStream_t s);
+int embed_nwt(int64_t B);
+int embed_ln_bwd(const void* dy, const void* s_in, const void* gamma, const float* mean, const float* rstd,
+                 const int* tids, int tvocab, void* ds_out, float* part_pos, float* part_tg, void* dWp, void* dWt,
+                 void* dgamma, void* dbeta, int64_t B, int cols, int S, uint64_t seed, uint64_t offset,
+                 uint32_t thresh, float scale, int xdt, int wdt, hipStream_t s);
+int embed_segsum(const void* ds, const int* sorted, const int64_t* perm, void* dW, int64_t R, int cols, int xdt,
+                 hipStream_t s);
 int64_t bdaln_ws_floats(int64_t rows, int cols);
 int bdaln_bwd(const void* dy, const void* s_in, const void* gamma, const float* mean, const float* rstd,
               void* dres, void* dx, void* dgamma, void* dbeta, void* dbias, float* ws, int64_t rows,
