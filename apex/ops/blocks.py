@@ -28,7 +28,7 @@ import torch
 
 from .. import _ext
 from . import gemm as G
-from .fused import ACT_GELU, _2d, _seed, _wgrad
+from .fused import ACT_GELU, _2d, _gt, _seed, _wgrad
 
 
 # MLP forward keeps gelu'(h) for the backward (EPI_BIAS_GELU_D + EPI_MUL) by default;
@@ -54,6 +54,7 @@ class _AttnSublayer(torch.autograd.Function):
         y, s, mean, rstd = C.bdaln_fwd(t, bo, x2.contiguous(), gamma, beta, float(eps), float(p_hidden), sh, oh)
         ctx.save_for_backward(x2, wqkv, qkv, o, lse, k_lens, dmask, wo, s, gamma, mean, rstd)
         ctx.f8 = f8
+        ctx.params = (wqkv, bqkv, wo, bo, gamma, beta)
         ctx.cfg = (B, S, E, heads, d, scale, causal, p_attn, sa, oa, p_hidden, sh, oh, bqkv is not None,
                    bo is not None, bqkv.dtype if bqkv is not None else None)
         return y.view(B, S, E)
@@ -63,10 +64,13 @@ class _AttnSublayer(torch.autograd.Function):
         C = _ext.require()
         x2, wqkv, qkv, o, lse, k_lens, dmask, wo, s, gamma, mean, rstd = ctx.saved_tensors
         B, S, E, heads, d, scale, causal, p_attn, sa, oa, p_hidden, sh, oh, has_bqkv, has_bo, bdt = ctx.cfg
-        dres, dt, dgamma, dbeta, dbo = C.bdaln_bwd(_2d(dy), s, gamma, mean, rstd, float(p_hidden), sh, oh, has_bo)
+        pqkv, pbqkv, pwo, pbo, pg, pb = ctx.params
+        dres, dt, dgamma, dbeta, dbo = C.bdaln_bwd(_2d(dy), s, gamma, mean, rstd, float(p_hidden), sh, oh, has_bo,
+                                                   dgamma_out=_gt(pg), dbeta_out=_gt(pb),
+                                                   dbias_out=_gt(pbo) if has_bo else None)
         f8 = ctx.f8
         dctx = G.dgrad(dt, wo, f8=f8).view(B, S, heads, d)
-        dwo = _wgrad(dt, o.view(B * S, E))
+        dwo = _wgrad(dt, o.view(B * S, E), out=_gt(pwo))
         q, k, v = qkv.view(B, S, 3, heads, d).unbind(2)
         dqkv = torch.empty_like(qkv)
         dq, dk, dv = dqkv.view(B, S, 3, heads, d).unbind(2)
@@ -75,9 +79,9 @@ class _AttnSublayer(torch.autograd.Function):
         dsum = torch.zeros(B, 3 * E, device=dqkv.device, dtype=torch.float32) if has_bqkv else None
         C.flash_attn_bwd(dctx, q, k, v, o, lse, dq, dk, dv, bool(causal), scale, float(p_attn), sa, oa, k_lens,
                          dmask, dsum)
-        dbqkv = C.partial_colsum(dsum, bdt) if has_bqkv else None
+        dbqkv = C.partial_colsum(dsum, bdt, _gt(pbqkv)) if has_bqkv else None
         dx = G.dgrad_resid(dqkv, wqkv, dres, f8=f8)  # residual grad accumulated in the GEMM epilogue
-        dwqkv = _wgrad(dqkv, x2)
+        dwqkv = _wgrad(dqkv, x2, out=_gt(pqkv))
         return (dx.view(B, S, E), dwqkv, dbqkv, dwo, dbo if has_bo else None, dgamma, dbeta,
                 None, None, None, None, None, None)
 
@@ -102,6 +106,7 @@ class _FFNSublayer(torch.autograd.Function):
         y, s, mean, rstd = C.bdaln_fwd(t, b2, x2.contiguous(), gamma, beta, float(eps), float(p), seed, off)
         ctx.save_for_backward(x2, w1, hb, h, g, w2, s, gamma, mean, rstd)
         ctx.cfg = (p, seed, off, act, b2 is not None, b1.dtype if b1 is not None else None)
+        ctx.params = (w1, b1, w2, b2, gamma, beta)
         return y.view_as(x)
 
     @staticmethod
@@ -110,17 +115,24 @@ class _FFNSublayer(torch.autograd.Function):
         x2, w1, hb, h, g, w2, s, gamma, mean, rstd = ctx.saved_tensors
         p, seed, off, act, has_b2, b1dt = ctx.cfg
         f8 = ctx.f8
-        dres, dt, dgamma, dbeta, db2 = C.bdaln_bwd(_2d(dy), s, gamma, mean, rstd, float(p), seed, off, has_b2)
+        pw1, pb1, pw2, pb2, pg, pb = ctx.params
+        dres, dt, dgamma, dbeta, db2 = C.bdaln_bwd(_2d(dy), s, gamma, mean, rstd, float(p), seed, off, has_b2,
+                                                   dgamma_out=_gt(pg), dbeta_out=_gt(pb),
+                                                   dbias_out=_gt(pb2) if has_b2 else None)
         if hb is None and act == ACT_GELU and b1dt is not None:
+            tb1 = _gt(pb1)
             if _STORE_DERIV:
-                dh, db1 = G.dgrad_mul(dt, w2, h, b1dt, f8=f8)  # (dt W2) * gelu'(h) (stored) and its column sums
+                # (dt W2) * gelu'(h) (stored) and its column sums
+                dh, db1 = G.dgrad_mul(dt, w2, h, b1dt, f8=f8, bias_grad_out=tb1)
             else:
-                dh, db1 = G.dgrad_dgelu(dt, w2, h, b1dt, f8=f8)  # (dt W2) * gelu'(h) from h
+                dh, db1 = G.dgrad_dgelu(dt, w2, h, b1dt, f8=f8, bias_grad_out=tb1)  # (dt W2) * gelu'(h) from h
+            if tb1 is not None and db1 is not None and db1.data_ptr() != tb1.data_ptr():
+                db1 = tb1.copy_(db1)  # a path that could not write the slot: keep the handed-out view valid
         else:
             dh, db1 = C.bias_act_bwd(G.dgrad(dt, w2, f8=f8), h, hb, act)
-        dw2 = _wgrad(dt, g)
+        dw2 = _wgrad(dt, g, out=_gt(pw2))
         dx = G.dgrad_resid(dh, w1, dres, f8=f8)  # residual grad accumulated in the GEMM epilogue
-        dw1 = _wgrad(dh, x2)
+        dw1 = _wgrad(dh, x2, out=_gt(pw1))
         return (dx.view_as(dy), dw1, db1 if b1dt is not None else None, dw2, db2 if has_b2 else None, dgamma,
                 dbeta, None, None, None)
 

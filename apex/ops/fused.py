@@ -76,8 +76,17 @@ def _wgrad_splits(M, N, K):
     return s
 
 
-def _wgrad(dy2, x2):
-    """Weight gradient dy2^T @ x2 in dy2's dtype (split-K batched GEMM when it pays)."""
+def _gt(p):
+    """The parameter's DDP bucket slot to write its gradient into, or None
+    (apex.parallel.distributed.grad_target)."""
+    from ..parallel.distributed import grad_target
+
+    return grad_target(p) if p is not None else None
+
+
+def _wgrad(dy2, x2, out=None):
+    """Weight gradient dy2^T @ x2 in dy2's dtype (split-K batched GEMM when it pays), written into
+    ``out`` when given (a gradient-bucket slot)."""
     M, N = dy2.shape
     K = x2.shape[1]
     s = _wgrad_splits(M, N, K) if dy2.dtype in (torch.bfloat16, torch.float16) else 1
@@ -89,11 +98,12 @@ def _wgrad(dy2, x2):
         if C.gemm_tt_supported(dy2, x2, st):
             # hand-written transposed-read MFMA GEMM (csrc/gemm.hip, TR main loop); at parity with
             # the library here (profiles/r1_gemm_policy.jsonl), so only in the all-MFMA mode
-            return C.gemm_tt(dy2, x2, st, dy2.dtype)
+            r = C.gemm_tt(dy2, x2, st, dy2.dtype)
+            return out.copy_(r) if out is not None else r
     if s == 1 or not (dy2.is_contiguous() and x2.is_contiguous()):
-        return torch.mm(dy2.t(), x2)
+        return torch.mm(dy2.t(), x2, out=out) if out is not None else torch.mm(dy2.t(), x2)
     slabs = torch.bmm(dy2.view(s, M // s, N).transpose(1, 2), x2.view(s, M // s, K), out_dtype=torch.float32)
-    return _ext.require().splitk_reduce(slabs, dy2.dtype)
+    return _ext.require().splitk_reduce(slabs, dy2.dtype, out)
 
 
 # ---------------------------------------------------------------------------
@@ -121,6 +131,7 @@ class _FusedDense(torch.autograd.Function):
         ctx.f8 = G.fp8_state()
         y = G.linear(x2, w, b, f8=ctx.f8)
         ctx.save_for_backward(x2, w)
+        ctx.params = (w, b)
         ctx.has_b = b is not None
         ctx.bdtype = b.dtype if b is not None else None
         return y.view(*x.shape[:-1], w.shape[0])
@@ -135,7 +146,7 @@ class _FusedDense(torch.autograd.Function):
 
             dx = G.dgrad(dy2, w, f8=ctx.f8).view(*dy.shape[:-1], w.shape[1])
         if ctx.needs_input_grad[1]:
-            dw = _wgrad(dy2, x2)
+            dw = _wgrad(dy2, x2, out=_gt(ctx.params[0]))
         if ctx.has_b and ctx.needs_input_grad[2]:
             db = _ext.require().colsum(dy2, ctx.bdtype)
         return dx, dw, db
@@ -254,6 +265,7 @@ class _BertEmbeddings(torch.autograd.Function):
         y, sv, mean, rstd = C.embed_ln_fwd(ids32, t32, Ww, Wp, Wt, gamma, beta, float(eps), float(p), seed, off)
         ctx.save_for_backward(ids32, t32, sv, gamma, mean, rstd)
         ctx.cfg = (float(p), seed, off, V, Wp.shape[0], TV)
+        ctx.params = (Ww, Wp, Wt, gamma, beta)
         return y
 
     @staticmethod
@@ -261,9 +273,12 @@ class _BertEmbeddings(torch.autograd.Function):
         C = _ext.require()
         ids32, t32, sv, gamma, mean, rstd = ctx.saved_tensors
         p, seed, off, V, npos, TV = ctx.cfg
-        ds, dWp, dWt, dg, db = C.embed_ln_bwd(dy, sv, gamma, mean, rstd, t32, TV, npos, p, seed, off)
+        pw, pp, pt, pg, pb = ctx.params
+        ds, dWp, dWt, dg, db = C.embed_ln_bwd(dy, sv, gamma, mean, rstd, t32, TV, npos, p, seed, off,
+                                              dwp_out=_gt(pp), dwt_out=_gt(pt), dgamma_out=_gt(pg),
+                                              dbeta_out=_gt(pb))
         sorted_ids, perm = torch.sort(ids32.view(-1), stable=True)
-        dWw = C.embed_segsum(ds, sorted_ids, perm, V)
+        dWw = C.embed_segsum(ds, sorted_ids, perm, V, _gt(pw))
         return None, None, dWw, dWp, dWt, dg, db, None, None
 
 
@@ -304,6 +319,7 @@ class _DenseBDALN(torch.autograd.Function):
                                        seed, off)
         ctx.save_for_backward(x2, w, s, gamma, mean, rstd)
         ctx.cfg = (p, seed, off, b is not None)
+        ctx.params = (w, b, gamma, beta)
         return y.view(*x.shape[:-1], w.shape[0])
 
     @staticmethod
@@ -311,11 +327,14 @@ class _DenseBDALN(torch.autograd.Function):
         C = _ext.require()
         x2, w, s, gamma, mean, rstd = ctx.saved_tensors
         p, seed, off, has_b = ctx.cfg
-        dres, dt, dg, dbeta, db = C.bdaln_bwd(_2d(dy), s, gamma, mean, rstd, float(p), seed, off, has_b)
+        pw, pb, pg, pbeta = ctx.params
+        dres, dt, dg, dbeta, db = C.bdaln_bwd(_2d(dy), s, gamma, mean, rstd, float(p), seed, off, has_b,
+                                              dgamma_out=_gt(pg), dbeta_out=_gt(pbeta),
+                                              dbias_out=_gt(pb) if has_b else None)
         from . import gemm as G
 
         dx = G.dgrad(dt, w, f8=ctx.f8).view(*dy.shape[:-1], w.shape[1]) if ctx.needs_input_grad[0] else None
-        dw = _wgrad(dt, x2) if ctx.needs_input_grad[1] else None
+        dw = _wgrad(dt, x2, out=_gt(pw)) if ctx.needs_input_grad[1] else None
         return dx, dw, (db if has_b else None), dres.view_as(dy), dg, dbeta, None, None
 
 

@@ -140,8 +140,9 @@ def linear_gelu_d(x, w, b, act=ACT_GELU, f8=None):
     return y.view(shp), gd.view(shp)
 
 
-def dgrad_mul(dy, w, gd, bias_dtype, wT=None, f8=None):
-    """(dh, db): dh = (dy @ w) * gd (gd = the stored activation derivative), db = column sums of dh."""
+def dgrad_mul(dy, w, gd, bias_dtype, wT=None, f8=None, bias_grad_out=None):
+    """(dh, db): dh = (dy @ w) * gd (gd = the stored activation derivative), db = column sums of dh
+    (written into ``bias_grad_out`` on the MFMA path when given)."""
     a = _2d(dy)
     g2 = _2d(gd)
     C = _C()
@@ -151,7 +152,7 @@ def dgrad_mul(dy, w, gd, bias_dtype, wT=None, f8=None):
     if _MODE != "blas" and a.is_cuda and g2.is_contiguous() and g2.dtype == a.dtype:
         wT = transpose(w) if wT is None else wT
         if use_mfma(a, wT):
-            dh, db = C.gemm(a, wT, C.EPI_MUL, None, g2, bias_dtype)
+            dh, db = C.gemm(a, wT, C.EPI_MUL, None, g2, bias_dtype, bias_grad_out)
             return dh, db
     dh = torch.mm(a, w) * g2
     db = C.colsum(dh, bias_dtype) if bias_dtype is not None else None
@@ -191,8 +192,9 @@ def dgrad_resid(dy, w, r, wT=None, f8=None):
     return torch.addmm(r2, a, w).view(*dy.shape[:-1], w.shape[1])
 
 
-def dgrad_dgelu(dy, w, h, bias_dtype, wT=None, act=ACT_GELU, f8=None):
-    """(dh, db): dh = (dy @ w) * gelu'(h), db = column sums of dh (in bias_dtype)."""
+def dgrad_dgelu(dy, w, h, bias_dtype, wT=None, act=ACT_GELU, f8=None, bias_grad_out=None):
+    """(dh, db): dh = (dy @ w) * gelu'(h), db = column sums of dh (in bias_dtype; written into
+    ``bias_grad_out`` on the MFMA path when given)."""
     a = _2d(dy)
     h2 = _2d(h)
     C = _C()
@@ -204,7 +206,7 @@ def dgrad_dgelu(dy, w, h, bias_dtype, wT=None, act=ACT_GELU, f8=None):
         wT = transpose(w) if wT is None else wT
         if use_mfma(a, wT):
             epi = C.EPI_DGELU_TANH if act == ACT_GELU_TANH else C.EPI_DGELU
-            dh, db = C.gemm(a, wT, epi, None, h2, bias_dtype)
+            dh, db = C.gemm(a, wT, epi, None, h2, bias_dtype, bias_grad_out)
             return dh, db
     dg = torch.mm(a, w)
     dh, _ = C.bias_act_bwd(dg, h2, None, act)

@@ -91,8 +91,18 @@ class FusedOptimizerBase(Optimizer):
                     flats[id(f)] = f
                     members[id(f)] = members.get(id(f), 0) + 1
         whole = {k for k, f in flats.items() if members[k] == getattr(f, "_apex_nparams", -1)}
-        for k in whole:
-            flats[k].zero_()
+        if set_none:
+            # release the bucket views instead of zero-filling the buffers: the next backward's
+            # fused producers then write each gradient straight into its slot
+            # (apex.parallel.grad_target) and the rest are copied in by DDP, so no parameter pays
+            # an accumulate kernel; DDP zero-fills the slots of parameters that get no gradient
+            for ps in groups:
+                for p in ps:
+                    if p.grad is not None and id(getattr(p, "_apex_bucket_flat", None)) in whole:
+                        p.grad = None
+        else:
+            for k in whole:
+                flats[k].zero_()
         for ps in groups:
             for p in ps:
                 if p.grad is None:

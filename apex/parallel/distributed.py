@@ -194,6 +194,27 @@ class _Bucket:
         return self.flat[self.start:self.start + self.numel]
 
 
+_TARGETS_GIVEN = set()  # ids of params whose bucket slot was handed out in the current backward
+
+
+def grad_target(p):
+    """Where a fused backward may write ``p``'s gradient directly: a FRESH view of p's slot in
+    its apex DDP gradient bucket, when p has no gradient yet in this backward (the fused
+    optimizers' ``zero_grad`` releases the views instead of zero-filling the buckets). The
+    producer writes the whole gradient there and returns the view; autograd then adopts it as
+    ``p.grad`` without a copy (a fresh, unshared view is what lets AccumulateGrad steal it) and
+    the bucket needs no accumulate kernel. ``None``: allocate as usual (no DDP, not contiguous,
+    or a gradient is already accumulating, e.g. inside ``no_sync()`` micro-batches)."""
+    slot = getattr(p, "_apex_grad_slot", None)
+    if slot is None or p.grad is not None or id(p) in _TARGETS_GIVEN:
+        # (a second producer of the same parameter in one backward — tied weights — must not
+        # write the slot too: autograd sums both results before p.grad is set)
+        return None
+    _TARGETS_GIVEN.add(id(p))
+    flat, off, n = slot
+    return flat.narrow(0, off, n).view(p.shape)
+
+
 class DistributedDataParallel(Module):
     """Bucketed, backward-overlapped data parallelism over RCCL.
 
@@ -357,6 +378,7 @@ class DistributedDataParallel(Module):
             self._reduce_now(flat)
 
     def forward(self, *inputs, **kwargs):
+        _TARGETS_GIVEN.clear()
         self._callback_queued = False
         self._next_bucket = 0
         self._trigger_seen = 0
@@ -487,6 +509,7 @@ class DistributedDataParallel(Module):
                 cur.wait_stream(s)
 
     def _end_of_backward(self):
+        _TARGETS_GIVEN.clear()
         ev0 = None
         if self.comm_timing and self._cuda:
             ev0 = torch.cuda.Event(enable_timing=True)
@@ -498,8 +521,11 @@ class DistributedDataParallel(Module):
             self._layout_ready = True
             return
         if self.delay_allreduce:
+            for idx, p in enumerate(self._params):
+                if p.grad is None:  # no grad this step (zero_grad released the view)
+                    self._views[idx].zero_()
+                    p.grad = self._views[idx]
             for flat in self._flat.values():
-                # any param that produced no grad this step still has a view (zeroed)
                 self._reduce_now(flat)
         else:
             # params that did not receive a grad this iteration: treat as ready (zero grads)
@@ -590,6 +616,10 @@ class DistributedDataParallel(Module):
                     v.copy_(p.grad)
                 p.grad = v
                 p._apex_grad_is_bucket_view = True
+                if p.is_contiguous():
+                    # lets a fused producer write this param's gradient straight into the bucket
+                    # (apex.parallel.grad_target)
+                    p._apex_grad_slot = (flat, off, n)
                 p._apex_bucket_flat = flat
                 self._views[i] = v
                 cur.append(i)

@@ -430,6 +430,19 @@ std::pair<uint32_t, float> drop_params(double p) {
 
 int64_t cols_of(const Tensor& x) { return x.dim() ? x.size(-1) : 1; }
 
+// optional caller-provided output (e.g. a parameter's slot in a DDP gradient bucket, so the
+// gradient lands there with no copy); checked against the shape / dtype the op would allocate
+Tensor out_or_empty(const c10::optional<Tensor>& out, at::IntArrayRef sizes, const at::TensorOptions& opt,
+                    const char* what) {
+  if (out.has_value() && out->defined()) {
+    TORCH_CHECK(out->is_contiguous() && out->numel() == c10::multiply_integers(sizes) &&
+                    out->scalar_type() == opt.dtype().toScalarType() && out->device() == opt.device(),
+                what, ": out must be a contiguous tensor of the result's size, dtype and device");
+    return *out;
+  }
+  return at::empty(sizes, opt);
+}
+
 Tensor k_bias_act_fwd(Tensor x, const c10::optional<Tensor>& b, int64_t act) {
   TORCH_CHECK(x.is_contiguous(), "bias_act: x must be contiguous");
   const int64_t cols = cols_of(x), rows = x.numel() / std::max<int64_t>(cols, 1);
@@ -500,10 +513,10 @@ Tensor k_colsum(Tensor x, at::ScalarType out_dtype) {
 }
 
 // split-K combine: slabs fp32 [S, ...] -> sum over S in out_dtype, shape slabs.shape[1:]
-Tensor k_splitk_reduce(Tensor slabs, at::ScalarType out_dtype) {
+Tensor k_splitk_reduce(Tensor slabs, at::ScalarType out_dtype, const c10::optional<Tensor>& out_opt) {
   TORCH_CHECK(slabs.is_cuda() && slabs.scalar_type() == at::kFloat && slabs.dim() >= 2, "splitk_reduce: fp32 slabs");
   Tensor sc = slabs.contiguous();
-  Tensor out = at::empty(sc.sizes().slice(1), sc.options().dtype(out_dtype));
+  Tensor out = out_or_empty(out_opt, sc.sizes().slice(1), sc.options().dtype(out_dtype), "splitk_reduce");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(sc.data_ptr()) % 16 == 0 && (out.numel() % 4 == 0 || sc.size(0) == 1),
               "splitk_reduce: alignment");
   check(apex::splitk_reduce(sc.data_ptr<float>(), out.data_ptr(), out.numel(), (int)sc.size(0), dt_code(out_dtype),
@@ -531,12 +544,14 @@ std::vector<Tensor> k_bdaln_fwd(Tensor x, const c10::optional<Tensor>& b, Tensor
 }
 
 std::vector<Tensor> k_bdaln_bwd(Tensor dy, Tensor s, Tensor gamma, Tensor mean, Tensor rstd, double p,
-                                int64_t seed, int64_t offset, bool has_bias) {
+                                int64_t seed, int64_t offset, bool has_bias, const c10::optional<Tensor>& dgamma_out,
+                                const c10::optional<Tensor>& dbeta_out, const c10::optional<Tensor>& dbias_out) {
   Tensor dyc = dy.contiguous();
   const int64_t cols = cols_of(s), rows = s.numel() / std::max<int64_t>(cols, 1);
   Tensor dres = at::empty_like(s), dx = at::empty_like(s);
-  Tensor dgamma = at::empty_like(gamma), dbeta = at::empty_like(gamma);
-  Tensor dbias = has_bias ? at::empty_like(gamma) : Tensor();
+  Tensor dgamma = out_or_empty(dgamma_out, gamma.sizes(), gamma.options(), "bdaln_bwd dgamma");
+  Tensor dbeta = out_or_empty(dbeta_out, gamma.sizes(), gamma.options(), "bdaln_bwd dbeta");
+  Tensor dbias = has_bias ? out_or_empty(dbias_out, gamma.sizes(), gamma.options(), "bdaln_bwd dbias") : Tensor();
   Tensor ws = at::empty({apex::bdaln_ws_floats(rows, (int)cols)}, s.options().dtype(at::kFloat));
   auto dp = drop_params(p);
   check(apex::bdaln_bwd(dyc.data_ptr(), s.data_ptr(), gamma.data_ptr(), mean.data_ptr<float>(),
@@ -582,7 +597,9 @@ std::vector<Tensor> k_embed_ln_fwd(Tensor ids, const c10::optional<Tensor>& tids
 // -> {ds [B, S, H], dWp [npos, H] (rows >= S zero), dWt [tvocab, H], dgamma, dbeta}
 std::vector<Tensor> k_embed_ln_bwd(Tensor dy, Tensor sv, Tensor gamma, Tensor mean, Tensor rstd,
                                    const c10::optional<Tensor>& tids, int64_t tvocab, int64_t npos, double p,
-                                   int64_t seed, int64_t offset) {
+                                   int64_t seed, int64_t offset, const c10::optional<Tensor>& dwp_out,
+                                   const c10::optional<Tensor>& dwt_out, const c10::optional<Tensor>& dgamma_out,
+                                   const c10::optional<Tensor>& dbeta_out) {
   Tensor dyc = dy.contiguous();
   TORCH_CHECK(sv.dim() == 3 && dyc.sizes() == sv.sizes(), "embed_ln_bwd: shapes");
   const int64_t B = sv.size(0), S = sv.size(1), H = sv.size(2);
@@ -590,9 +607,11 @@ std::vector<Tensor> k_embed_ln_bwd(Tensor dy, Tensor sv, Tensor gamma, Tensor me
   const int* tp = nullptr;
   if (tids.has_value() && tids->defined()) tp = tids->data_ptr<int>();
   Tensor ds = at::empty_like(sv);
-  Tensor dWp = at::zeros({npos, H}, sv.options());
-  Tensor dWt = at::empty({tvocab, H}, sv.options());
-  Tensor dgamma = at::empty_like(gamma), dbeta = at::empty_like(gamma);
+  Tensor dWp = out_or_empty(dwp_out, {npos, H}, sv.options(), "embed_ln_bwd dWp");
+  if (npos > S) dWp.view({npos, H}).narrow(0, S, npos - S).zero_();  // positions past S: no gradient
+  Tensor dWt = out_or_empty(dwt_out, {tvocab, H}, sv.options(), "embed_ln_bwd dWt");
+  Tensor dgamma = out_or_empty(dgamma_out, gamma.sizes(), gamma.options(), "embed_ln_bwd dgamma");
+  Tensor dbeta = out_or_empty(dbeta_out, gamma.sizes(), gamma.options(), "embed_ln_bwd dbeta");
   const int nwt = apex::embed_nwt(B);
   auto fo = sv.options().dtype(at::kFloat);
   Tensor part_pos = at::empty({(int64_t)nwt * S * H}, fo);
@@ -608,13 +627,14 @@ std::vector<Tensor> k_embed_ln_bwd(Tensor dy, Tensor sv, Tensor gamma, Tensor me
 }
 
 // dW [vocab, H]: zero rows, plus the ds rows of every token summed into its id's row
-Tensor k_embed_segsum(Tensor ds, Tensor sorted_ids, Tensor perm, int64_t vocab) {
+Tensor k_embed_segsum(Tensor ds, Tensor sorted_ids, Tensor perm, int64_t vocab, const c10::optional<Tensor>& out) {
   TORCH_CHECK(ds.is_contiguous() && sorted_ids.scalar_type() == at::kInt && perm.scalar_type() == at::kLong &&
                   sorted_ids.is_contiguous() && perm.is_contiguous() && sorted_ids.numel() == perm.numel(),
               "embed_segsum: int32 sorted ids, int64 permutation");
   const int64_t H = ds.size(-1), R = ds.numel() / H;
   TORCH_CHECK(sorted_ids.numel() == R, "embed_segsum: one id per ds row");
-  Tensor dW = at::zeros({vocab, H}, ds.options());
+  Tensor dW = out_or_empty(out, {vocab, H}, ds.options(), "embed_segsum");
+  dW.zero_();
   check(apex::embed_segsum(ds.data_ptr(), sorted_ids.data_ptr<int>(), perm.data_ptr<int64_t>(), dW.data_ptr(), R,
                            (int)H, dt_code(ds.scalar_type()), cur_stream()),
         "embed_segsum");
@@ -885,7 +905,8 @@ bool k_gemm_supported(Tensor a, Tensor b) {
 }
 
 std::vector<Tensor> k_gemm(Tensor a, Tensor b, int64_t epi, const c10::optional<Tensor>& bias,
-                           const c10::optional<Tensor>& aux, c10::optional<at::ScalarType> bias_grad_dtype) {
+                           const c10::optional<Tensor>& aux, c10::optional<at::ScalarType> bias_grad_dtype,
+                           const c10::optional<Tensor>& bias_grad_out) {
   TORCH_CHECK(k_gemm_supported(a, b), "gemm: unsupported operands (bf16/fp16, K % 64 == 0, N % 8 == 0, "
               "16-byte aligned, unit inner stride)");
   const int64_t K = a.size(-1), N = b.size(0), M = a.numel() / K;
@@ -933,7 +954,7 @@ std::vector<Tensor> k_gemm(Tensor a, Tensor b, int64_t epi, const c10::optional<
   }
   check(apex::gemm_nt(g, dt_code(a.scalar_type()), cur_stream()), "gemm");
   if (dgelu && bias_grad_dtype.has_value()) {
-    extra = at::empty({N}, a.options().dtype(*bias_grad_dtype));
+    extra = out_or_empty(bias_grad_out, {N}, a.options().dtype(*bias_grad_dtype), "gemm bias grad");
     check(apex::gemm_bias_grad(part.data_ptr<float>(), (int)part.size(0), (int)N, extra.data_ptr(),
                                dt_code(*bias_grad_dtype), cur_stream()),
           "gemm_bias_grad");
@@ -1128,14 +1149,14 @@ Tensor k_gemm_tt(Tensor a, Tensor b, int64_t splits, at::ScalarType out_dtype) {
   g.part = slabs.data_ptr<float>();
   g.epi = apex::EPI_F32;
   check(apex::gemm_tt(g, dt_code(a.scalar_type()), cur_stream()), "gemm_tt");
-  return k_splitk_reduce(slabs, out_dtype);
+  return k_splitk_reduce(slabs, out_dtype, c10::nullopt);
 }
 
 // sum the rows of an fp32 [P, N] partials tensor -> [N] in out_dtype
-Tensor k_partial_colsum(Tensor part, at::ScalarType out_dtype) {
+Tensor k_partial_colsum(Tensor part, at::ScalarType out_dtype, const c10::optional<Tensor>& out_opt) {
   TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.dim() == 2 && part.is_contiguous(),
               "partial_colsum: contiguous fp32 [P, N]");
-  Tensor out = at::empty({part.size(1)}, part.options().dtype(out_dtype));
+  Tensor out = out_or_empty(out_opt, {part.size(1)}, part.options().dtype(out_dtype), "partial_colsum");
   check(apex::gemm_bias_grad(part.data_ptr<float>(), (int)part.size(0), (int)part.size(1), out.data_ptr(),
                              dt_code(out_dtype), cur_stream()),
         "partial_colsum");
@@ -1196,7 +1217,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("o"), py::arg("lse"), py::arg("dq"), py::arg("dk"), py::arg("dv"), py::arg("causal"),
         py::arg("scale"), py::arg("p_drop"), py::arg("seed"), py::arg("offset"), py::arg("k_lens"),
         py::arg("dmask"), py::arg("dsum") = py::none(), py::arg("dbg") = 0, py::arg("bias") = py::none());
-  m.def("partial_colsum", &k_partial_colsum);
+  m.def("partial_colsum", &k_partial_colsum, py::arg("part"), py::arg("out_dtype"), py::arg("out") = py::none());
   m.def("flash_dropout_mask", &flash_dropout_mask);
   m.def("weight_norm_fwd", &k_wn_fwd);
   m.def("weight_norm_bwd", &k_wn_bwd);
@@ -1217,17 +1238,23 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bias_dropout_add_fwd", &k_bda_fwd);
   m.def("bias_dropout_add_bwd", &k_bda_bwd);
   m.def("colsum", &k_colsum);
-  m.def("splitk_reduce", &k_splitk_reduce);
+  m.def("splitk_reduce", &k_splitk_reduce, py::arg("slabs"), py::arg("out_dtype"), py::arg("out") = py::none());
   m.def("bdaln_supported", &k_bdaln_supported);
   m.def("bdaln_fwd", &k_bdaln_fwd);
   m.def("embed_ln_fwd", &k_embed_ln_fwd);
-  m.def("embed_ln_bwd", &k_embed_ln_bwd);
-  m.def("embed_segsum", &k_embed_segsum);
-  m.def("bdaln_bwd", &k_bdaln_bwd);
+  m.def("embed_ln_bwd", &k_embed_ln_bwd, py::arg("dy"), py::arg("s"), py::arg("gamma"), py::arg("mean"),
+        py::arg("rstd"), py::arg("tids"), py::arg("tvocab"), py::arg("npos"), py::arg("p"), py::arg("seed"),
+        py::arg("offset"), py::arg("dwp_out") = py::none(), py::arg("dwt_out") = py::none(),
+        py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none());
+  m.def("embed_segsum", &k_embed_segsum, py::arg("ds"), py::arg("sorted_ids"), py::arg("perm"), py::arg("vocab"),
+        py::arg("out") = py::none());
+  m.def("bdaln_bwd", &k_bdaln_bwd, py::arg("dy"), py::arg("s"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"),
+        py::arg("p"), py::arg("seed"), py::arg("offset"), py::arg("has_bias"), py::arg("dgamma_out") = py::none(),
+        py::arg("dbeta_out") = py::none(), py::arg("dbias_out") = py::none());
   m.def("input_normalize", &k_input_normalize);
   m.def("gemm_supported", &k_gemm_supported);
   m.def("gemm", &k_gemm, py::arg("a"), py::arg("b"), py::arg("epi") = 0, py::arg("bias") = py::none(),
-        py::arg("aux") = py::none(), py::arg("bias_grad_dtype") = py::none());
+        py::arg("aux") = py::none(), py::arg("bias_grad_dtype") = py::none(), py::arg("bias_grad_out") = py::none());
   m.def("transpose", &k_transpose);
   m.def("gemm_tt_supported", &k_gemm_tt_supported);
   m.def("gemm_tt", &k_gemm_tt);
