@@ -9,6 +9,8 @@ import re
 import pytest
 
 DOCS = os.path.join(os.path.dirname(__file__), "..", "docs", "source")
+if not os.path.isdir(DOCS):  # e.g. a GPU-box snapshot that leaves the docs out (.gpurunignore)
+    pytest.skip("docs/source not present", allow_module_level=True)
 DIRECTIVE = re.compile(r"^\.\. (automodule|autoclass|autofunction|currentmodule):: (\S+)")
 
 
