@@ -153,6 +153,7 @@ class _MLP(torch.autograd.Function):
             g, gd = G.linear_gelu(x2, w1, b1, act, f8=f8)  # gelu(h) and h
         t = G.linear(g, w2, f8=f8)
         ctx.save_for_backward(x2, w1, gd, g, w2)
+        ctx.params = (w1, b1, w2)
         ctx.act = act
         ctx.b1dt = b1.dtype
         return t.view(*x.shape[:-1], w2.shape[0])
@@ -160,14 +161,18 @@ class _MLP(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dt):
         x2, w1, gd, g, w2 = ctx.saved_tensors
+        pw1, pb1, pw2 = ctx.params
         dt2 = _2d(dt).contiguous()
+        tb1 = _gt(pb1)
         if _STORE_DERIV:
-            dh, db1 = G.dgrad_mul(dt2, w2, gd, ctx.b1dt, f8=ctx.f8)
+            dh, db1 = G.dgrad_mul(dt2, w2, gd, ctx.b1dt, f8=ctx.f8, bias_grad_out=tb1)
         else:
-            dh, db1 = G.dgrad_dgelu(dt2, w2, gd, ctx.b1dt, act=ctx.act, f8=ctx.f8)
-        dw2 = _wgrad(dt2, g)
+            dh, db1 = G.dgrad_dgelu(dt2, w2, gd, ctx.b1dt, act=ctx.act, f8=ctx.f8, bias_grad_out=tb1)
+        if tb1 is not None and db1 is not None and db1.data_ptr() != tb1.data_ptr():
+            db1 = tb1.copy_(db1)
+        dw2 = _wgrad(dt2, g, out=_gt(pw2))
         dx = G.dgrad(dh, w1, f8=ctx.f8).view(*dt.shape[:-1], w1.shape[1])
-        dw1 = _wgrad(dh, x2)
+        dw1 = _wgrad(dh, x2, out=_gt(pw1))
         return dx, dw1, db1, dw2, None
 
 
