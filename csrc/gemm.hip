@@ -39,6 +39,8 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <cstdio>
+#include <cstdlib>
 #include <type_traits>
 
 namespace apex {
@@ -694,10 +696,28 @@ __global__ void __launch_bounds__(256) transpose_kernel(const T* __restrict__ in
   }
 }
 
+// per-epilogue first-round stagger units from APEX_GEMM_STAGGER="epi:units,..." (experiment; read once)
+inline int host_stagger(int epi) {
+  static int table[16] = {-1};
+  if (table[0] == -1) {
+    for (int& t : table) t = 0;
+    if (const char* e = getenv("APEX_GEMM_STAGGER")) {
+      int ep = 0, u = 0;
+      const char* p = e;
+      while (*p) {
+        if (sscanf(p, "%d:%d", &ep, &u) == 2 && ep >= 0 && ep < 16) table[ep] = u;
+        while (*p && *p != ',') ++p;
+        if (*p == ',') ++p;
+      }
+    }
+  }
+  return table[epi];
+}
+
 template <typename T, int EPI, bool TR = false>
 void launch_gemm(const GemmArgs& g, hipStream_t s) {
   const int tiles = ((g.M + GB_M - 1) / GB_M) * ((g.N + GB_N - 1) / GB_N);
-  const int stagger = 0;  // see g_gemm_stagger
+  const int stagger = host_stagger(EPI);  // see g_gemm_stagger
   hipLaunchKernelGGL((gemm_nt_kernel<T, EPI, TR>), dim3(tiles, TR ? g.splits : 1), dim3(G_THREADS), 0, s, (const T*)g.A, (const T*)g.B,
                      (T*)g.C, g.M, g.N, g.K, g.lda, g.ldb, g.ldc, (const T*)g.bias, (const T*)g.aux, g.ldaux,
                      (T*)g.aux_out, g.part, stagger);
