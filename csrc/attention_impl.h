@@ -73,6 +73,18 @@ __device__ __forceinline__ s16x4 lds_tr16(const void* p) {
       (__attribute__((address_space(3))) s16x4*)(p));
 }
 
+// LDS row strides (elements) of the 16-bit tiles, by how a tile is read. Bank model of
+// MI355X_MICROARCH.md (LDS table): 16-byte row reads (ds_read_b128) are conflict-free at D + 8;
+// transposed reads (ds_read_b64_tr_b16: 4 rows x 64 B per 32-lane group) need the rows 64 B apart
+// modulo 256 B, i.e. D + 32; a tile read both ways is best at D + 8 (D = 64) / D + 24 (D >= 128),
+// 2-way on the transposed reads. The uniform D + 8 made V's transposed reads 2-way (D = 64) and
+// 4-way (D >= 128) conflicted: 22-48 % of all LDS cycles by rocprofv3 (profiles/r2_pmc_attn.json).
+// (An XOR chunk swizzle makes the both-ways case conflict-free too, but its per-access address
+// arithmetic cost registers — spills at D = 128 — in these VALU-bound loops.)
+template <int D> constexpr int ld_rows() { return D + 8; }
+template <int D> constexpr int ld_tr() { return D == 32 ? D : D + 32; }
+template <int D> constexpr int ld_both() { return D >= 128 ? D + 24 : D + 8; }
+
 // Workgroup barrier ordering LDS traffic only: the fences are restricted to the "local"
 // address space, so outstanding global loads (register prefetches) are NOT drained at the
 // barrier the way __syncthreads()'s full workgroup fence drains them.
@@ -162,10 +174,11 @@ attn_fwd_kernel(AttnArgs a) {
   static_assert(!SHORT || D == 64, "SHORT is the D = 64 single-pass variant");
   using M = MfmaT<T>;
   using V8 = typename M::V8;
-  constexpr int LDR = D + 8;  // padded LDS row (elements)
+  constexpr int LDR = ld_rows<D>();  // K: row reads
+  constexpr int LDV = ld_tr<D>();    // V: transposed reads
   constexpr int NBUF = SHORT ? 2 : 1;
   __shared__ __attribute__((aligned(16))) T lds_k[NBUF * kFwdKB * LDR];
-  __shared__ __attribute__((aligned(16))) T lds_v[NBUF * kFwdKB * LDR];
+  __shared__ __attribute__((aligned(16))) T lds_v[NBUF * kFwdKB * LDV];
 
   // wid through readfirstlane: wave-uniform in SGPRs, so tile-level conditions become scalar branches
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -242,7 +255,7 @@ attn_fwd_kernel(AttnArgs a) {
       const int idx = threadIdx.x + 256 * c;
       const int row = rowoff + idx / CPR, col = (idx % CPR) * 8;
       *(uint4*)(lds_k + row * LDR + col) = kreg[c];
-      *(uint4*)(lds_v + row * LDR + col) = vreg[c];
+      *(uint4*)(lds_v + row * LDV + col) = vreg[c];
     }
   };
 
@@ -316,7 +329,7 @@ attn_fwd_kernel(AttnArgs a) {
           for (int db = 0; db < D / 32; ++db) {
             const int k0 = lr0 + 32 * sb + 16 * s2 + 4 * hl + ((lane & 15) >> 2);
             const int c0 = 32 * db + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-            vt[sb][s2][db] = join4<V8>(lds_tr16(lds_v + k0 * LDR + c0), lds_tr16(lds_v + (k0 + 8) * LDR + c0));
+            vt[sb][s2][db] = join4<V8>(lds_tr16(lds_v + k0 * LDV + c0), lds_tr16(lds_v + (k0 + 8) * LDV + c0));
           }
     }
     // ---- mask (boundary tiles only) + running max on the RAW scores; the softmax scale is
@@ -382,8 +395,8 @@ attn_fwd_kernel(AttnArgs a) {
             o[db] = M::mma(vt[sb][s2][db], pf, o[db]);
           } else {
             const int c0 = 32 * db + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-            const s16x4 lo = lds_tr16(lds_v + k0 * LDR + c0);
-            const s16x4 hi = lds_tr16(lds_v + (k0 + 8) * LDR + c0);
+            const s16x4 lo = lds_tr16(lds_v + k0 * LDV + c0);
+            const s16x4 hi = lds_tr16(lds_v + (k0 + 8) * LDV + c0);
             o[db] = M::mma(join4<V8>(lo, hi), pf, o[db]);
           }
         }
@@ -449,12 +462,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
                                                          void* dk_out, void* dv_out) {
   using M = MfmaT<T>;
   using V8 = typename M::V8;
-  constexpr int LDR = D + 8;
+  constexpr int LDR = D + 8;          // dK / dV emit staging in lds_k (row reads)
+  constexpr int LDQ = ld_both<D>();  // Q / dO: row and transposed reads
   constexpr int LDS_S = kBwdBK + 8;  // dS row stride (elements)
   constexpr int KT_LD = kBwdBK + 8;  // K^T row stride (elements); K^T shares lds_k
   constexpr int LDSK = D * KT_LD > kBwdBK * LDR ? D * KT_LD : kBwdBK * LDR;
-  __shared__ __attribute__((aligned(16))) T lds_q[kBwdBQ * LDR];
-  __shared__ __attribute__((aligned(16))) T lds_do[kBwdBQ * LDR];
+  __shared__ __attribute__((aligned(16))) T lds_q[kBwdBQ * LDQ];
+  __shared__ __attribute__((aligned(16))) T lds_do[kBwdBQ * LDQ];
   __shared__ __attribute__((aligned(16))) T lds_k[LDSK];
   __shared__ __attribute__((aligned(16))) T lds_ds[kBwdBQ * LDS_S];
   __shared__ float lds_lse[kBwdBQ], lds_delta[kBwdBQ];
@@ -600,8 +614,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
         lds_delta[row] = part;
         if (!DQ && blockIdx.x == 0 && qb + row < nq) delta_out[(int64_t)bh * a.Sq + qb + row] = part;
       }
-      *(uint4*)(lds_q + row * LDR + col) = pf_q[c];
-      *(uint4*)(lds_do + row * LDR + col) = pf_do[c];
+      *(uint4*)(lds_q + row * LDQ + col) = pf_q[c];
+      *(uint4*)(lds_do + row * LDQ + col) = pf_do[c];
     }
     if (threadIdx.x < kBwdBQ) lds_lse[threadIdx.x] = P.lse * kLog2e;  // +inf stays +inf
     if (DROPOUT && threadIdx.x < 4 * kBwdBQ) lds_mask[threadIdx.x] = P.mask;
@@ -612,8 +626,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
     f32x16 sacc = f32x16{}, dpacc = f32x16{};
 #pragma unroll
     for (int s = 0; s < D / 16; ++s) {
-      const V8 qa = *(const V8*)(lds_q + r * LDR + 16 * s + 8 * hl);
-      const V8 da = *(const V8*)(lds_do + r * LDR + 16 * s + 8 * hl);
+      const V8 qa = *(const V8*)(lds_q + r * LDQ + 16 * s + 8 * hl);
+      const V8 da = *(const V8*)(lds_do + r * LDQ + 16 * s + 8 * hl);
       sacc = M::mma(qa, kf[s], sacc);
       dpacc = M::mma(da, vf[s], dpacc);
     }
@@ -662,8 +676,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
 #pragma unroll
       for (int db = 0; db < D / 32; ++db) {
         const int c0 = 32 * db + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-        const V8 dob = join4<V8>(lds_tr16(lds_do + kq * LDR + c0), lds_tr16(lds_do + (kq + 8) * LDR + c0));
-        const V8 qbf = join4<V8>(lds_tr16(lds_q + kq * LDR + c0), lds_tr16(lds_q + (kq + 8) * LDR + c0));
+        const V8 dob = join4<V8>(lds_tr16(lds_do + kq * LDQ + c0), lds_tr16(lds_do + (kq + 8) * LDQ + c0));
+        const V8 qbf = join4<V8>(lds_tr16(lds_q + kq * LDQ + c0), lds_tr16(lds_q + (kq + 8) * LDQ + c0));
         dv[db] = M::mma(pa, dob, dv[db]);
         dk[db] = M::mma(sa, qbf, dk[db]);
       }
@@ -788,8 +802,9 @@ template <typename T, int D, bool CAUSAL, bool DROPOUT, bool DSUM, bool BIAS>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2 : 1, D <= 64 ? 2 : 1))) attn_bwd_dq_kernel(AttnArgs a, const void* dout, const float* delta_in) {
   using M = MfmaT<T>;
   using V8 = typename M::V8;
-  constexpr int LDR = D + 8;
-  __shared__ __attribute__((aligned(16))) T lds_k[kFwdKB * LDR];
+  constexpr int LDR = ld_rows<D>();  // V: row reads
+  constexpr int LDK = ld_both<D>();  // K: row and transposed reads
+  __shared__ __attribute__((aligned(16))) T lds_k[kFwdKB * LDK];
   __shared__ __attribute__((aligned(16))) T lds_v[kFwdKB * LDR];
 
   // wid through readfirstlane: wave-uniform in SGPRs, so tile-level conditions become scalar branches
@@ -877,7 +892,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
     for (int c = 0; c < CH; ++c) {
       const int idx = threadIdx.x + 256 * c;
       const int row = idx / CPR, col = (idx % CPR) * 8;
-      *(uint4*)(lds_k + row * LDR + col) = kreg[c];
+      *(uint4*)(lds_k + row * LDK + col) = kreg[c];
       *(uint4*)(lds_v + row * LDR + col) = vreg[c];
     }
   };
@@ -899,7 +914,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
       V8 kf[D / 16], vf[D / 16];
 #pragma unroll
       for (int s = 0; s < D / 16; ++s) {
-        kf[s] = *(const V8*)(lds_k + (32 * sb + r) * LDR + 16 * s + 8 * hl);
+        kf[s] = *(const V8*)(lds_k + (32 * sb + r) * LDK + 16 * s + 8 * hl);
         vf[s] = *(const V8*)(lds_v + (32 * sb + r) * LDR + 16 * s + 8 * hl);
       }
       __builtin_amdgcn_sched_group_barrier(0x100, 2 * (D / 16), 0);
@@ -954,8 +969,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
 #pragma unroll
         for (int db = 0; db < D / 32; ++db) {
           const int c0 = 32 * db + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-          const s16x4 lo = lds_tr16(lds_k + k0 * LDR + c0);
-          const s16x4 hi = lds_tr16(lds_k + (k0 + 8) * LDR + c0);
+          const s16x4 lo = lds_tr16(lds_k + k0 * LDK + c0);
+          const s16x4 hi = lds_tr16(lds_k + (k0 + 8) * LDK + c0);
           dq[db] = M::mma(join4<V8>(lo, hi), sf, dq[db]);
         }
       }
