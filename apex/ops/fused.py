@@ -60,7 +60,9 @@ def _wgrad_splits(M, N, K):
     Slicing M into S batched GEMMs fills the chip (S*tiles ~ 128-256 workgroups); the fp32
     slabs are combined by one HIP reduction that writes the grad dtype. Measured on MI355X
     (tools/gemm_bench.py, BERT-Large shapes, M = 32768): 1024x1024 199 -> 79 us (S=8),
-    3072x1024 288 -> 199 us (S=4), 4096x1024 316 -> 262 us (S=4).
+    3072x1024 288 -> 199 us (S=4), 4096x1024 316 -> 262 us (S=4). At M = 98304
+    (profiles/r2_wgrad_split_sweep.jsonl, every S dividing M): 1024x1024 best at S=16 (194 us vs
+    215 at 8, 499 unsplit), 3072x1024 and the FFN shapes at S=4 — i.e. S*tiles ~ 256 workgroups.
     """
     if _WGRAD_SPLITK == "0":
         return 1
@@ -71,7 +73,7 @@ def _wgrad_splits(M, N, K):
         return 1
     tiles = ((N + 255) // 256) * ((K + 255) // 256)
     s = 1
-    while s < 8 and 2 * s * tiles <= 256 and M % (2 * s) == 0 and M // (2 * s) >= 1024:
+    while s < 16 and 2 * s * tiles <= 256 and M % (2 * s) == 0 and M // (2 * s) >= 1024:
         s *= 2
     return s
 

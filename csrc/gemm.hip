@@ -387,52 +387,68 @@ __device__ __forceinline__ void mainloop_bk64(const T* __restrict__ A, const T* 
   }
 }
 
+// Buffer resource for a wave-uniform base address (the epilogue's full-tile path): every lane
+// addresses rows through ONE 32-bit voffset plus an SGPR soffset per row slot, instead of a 64-bit
+// VGPR address pair per access (32 pairs per lane for a load+store epilogue, which the scheduler
+// hoisted and spilled). Inputs go through readfirstlane so no waterfall loop is emitted
+// (cdna_hip_programming.md T8 / T20).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const void* p, uint32_t bytes) {
+  const uint64_t a = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0,
+                                           (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
 // Epilogue shared by both kernels (wave tile 128 x 64 at rows m0 + wr*128, cols n0 + wc*64).
-template <typename T, int EPI, int TBM, int TBN>
+template <typename T, int EPI, bool EDGE>
 __device__ __forceinline__ void epilogue(const f32x4 (&acc)[4][8], char* reg, T* __restrict__ C, int M, int N,
                                          int64_t ldc, const T* __restrict__ bias, const T* __restrict__ aux,
                                          int64_t ldaux, T* __restrict__ aux_out, float* __restrict__ part, int m0,
                                          int n0, int tm, int wr, int wc, int lane, float alpha = 1.f) {
   const int lr = lane & 15, lk = lane >> 4;
-  // ---- epilogue ----
   // acc[j][i] holds rows wr*128 + i*16 + lr, cols wc*64 + j*16 + 4*lk .. +3 of the tile. The fp32
   // accumulators are rounded to T and transposed through the wave's own 16 KB LDS region
   // ([128 rows][64 cols], 16-B chunks XOR-swizzled by row, 8-B halves swapped on rows 8..15 of every
   // 16 so the ds_write_b64 groups are conflict-free); then every lane owns 8 consecutive columns of
-  // 16 rows, and the epilogue math (bias, GELU, dGELU, residual) runs on 16-byte vectors with
-  // 16-byte loads/stores (8 lanes = one 128-B row run). Rounding before the bias matches the unfused
-  // composition (GEMM output in T, then the bias/activation kernel in fp32).
-  // All LDS reads are issued before the first global access (hipcc drains vmcnt before an LDS access
-  // while VMEM ops are pending), and the interior tiles take a branch-free path (a per-element
-  // guarded load makes hipcc wait vmcnt(0) per element).
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int row = i * 16 + lr;
-      const int chunk = (2 * j + (lk >> 1)) ^ (row & 7);
-      const int half = (lk & 1) ^ ((row >> 3) & 1);
-      Pack<T, 4> pk;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) pk.v[e] = from_f<T>(acc[j][i][e] * alpha);
-      *reinterpret_cast<Pack<T, 4>*>(reg + row * 128 + chunk * 16 + half * 8) = pk;
-    }
+  // 16 rows ("row slots" it = 0..15, rows lane/8 + 8 it of the wave tile), and the epilogue math
+  // (bias, GELU, dGELU, residual) runs on 16-byte vectors with 16-byte loads/stores (8 lanes = one
+  // 128-B row run). Rounding before the bias matches the unfused composition (GEMM output in T,
+  // then the bias/activation kernel in fp32).
+  //
+  // Register budget (the kernel runs at 256 VGPRs): the slots are processed in two halves of 8, and
+  // the [M, N] input operand of EPI_RESID / EPI_MUL / EPI_DGELU is loaded a half AHEAD — the first
+  // half's 8 x 16 B per lane are issued before the accumulators go through LDS (the HBM latency
+  // hides behind the transposition), the second half's while the first half computes and stores.
+  // Global accesses go through buffer resources based at the wave tile's origin: full tiles use one
+  // per-lane voffset plus an SGPR soffset per slot; edge tiles a per-slot voffset that points past
+  // the resource for rows >= M or columns >= N (loads return 0, stores are dropped). With 64-bit
+  // flat addresses per access and all 16 slots at once, these epilogues spilled 120-340 B per lane
+  // to scratch (137 scratch instructions in EPI_MUL).
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-  u32x4 rc[16];
-#pragma unroll
-  for (int it = 0; it < 16; ++it) {
-    const int row = it * 8 + (lane >> 3), c = lane & 7;
-    u32x4 x = *reinterpret_cast<const u32x4*>(reg + row * 128 + ((c ^ (row & 7)) << 4));
-    if ((row >> 3) & 1) x = u32x4{x[2], x[3], x[0], x[1]};
-    rc[it] = x;
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
+  constexpr bool GELU_D = EPI == EPI_BIAS_GELU_D || EPI == EPI_BIAS_GELU_TANH_D;
+  constexpr bool GELU_FWD = EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_TANH || GELU_D;
+  constexpr bool DGELU = EPI == EPI_DGELU || EPI == EPI_DGELU_TANH;
+  constexpr bool MUL = EPI == EPI_MUL;
+  constexpr bool COLSUM = DGELU || MUL;
+  constexpr bool TANH = EPI == EPI_BIAS_GELU_TANH || EPI == EPI_DGELU_TANH || EPI == EPI_BIAS_GELU_TANH_D;
+  constexpr bool AUX_IN = DGELU || MUL || EPI == EPI_RESID;
 
   const int ncol = n0 + wc * 64 + (lane & 7) * 8;
-  const int mrow = m0 + wr * 128 + (lane >> 3);
-  const bool full = m0 + TBM <= M && n0 + TBN <= N;
+  const int wrow0 = m0 + wr * 128, wcol0 = n0 + wc * 64;
+  const int lrow = lane >> 3, lcol = (lane & 7) * 8;
+  auto wave_res = [&](const T* base, int64_t ld) {
+    return wave_rsrc(base + (int64_t)wrow0 * ld + wcol0, (uint32_t)(128 * ld * (int64_t)sizeof(T)));
+  };
+  // bounds-aware per-slot offset (any tile)
+  auto voff_g = [&](int64_t ld, int slot) -> uint32_t {
+    const int r = lrow + slot * 8;
+    return (wrow0 + r < M && ncol < N) ? (uint32_t)((r * ld + lcol) * (int64_t)sizeof(T)) : 0x80000000u;
+  };
+  const __amdgpu_buffer_rsrc_t rs_c = wave_res(C, ldc);
+  __amdgpu_buffer_rsrc_t rs_o = rs_c, rs_x = rs_c;
+  if constexpr (GELU_FWD) rs_o = wave_res(aux_out, ldc);
+  if constexpr (AUX_IN) rs_x = wave_res(aux, ldaux);
   auto unpack = [&](const u32x4& x, float (&v)[8]) {
     Pack<T, 8> pk = *reinterpret_cast<const Pack<T, 8>*>(&x);
 #pragma unroll
@@ -444,117 +460,136 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[4][8], char* reg, T*
     for (int e = 0; e < 8; ++e) pk.v[e] = from_f<T>(v[e]);
     return *reinterpret_cast<const u32x4*>(&pk);
   };
-  // guarded 16-byte access for edge tiles (N % 8 == 4 leaves a 4-column tail)
-  auto ld16 = [&](const T* base, int64_t ld, int m) -> u32x4 {
-    // branch-free: clamp the address into the tensor, then shift/mask the 4-column tail
-    const int mc = m < M ? m : M - 1;
-    const int nc = ncol + 8 <= N ? ncol : (N >= 8 ? N - 8 : 0);
-    u32x4 r = *reinterpret_cast<const u32x4*>(base + (int64_t)mc * ld + nc);
-    if (nc != ncol) r = u32x4{r[2], r[3], 0u, 0u};
-    return r;
-  };
-  auto st16 = [&](T* base, int m, const u32x4& x) {
-    if (m < M && ncol < N) {
-      T* p = base + (int64_t)m * ldc + ncol;
-      if (ncol + 8 <= N) *reinterpret_cast<u32x4*>(p) = x;
-      else *reinterpret_cast<u32x2*>(p) = u32x2{x[0], x[1]};
-    }
-  };
 
-  auto body = [&](auto full_tag) {
-    constexpr bool F = decltype(full_tag)::value;
-    float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    constexpr bool GELU_D = EPI == EPI_BIAS_GELU_D || EPI == EPI_BIAS_GELU_TANH_D;
-    constexpr bool GELU_FWD = EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_TANH || GELU_D;
-    constexpr bool DGELU = EPI == EPI_DGELU || EPI == EPI_DGELU_TANH;
-    constexpr bool MUL = EPI == EPI_MUL;
-    constexpr bool COLSUM = DGELU || MUL;
-    constexpr bool TANH = EPI == EPI_BIAS_GELU_TANH || EPI == EPI_DGELU_TANH || EPI == EPI_BIAS_GELU_TANH_D;
-    if constexpr (EPI == EPI_BIAS || GELU_FWD) {
-      u32x4 braw;
-      if constexpr (F) braw = *reinterpret_cast<const u32x4*>(bias + ncol);
-      else braw = ld16(bias, 0, 0);  // (bias is [N]: row 0 of a 1-row tensor)
-      unpack(braw, bv);
-    }
-    u32x4 ra[16];
-    if constexpr (DGELU || MUL || EPI == EPI_RESID) {
+  // F (EDGE = false: the launch has only full tiles, M % 256 == 0 and N % 256 == 0) or the
+  // bounds-checked form for every tile. One variant per kernel, no runtime branch: with both
+  // variants in one kernel the compiler hoisted their common code (conversions, LDS reads,
+  // unpacks) above the branch and spilled.
+  {
+    constexpr bool F = !EDGE;
+    auto voff = [&](int64_t ld, int slot) -> uint32_t {
+      if constexpr (F) return (uint32_t)((lrow * ld + lcol) * (int64_t)sizeof(T));
+      return voff_g(ld, slot);
+    };
+    auto soff = [&](int64_t ld, int slot) -> int { return F ? (int)(slot * 8 * ld * (int64_t)sizeof(T)) : 0; };
+    // stores take the slot offset in voffset with soffset = 0: with a register soffset hipcc
+    // (ROCm 7.2) does not count the gfx950 store-data hazard — a VALU overwrote the data VGPRs of
+    // a buffer_store_dwordx4 right after issue and corrupted a dword of the stored row (seen on
+    // the GPU: sporadic dwords of EPI_BIAS_GELU's pre-activation output)
+    auto st = [&](const __amdgpu_buffer_rsrc_t& rs, int slot, const u32x4& x) {
+      __builtin_amdgcn_raw_buffer_store_b128(x, rs, voff(ldc, slot) + (uint32_t)soff(ldc, slot), 0, 0);
+    };
+    // first half of the input operand in flight (sched_barriers pin the phase order: left alone,
+    // the scheduler hoists both halves' loads above the transposition and spills around them)
+    u32x4 ra[8];
+    if constexpr (AUX_IN) {
 #pragma unroll
-      for (int it = 0; it < 16; ++it) {
-        const int m = mrow + it * 8;
-        if constexpr (F) ra[it] = *reinterpret_cast<const u32x4*>(aux + (int64_t)m * ldaux + ncol);
-        else ra[it] = ld16(aux, ldaux, m);
+      for (int it = 0; it < 8; ++it) ra[it] = __builtin_amdgcn_raw_buffer_load_b128(rs_x, voff(ldaux, it), soff(ldaux, it), 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int row = i * 16 + lr;
+        const int chunk = (2 * j + (lk >> 1)) ^ (row & 7);
+        const int half = (lk & 1) ^ ((row >> 3) & 1);
+        Pack<T, 4> pk;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pk.v[e] = from_f<T>(acc[j][i][e] * alpha);
+        *reinterpret_cast<Pack<T, 4>*>(reg + row * 128 + chunk * 16 + half * 8) = pk;
       }
+    __builtin_amdgcn_sched_barrier(0);
+    float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if constexpr (EPI == EPI_BIAS || GELU_FWD) {
+      const int nc = ncol < N ? ncol : N - 8;  // (N % 8 == 0: edge lanes read a valid chunk, unused)
+      unpack(*reinterpret_cast<const u32x4*>(bias + nc), bv);
     }
     float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    u32x4 rb[8];
 #pragma unroll
-    for (int it = 0; it < 16; ++it) {
-      const int m = mrow + it * 8;
-      u32x4 out = rc[it];
-      if constexpr (EPI != EPI_NONE) {
-        float v[8];
-        unpack(rc[it], v);
-        if constexpr (EPI == EPI_BIAS) {
+    for (int h = 0; h < 2; ++h) {
+      u32x4 rc[8];
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += bv[e];
-        } else if constexpr (GELU_FWD) {
+      for (int it = 0; it < 8; ++it) {
+        const int row = (8 * h + it) * 8 + lrow, c = lane & 7;
+        u32x4 x = *reinterpret_cast<const u32x4*>(reg + row * 128 + ((c ^ (row & 7)) << 4));
+        if ((row >> 3) & 1) x = u32x4{x[2], x[3], x[0], x[1]};
+        rc[it] = x;
+      }
+      if constexpr (AUX_IN) {
+        if (h == 0) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += bv[e];
-          const u32x4 hraw = pack(v);
-          if constexpr (!GELU_D) {
-            if constexpr (F) *reinterpret_cast<u32x4*>(aux_out + (int64_t)m * ldc + ncol) = hraw;
-            else st16(aux_out, m, hraw);
-          }
-          unpack(hraw, v);  // GELU of the (rounded) pre-activation, as the unfused composition
-          float gd[8];
-#pragma unroll
-          for (int e = 0; e < 8; e += 2) {
-            if constexpr (GELU_D) {
-              f32x2 gv, gg;
-              gelu_and_grad2(f32x2{v[e], v[e + 1]}, TANH, gv, gg);
-              v[e] = gv[0];
-              v[e + 1] = gv[1];
-              gd[e] = gg[0];
-              gd[e + 1] = gg[1];
-            } else {
-              const f32x2 gv = TANH ? gelu_tanh2(f32x2{v[e], v[e + 1]}) : gelu2(f32x2{v[e], v[e + 1]});
-              v[e] = gv[0];
-              v[e + 1] = gv[1];
-            }
-          }
-          if constexpr (GELU_D) {
-            const u32x4 graw = pack(gd);
-            if constexpr (F) *reinterpret_cast<u32x4*>(aux_out + (int64_t)m * ldc + ncol) = graw;
-            else st16(aux_out, m, graw);
-          }
-        } else {
-          float x[8];
-          unpack(ra[it], x);
-          const bool ok = F || (m < M && ncol < N);
-#pragma unroll
-          for (int e = 0; e < 8; e += 2) {
-            if constexpr (DGELU) {
-              const f32x2 gg = TANH ? gelu_tanh_grad2(f32x2{x[e], x[e + 1]}) : gelu_grad2(f32x2{x[e], x[e + 1]});
-              v[e] = ok ? v[e] * gg[0] : 0.f;
-              v[e + 1] = ok ? v[e + 1] * gg[1] : 0.f;
-            } else if constexpr (MUL) {
-              v[e] = ok ? v[e] * x[e] : 0.f;
-              v[e + 1] = ok ? v[e + 1] * x[e + 1] : 0.f;
-            } else {
-              v[e] += x[e];
-              v[e + 1] += x[e + 1];
-            }
-          }
-        }
-        out = pack(v);
-        if constexpr (COLSUM) {
-          float r[8];
-          unpack(out, r);  // the bias grad sums the stored (rounded) values
-#pragma unroll
-          for (int e = 0; e < 8; ++e) csum[e] += r[e];
+          for (int it = 0; it < 8; ++it)
+            rb[it] = __builtin_amdgcn_raw_buffer_load_b128(rs_x, voff(ldaux, 8 + it), soff(ldaux, 8 + it), 0);
         }
       }
-      if constexpr (F) *reinterpret_cast<u32x4*>(C + (int64_t)m * ldc + ncol) = out;
-      else st16(C, m, out);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const int slot = 8 * h + it;
+        u32x4 out = rc[it];
+        if constexpr (EPI != EPI_NONE) {
+          float v[8];
+          unpack(rc[it], v);
+          if constexpr (EPI == EPI_BIAS) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += bv[e];
+          } else if constexpr (GELU_FWD) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += bv[e];
+            const u32x4 hraw = pack(v);
+            if constexpr (!GELU_D) st(rs_o, slot, hraw);
+            unpack(hraw, v);  // GELU of the (rounded) pre-activation, as the unfused composition
+            float gd[8];
+#pragma unroll
+            for (int e = 0; e < 8; e += 2) {
+              if constexpr (GELU_D) {
+                f32x2 gv, gg;
+                gelu_and_grad2(f32x2{v[e], v[e + 1]}, TANH, gv, gg);
+                v[e] = gv[0];
+                v[e + 1] = gv[1];
+                gd[e] = gg[0];
+                gd[e + 1] = gg[1];
+              } else {
+                const f32x2 gv = TANH ? gelu_tanh2(f32x2{v[e], v[e + 1]}) : gelu2(f32x2{v[e], v[e + 1]});
+                v[e] = gv[0];
+                v[e + 1] = gv[1];
+              }
+            }
+            if constexpr (GELU_D) st(rs_o, slot, pack(gd));
+          } else {
+            float x[8];
+            unpack(h == 0 ? ra[it] : rb[it], x);
+            const bool ok = F || (wrow0 + lrow + 8 * slot < M && ncol < N);
+#pragma unroll
+            for (int e = 0; e < 8; e += 2) {
+              if constexpr (DGELU) {
+                const f32x2 gg = TANH ? gelu_tanh_grad2(f32x2{x[e], x[e + 1]}) : gelu_grad2(f32x2{x[e], x[e + 1]});
+                v[e] = ok ? v[e] * gg[0] : 0.f;
+                v[e + 1] = ok ? v[e + 1] * gg[1] : 0.f;
+              } else if constexpr (MUL) {
+                v[e] = ok ? v[e] * x[e] : 0.f;
+                v[e + 1] = ok ? v[e + 1] * x[e + 1] : 0.f;
+              } else {
+                v[e] += x[e];
+                v[e + 1] += x[e + 1];
+              }
+            }
+          }
+          out = pack(v);
+          if constexpr (COLSUM) {
+            float r[8];
+            unpack(out, r);  // the bias grad sums the stored (rounded) values
+#pragma unroll
+            for (int e = 0; e < 8; ++e) csum[e] += r[e];
+          }
+        }
+        st(rs_c, slot, out);
+        // one slot at a time: unpacking every slot's operands up front (16 bf16 -> 16 fp32 per
+        // slot, hoisted by the scheduler) is what pushed these epilogues past 256 VGPRs
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
     if constexpr (COLSUM) {
       // lanes l, l^8, l^16, ... share the column chunk: reduce over the wave's 8 row slots
@@ -570,12 +605,10 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[4][8], char* reg, T*
       if (lane < 8 && ncol < N) {
         float* pp = part + (int64_t)(tm * 2 + wr) * N + ncol;
         *reinterpret_cast<f32x4*>(pp) = f32x4{csum[0], csum[1], csum[2], csum[3]};
-        if (ncol + 8 <= N) *reinterpret_cast<f32x4*>(pp + 4) = f32x4{csum[4], csum[5], csum[6], csum[7]};
+        *reinterpret_cast<f32x4*>(pp + 4) = f32x4{csum[4], csum[5], csum[6], csum[7]};
       }
     }
-  };
-  if (full) body(std::integral_constant<bool, true>{});
-  else body(std::integral_constant<bool, false>{});
+  }
 }
 
 // diagnostics only (tools/gemm_epi_cost.py): 2 = skip the epilogue (main-loop-only timing)
@@ -590,7 +623,7 @@ __device__ int g_gemm_stagger = 0;
 
 // T: output / epilogue dtype; TI: operand dtype (T, or uint8_t fp8 with formats FA (A) / FB (B) and
 // the dequantisation alpha = alpha_a[0] * alpha_b[0] read on the device)
-template <typename T, int EPI, bool TR, typename TI = T, int FA = -1, int FB = -1>
+template <typename T, int EPI, bool TR, bool EDGE, typename TI = T, int FA = -1, int FB = -1>
 __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(const TI* __restrict__ A, const TI* __restrict__ B,
                                                             T* __restrict__ C, int M, int N, int K, int64_t lda,
                                                             int64_t ldb, int64_t ldc, const T* __restrict__ bias,
@@ -662,7 +695,7 @@ __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(const TI* __restrict
   }
   float alpha = 1.f;
   if constexpr (FA >= 0) alpha = alpha_a[0] * alpha_b[0];
-  epilogue<T, EPI, GB_M, GB_N>(acc, smem + wid * 16384, C, M, N, ldc, bias, aux, ldaux, aux_out, part, m0, n0, tm, wr,
+  epilogue<T, EPI, EDGE>(acc, smem + wid * 16384, C, M, N, ldc, bias, aux, ldaux, aux_out, part, m0, n0, tm, wr,
                                 wc, lane, alpha);
 }
 
@@ -718,17 +751,28 @@ template <typename T, int EPI, bool TR = false>
 void launch_gemm(const GemmArgs& g, hipStream_t s) {
   const int tiles = ((g.M + GB_M - 1) / GB_M) * ((g.N + GB_N - 1) / GB_N);
   const int stagger = host_stagger(EPI);  // see g_gemm_stagger
-  hipLaunchKernelGGL((gemm_nt_kernel<T, EPI, TR>), dim3(tiles, TR ? g.splits : 1), dim3(G_THREADS), 0, s, (const T*)g.A, (const T*)g.B,
-                     (T*)g.C, g.M, g.N, g.K, g.lda, g.ldb, g.ldc, (const T*)g.bias, (const T*)g.aux, g.ldaux,
-                     (T*)g.aux_out, g.part, stagger);
+  const bool edge = !TR && (g.M % GB_M != 0 || g.N % GB_N != 0);  // (gemm_tt shapes are tile multiples)
+  if (!TR && edge)
+    hipLaunchKernelGGL((gemm_nt_kernel<T, EPI, TR, !TR>), dim3(tiles, TR ? g.splits : 1), dim3(G_THREADS), 0, s,
+                       (const T*)g.A, (const T*)g.B, (T*)g.C, g.M, g.N, g.K, g.lda, g.ldb, g.ldc, (const T*)g.bias,
+                       (const T*)g.aux, g.ldaux, (T*)g.aux_out, g.part, stagger);
+  else
+    hipLaunchKernelGGL((gemm_nt_kernel<T, EPI, TR, false>), dim3(tiles, TR ? g.splits : 1), dim3(G_THREADS), 0, s,
+                       (const T*)g.A, (const T*)g.B, (T*)g.C, g.M, g.N, g.K, g.lda, g.ldb, g.ldc, (const T*)g.bias,
+                       (const T*)g.aux, g.ldaux, (T*)g.aux_out, g.part, stagger);
 }
 
 template <typename T, int EPI, int FA, int FB>
 void launch_gemm_f8(const GemmArgs& g, hipStream_t s) {
   const int tiles = ((g.M + GB_M - 1) / GB_M) * ((g.N + GB_N - 1) / GB_N);
-  hipLaunchKernelGGL((gemm_nt_kernel<T, EPI, false, uint8_t, FA, FB>), dim3(tiles), dim3(G_THREADS), 0, s,
-                     (const uint8_t*)g.A, (const uint8_t*)g.B, (T*)g.C, g.M, g.N, g.K, g.lda, g.ldb, g.ldc,
-                     (const T*)g.bias, (const T*)g.aux, g.ldaux, (T*)g.aux_out, g.part, 0, g.alpha_a, g.alpha_b);
+  if (g.M % GB_M != 0 || g.N % GB_N != 0)
+    hipLaunchKernelGGL((gemm_nt_kernel<T, EPI, false, true, uint8_t, FA, FB>), dim3(tiles), dim3(G_THREADS), 0, s,
+                       (const uint8_t*)g.A, (const uint8_t*)g.B, (T*)g.C, g.M, g.N, g.K, g.lda, g.ldb, g.ldc,
+                       (const T*)g.bias, (const T*)g.aux, g.ldaux, (T*)g.aux_out, g.part, 0, g.alpha_a, g.alpha_b);
+  else
+    hipLaunchKernelGGL((gemm_nt_kernel<T, EPI, false, false, uint8_t, FA, FB>), dim3(tiles), dim3(G_THREADS), 0, s,
+                       (const uint8_t*)g.A, (const uint8_t*)g.B, (T*)g.C, g.M, g.N, g.K, g.lda, g.ldb, g.ldc,
+                       (const T*)g.bias, (const T*)g.aux, g.ldaux, (T*)g.aux_out, g.part, 0, g.alpha_a, g.alpha_b);
 }
 
 template <typename T, int FA, int FB>
@@ -770,7 +814,9 @@ int gemm_dispatch(const GemmArgs& g, hipStream_t s) {
 }  // namespace
 
 bool gemm_supported(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc) {
+  // ldc < 2^22: the epilogue addresses a 128-row wave tile through 32-bit buffer offsets
   return M > 0 && N > 0 && K > 0 && K % GB_K == 0 && N % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 && ldc % 8 == 0 &&
+         ldc < (1 << 22) &&
          (int64_t)M * lda < (1ll << 40);
 }
 
@@ -787,6 +833,7 @@ int gemm_set_dbg(int v) {
 
 int gemm_nt(const GemmArgs& g, int dt, hipStream_t s) {
   if (!gemm_supported(g.M, g.N, g.K, g.lda, g.ldb, g.ldc)) return -2;
+  if (g.aux && g.ldaux >= (1 << 22)) return -2;  // 32-bit buffer offsets in the epilogue
   if (dt == kBF16Code) return gemm_dispatch<bf16>(g, s);
   if (dt == kF16Code) return gemm_dispatch<f16>(g, s);
   return -1;
@@ -794,12 +841,14 @@ int gemm_nt(const GemmArgs& g, int dt, hipStream_t s) {
 
 bool gemm_f8_supported(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc) {
   return M > 0 && N > 0 && K > 0 && K % 128 == 0 && N % 8 == 0 && lda % 16 == 0 && ldb % 16 == 0 && ldc % 8 == 0 &&
+         ldc < (1 << 22) &&
          (int64_t)M * lda < (1ll << 40);
 }
 
 int gemm_nt_f8(const GemmArgs& g, int fmt_a, int fmt_b, int out_dt, hipStream_t s) {
   // A (activations / gradients): e4m3 (0) or e5m2 (1); B (weights): e4m3
   if (!gemm_f8_supported(g.M, g.N, g.K, g.lda, g.ldb, g.ldc) || fmt_b != 0 || !g.alpha_a || !g.alpha_b) return -2;
+  if (g.aux && g.ldaux >= (1 << 22)) return -2;
   if (out_dt == kBF16Code) {
     if (fmt_a == 0) return gemm_dispatch_f8<bf16, 0, 0>(g, s);
     if (fmt_a == 1) return gemm_dispatch_f8<bf16, 1, 0>(g, s);
