@@ -175,7 +175,9 @@ attn_fwd_kernel(AttnArgs a) {
   using M = MfmaT<T>;
   using V8 = typename M::V8;
   constexpr int LDR = ld_rows<D>();  // K: row reads
-  constexpr int LDV = ld_tr<D>();    // V: transposed reads
+  // V: transposed reads (SHORT keeps D + 8: the wider stride would take its two-tile LDS image to
+  // 43 KB and the variant from 4 to 3 workgroups per CU)
+  constexpr int LDV = SHORT ? ld_rows<D>() : ld_tr<D>();
   constexpr int NBUF = SHORT ? 2 : 1;
   __shared__ __attribute__((aligned(16))) T lds_k[NBUF * kFwdKB * LDR];
   __shared__ __attribute__((aligned(16))) T lds_v[NBUF * kFwdKB * LDV];
@@ -1032,6 +1034,8 @@ int attn_fwd_impl(const AttnArgs& a, int dt, hipStream_t s) {
   // SHORT: single LDS stage (k_lens <= Sk). Without dropout only: measured at the BERT shape
   // (tools/attn_bench.py, b256 s128 h16) p = 0 fwd 61.1 -> 56.1 us, but p = 0.1 72.7 -> 73.8 us:
   // with dropout the kernel is bound by the Philox integer multiplies, not by load latency.
+  // Re-measured with the dropout variant at 128 VGPRs / 4 workgroups per CU (round 2): 75.3-76.5
+  // vs 74.0-75.7 us — the same; p = 0 at 56 us is within ~10 % of its HBM floor (276 MB moved).
   if constexpr (D == 64) {
     if (a.Sk <= 2 * kFwdKB && !drop && !a.bias) {
       ATTN_DISPATCH(dt, T, ATTN_DISPATCH_B(a.causal, C,

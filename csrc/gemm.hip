@@ -246,7 +246,10 @@ __device__ __forceinline__ s16x8 frag(const char* tile, int rb, int s, int lr, i
 // stages, no ping-pong; profiles/r1_gemm_*_2wg_variant.jsonl) — its epilogue does overlap the
 // other workgroup's MFMAs (K = 64: 55 vs 65 us at N = 4096) but the main loop is ~60 % slower;
 // two phases per K-tile with the whole tile read in the first R section (half the barriers, next
-// loads 4 sections ahead, 256 VGPRs; profiles/r1_gemm_ksweep_2phase.jsonl) — within 1 %.
+// loads 4 sections ahead, 256 VGPRs; profiles/r1_gemm_ksweep_2phase.jsonl) — within 1 %; the two
+// glds pieces of each phase issued from inside the MFMA section (after 8 of its 16 MFMAs) instead
+// of the R section, same buffers and waits (vmcnt(2) in R4) — 5-7 % slower on every BERT shape
+// at M = 98304 (profiles/r2_gemm_glds_in_mma_ab.jsonl, same box).
 // hipBLASLt's kernel on the same shape (rocprof): one wave per SIMD with 128x128 wave tiles (256
 // AGPR accumulators), 74 % MFMA busy vs 64 % here. That geometry in HIP source (fragments
 // software-pipelined under 64-MFMA halves) makes hipcc shuffle ~220 accumulator copies
