@@ -34,13 +34,20 @@ class _FusedNormFn(torch.autograd.Function):
         y, mean, rstd = C.ln_fwd(xc, cols, w, b, float(eps), bool(rms))
         ctx.save_for_backward(xc, w, b, mean, rstd)
         ctx.cols, ctx.rms = cols, rms
+        ctx.params = (weight, bias)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         C = _ext.require()
         x, w, b, mean, rstd = ctx.saved_tensors
-        dx, dw, db = C.ln_bwd(dy.contiguous(), x, ctx.cols, w, b, mean, rstd, bool(ctx.rms))
+        from ..ops.fused import _gt
+
+        pw, pb = ctx.params
+        # weight / bias gradients straight into their DDP bucket slots when there are any
+        dx, dw, db = C.ln_bwd(dy.contiguous(), x, ctx.cols, w, b, mean, rstd, bool(ctx.rms),
+                              _gt(pw) if w is not None and ctx.needs_input_grad[1] else None,
+                              _gt(pb) if b is not None and ctx.needs_input_grad[2] else None)
         return (dx, dw if w is not None and ctx.needs_input_grad[1] else None,
                 db if b is not None and ctx.needs_input_grad[2] else None, None, None, None)
 

@@ -150,7 +150,7 @@ class _FusedDense(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             dw = _wgrad(dy2, x2, out=_gt(ctx.params[0]))
         if ctx.has_b and ctx.needs_input_grad[2]:
-            db = _ext.require().colsum(dy2, ctx.bdtype)
+            db = _ext.require().colsum(dy2, ctx.bdtype, _gt(ctx.params[1]))
         return dx, dw, db
 
 
@@ -366,7 +366,8 @@ class _BiasDropoutAdd(torch.autograd.Function):
     def backward(ctx, dy):
         C = _ext.require()
         p, seed, off = ctx.cfg
-        dx, db = C.bias_dropout_add_bwd(_2d(dy), float(p), seed, off, ctx.b_like if ctx.has_b else None)
+        tb = _gt(ctx.b_like) if ctx.has_b and ctx.needs_input_grad[1] else None
+        dx, db = C.bias_dropout_add_bwd(_2d(dy), float(p), seed, off, ctx.b_like if ctx.has_b else None, tb)
         return dx.view_as(dy), (db if ctx.has_b else None), dy, None
 
 

@@ -235,15 +235,20 @@ std::vector<Tensor> ln_fwd(Tensor x, int64_t cols, const c10::optional<Tensor>& 
   return {y, mean, rstd};
 }
 
+Tensor out_or_empty(const c10::optional<Tensor>& out, at::IntArrayRef sizes, const at::TensorOptions& opt,
+                    const char* what);
+
+// dgamma_out / dbeta_out: optional destinations (a DDP gradient-bucket slot, apex.parallel.grad_target)
 std::vector<Tensor> ln_bwd(Tensor dy, Tensor x, int64_t cols, const c10::optional<Tensor>& gamma,
-                           const c10::optional<Tensor>& beta, Tensor mean, Tensor rstd, bool rms) {
+                           const c10::optional<Tensor>& beta, Tensor mean, Tensor rstd, bool rms,
+                           const c10::optional<Tensor>& dgamma_out, const c10::optional<Tensor>& dbeta_out) {
   TORCH_CHECK(dy.is_contiguous() && x.is_contiguous(), "layer_norm_bwd: contiguous inputs");
   const int64_t rows = cols ? x.numel() / cols : 0;
   Tensor dx = at::empty_like(x);
   const bool hg = gamma.has_value() && gamma->defined();
   const bool hb = beta.has_value() && beta->defined();
-  Tensor dgamma = hg ? at::empty_like(*gamma) : Tensor();
-  Tensor dbeta = hb ? at::empty_like(*beta) : Tensor();
+  Tensor dgamma = hg ? out_or_empty(dgamma_out, gamma->sizes(), gamma->options(), "layer_norm_bwd dgamma") : Tensor();
+  Tensor dbeta = hb ? out_or_empty(dbeta_out, beta->sizes(), beta->options(), "layer_norm_bwd dbeta") : Tensor();
   Tensor ws;
   if (hg || hb)
     ws = at::empty({apex::layer_norm_bwd_ws_floats(rows, (int)cols)}, x.options().dtype(at::kFloat));
@@ -484,12 +489,12 @@ Tensor k_bda_fwd(Tensor x, const c10::optional<Tensor>& b, Tensor res, double p,
 }
 
 std::vector<Tensor> k_bda_bwd(Tensor dy, double p, int64_t seed, int64_t offset,
-                              const c10::optional<Tensor>& bias_like) {
+                              const c10::optional<Tensor>& bias_like, const c10::optional<Tensor>& dbias_out) {
   Tensor dyc = dy.contiguous();
   const int64_t cols = cols_of(dyc), rows = dyc.numel() / std::max<int64_t>(cols, 1);
   Tensor dx = at::empty_like(dyc);
   const bool hb = bias_like.has_value() && bias_like->defined();
-  Tensor db = hb ? at::empty_like(*bias_like) : Tensor();
+  Tensor db = hb ? out_or_empty(dbias_out, bias_like->sizes(), bias_like->options(), "bias_dropout_add_bwd") : Tensor();
   Tensor ws = hb ? at::empty({apex::colsum_parts(rows) * cols}, dyc.options().dtype(at::kFloat)) : Tensor();
   auto dp = drop_params(p);
   check(apex::bias_dropout_add_bwd(dyc.data_ptr(), dx.data_ptr(), hb ? db.data_ptr() : nullptr,
@@ -501,10 +506,10 @@ std::vector<Tensor> k_bda_bwd(Tensor dy, double p, int64_t seed, int64_t offset,
   return {dx, db};
 }
 
-Tensor k_colsum(Tensor x, at::ScalarType out_dtype) {
+Tensor k_colsum(Tensor x, at::ScalarType out_dtype, const c10::optional<Tensor>& out_opt) {
   Tensor xc = x.contiguous();
   const int64_t cols = cols_of(xc), rows = xc.numel() / std::max<int64_t>(cols, 1);
-  Tensor out = at::empty({cols}, xc.options().dtype(out_dtype));
+  Tensor out = out_or_empty(out_opt, {cols}, xc.options().dtype(out_dtype), "colsum");
   Tensor ws = at::empty({apex::colsum_parts(rows) * cols}, xc.options().dtype(at::kFloat));
   check(apex::colsum(xc.data_ptr(), out.data_ptr(), ws.data_ptr<float>(), rows, (int)cols,
                      dt_code(xc.scalar_type()), dt_code(out_dtype), cur_stream()),
@@ -1195,7 +1200,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("larc", &MTPlan::larc);
   m.def("update_scale", &update_scale);
   m.def("ln_fwd", &ln_fwd);
-  m.def("ln_bwd", &ln_bwd);
+  m.def("ln_bwd", &ln_bwd, py::arg("dy"), py::arg("x"), py::arg("cols"), py::arg("gamma"), py::arg("beta"),
+        py::arg("mean"), py::arg("rstd"), py::arg("rms"), py::arg("dgamma_out") = py::none(),
+        py::arg("dbeta_out") = py::none());
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd", &xent_bwd);
   m.def("gemm_f8_supported", &k_gemm_f8_supported);
@@ -1236,8 +1243,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bias_act_fwd", &k_bias_act_fwd);
   m.def("bias_act_bwd", &k_bias_act_bwd);
   m.def("bias_dropout_add_fwd", &k_bda_fwd);
-  m.def("bias_dropout_add_bwd", &k_bda_bwd);
-  m.def("colsum", &k_colsum);
+  m.def("bias_dropout_add_bwd", &k_bda_bwd, py::arg("dy"), py::arg("p"), py::arg("seed"), py::arg("offset"),
+        py::arg("bias_like"), py::arg("dbias_out") = py::none());
+  m.def("colsum", &k_colsum, py::arg("x"), py::arg("out_dtype"), py::arg("out") = py::none());
   m.def("splitk_reduce", &k_splitk_reduce, py::arg("slabs"), py::arg("out_dtype"), py::arg("out") = py::none());
   m.def("bdaln_supported", &k_bdaln_supported);
   m.def("bdaln_fwd", &k_bdaln_fwd);

@@ -101,3 +101,39 @@ def test_fused_producers_write_into_bucket_slots(rccl_one_rank, delay):
     ref(**batches[3]).backward()
     for n, p, q in zip(names, net.parameters(), ref.parameters()):
         torch.testing.assert_close(p.grad.float(), q.grad.float(), rtol=2e-2, atol=4e-3, msg=n)
+
+
+@pytest.mark.gpu
+def test_gpt_layernorm_and_bias_grads_written_into_slots(rccl_one_rank):
+    """The GPT-2 block's FusedLayerNorm weight/bias, fused-dense bias and bias-dropout-add bias
+    gradients are written by their HIP backward kernels straight into the DDP bucket slots
+    (ln_bwd / colsum / bias_dropout_add_bwd outputs), and every gradient over two steps equals
+    the same model's without DDP (tied embedding / LM-head weight included)."""
+    from apex.models.gpt import GPTConfig, GPTModel, synthetic_batch
+    from apex.optimizers import FusedAdam
+    from apex.parallel import DistributedDataParallel as DDP
+
+    cfg = GPTConfig.tiny()
+    cfg.dropout = 0.0
+    torch.manual_seed(0)
+    net = GPTModel(cfg).cuda().bfloat16()
+    ref = GPTModel(cfg).cuda().bfloat16()
+    ref.load_state_dict(net.state_dict())
+    model = DDP(net, message_size=1 << 20)
+    opt = FusedAdam(net.parameters(), lr=0.0)
+    g = torch.Generator(device="cuda").manual_seed(2)
+    batches = [synthetic_batch(cfg, 4, 64, device="cuda", generator=g) for _ in range(2)]
+    names = [n for n, _ in net.named_parameters()]
+    for it, b in enumerate(batches):
+        opt.zero_grad()
+        model(**b).backward()
+        ref.zero_grad(set_to_none=True)
+        ref(**b).backward()
+        for n, p, q in zip(names, net.parameters(), ref.parameters()):
+            assert p.grad is not None, n
+            if it > 0:
+                flat = p._apex_bucket_flat
+                lo, hi = flat.data_ptr(), flat.data_ptr() + flat.numel() * flat.element_size()
+                assert lo <= p.grad.data_ptr() < hi, n
+            torch.testing.assert_close(p.grad.float(), q.grad.float(), rtol=2e-2, atol=3e-3, msg=n)
+        opt.step()
