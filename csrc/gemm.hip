@@ -428,6 +428,10 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[4][8], char* reg, T*
   // the resource for rows >= M or columns >= N (loads return 0, stores are dropped). With 64-bit
   // flat addresses per access and all 16 slots at once, these epilogues spilled 120-340 B per lane
   // to scratch (137 scratch instructions in EPI_MUL).
+  // Measured alternative (profiles/r2_gemm_regroup_epilogue_ab.jsonl): the accumulators regrouped
+  // in registers by v_permlane16_swap instead of the LDS transposition (no LDS, no barrier, every
+  // lane 8 consecutive columns) — correct, but 2-10 % SLOWER (FFN2 dgrad x gelu' 796 -> 869 us):
+  // each 16-byte-per-lane access then covers 16 rows x 64 B instead of 8 rows x 128 B.
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   constexpr bool GELU_D = EPI == EPI_BIAS_GELU_D || EPI == EPI_BIAS_GELU_TANH_D;
   constexpr bool GELU_FWD = EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_TANH || GELU_D;
