@@ -27,6 +27,7 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace apex {
@@ -168,17 +169,23 @@ constexpr int kFwdKB = 64;              // keys per tile
 // and no register copy of K/V is live during the math, which brings the kernel to 128 VGPRs:
 // 4 workgroups (16 waves, 144 KB of LDS) per CU instead of 2 for a kernel that is one
 // load -> math -> store pass per workgroup, so the other workgroups' loads hide the HBM latency.
-template <typename T, int D, bool CAUSAL, bool DROPOUT, bool SHORT, bool BIAS>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SHORT ? 4 : (D > 128 ? 1 : 2))))
+// DB (long key ranges): K/V tiles double-buffered in LDS with ONE barrier per tile — tile kt + 1
+// (in registers since the middle of tile kt - 1) is written to the other buffer in the middle of
+// tile kt's math, right after the S products, and tile kt + 2's global loads are issued then
+// (cdna_hip_programming.md T14 "async-STAGE split"); the single-buffer loop pays two barriers per
+// tile (previous tile consumed / this tile staged).
+template <typename T, int D, bool CAUSAL, bool DROPOUT, bool SHORT, bool BIAS, bool DB = false>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SHORT ? 4 : (D > 128 ? 1 : (DB && D <= 64 && !DROPOUT ? 3 : 2)))))
 attn_fwd_kernel(AttnArgs a) {
   static_assert(!SHORT || D == 64, "SHORT is the D = 64 single-pass variant");
+  static_assert(!(SHORT && DB), "SHORT stages the whole key range once");
   using M = MfmaT<T>;
   using V8 = typename M::V8;
   constexpr int LDR = ld_rows<D>();  // K: row reads
   // V: transposed reads (SHORT keeps D + 8: the wider stride would take its two-tile LDS image to
   // 43 KB and the variant from 4 to 3 workgroups per CU)
   constexpr int LDV = SHORT ? ld_rows<D>() : ld_tr<D>();
-  constexpr int NBUF = SHORT ? 2 : 1;
+  constexpr int NBUF = SHORT || DB ? 2 : 1;
   __shared__ __attribute__((aligned(16))) T lds_k[NBUF * kFwdKB * LDR];
   __shared__ __attribute__((aligned(16))) T lds_v[NBUF * kFwdKB * LDV];
 
@@ -220,7 +227,7 @@ attn_fwd_kernel(AttnArgs a) {
   constexpr int CH = kFwdKB * CPR / 256;   // chunks per thread per tensor
   // K/V tiles of the tile TWO ahead are loaded into registers while the current tile computes
   // (two register sets, loop unrolled by two) at D <= 64; one ahead at D >= 128 (register budget)
-  constexpr bool KV2 = D <= 64;
+  constexpr bool KV2 = D <= 64 && !DB;
   constexpr int AHEAD = KV2 ? 2 : 1;
   struct KV {
     uint4 k[CH], v[CH];
@@ -263,9 +270,9 @@ attn_fwd_kernel(AttnArgs a) {
 
   if (ntiles > 0) gload(kva, 0);
   if (KV2 && ntiles > 1) gload(kvb, 1);
-  // math of key tile kt, read from LDS rows lr0 ..
-  auto compute = [&](const int kt) {
-    const int lr0 = SHORT ? kt * kFwdKB : 0;
+  // math of key tile kt, read from LDS rows lr0 ..; mid() runs right after the S products (DB)
+  auto compute = [&](const int kt, auto&& mid) {
+    const int lr0 = SHORT ? kt * kFwdKB : DB ? (kt & 1) * kFwdKB : 0;
     uint32_t mcur[2] = {0u, 0u};
     if (DROPOUT) {
 #pragma unroll
@@ -306,6 +313,7 @@ attn_fwd_kernel(AttnArgs a) {
           st[sb] = M::mma(*(const V8*)(lds_k + (lr0 + 32 * sb + r) * LDR + 16 * s + 8 * hl), qf[s], st[sb]);
       }
     }
+    mid();
     if constexpr (BIAS) {
       // element i of sub-block sb <-> key kb + 32 sb + (i & 3) + 8 (i >> 2) + 4 hl
 #pragma unroll
@@ -405,20 +413,35 @@ attn_fwd_kernel(AttnArgs a) {
       }
     }
   };
+  auto nomid = [] {};
   auto tile = [&](KV& R, const int kt) {
     lds_barrier();  // previous tile fully consumed
     lstore(R, 0);
     lds_barrier();
     if (kt + AHEAD < ntiles) gload(R, kt + AHEAD);
-    compute(kt);
+    compute(kt, nomid);
   };
   if constexpr (SHORT) {
     // both (<= 2) tiles were loaded above: one LDS stage, then the math with no K/V registers live
     if (ntiles > 0) lstore(kva, 0);
     if (ntiles > 1) lstore(kvb, kFwdKB);
     lds_barrier();
-    if (ntiles > 0) compute(0);
-    if (ntiles > 1) compute(1);
+    if (ntiles > 0) compute(0, nomid);
+    if (ntiles > 1) compute(1, nomid);
+  } else if constexpr (DB) {
+    // tile 0 staged, tile 1 in registers; then per tile: barrier, S products, stage tile kt + 1
+    // into the other buffer + issue tile kt + 2's loads, softmax, PV
+    if (ntiles > 0) lstore(kva, 0);
+    if (ntiles > 1) gload(kva, 1);
+    for (int kt = 0; kt < ntiles; ++kt) {
+      lds_barrier();  // tile kt's buffer complete; the other buffer's last readers (tile kt - 1) done
+      compute(kt, [&] {
+        if (kt + 1 < ntiles) {
+          lstore(kva, ((kt + 1) & 1) * kFwdKB);
+          if (kt + 2 < ntiles) gload(kva, kt + 2);
+        }
+      });
+    }
   } else if constexpr (KV2) {
     for (int kt = 0; kt < ntiles; kt += 2) {
       tile(kva, kt);
@@ -1027,6 +1050,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
   if (X) { constexpr bool NAME = true; __VA_ARGS__; }       \
   else { constexpr bool NAME = false; __VA_ARGS__; }
 
+// double-buffered forward for key ranges > 128 (APEX_ATTN_FWD_DB=0 selects the two-barrier loop)
+inline bool attn_fwd_db() {
+  static const bool on = [] {
+    const char* e = getenv("APEX_ATTN_FWD_DB");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 template <int D>
 int attn_fwd_impl(const AttnArgs& a, int dt, hipStream_t s) {
   dim3 grid((a.Sq + kFwdBQ - 1) / kFwdBQ, a.B * a.H);
@@ -1042,6 +1074,15 @@ int attn_fwd_impl(const AttnArgs& a, int dt, hipStream_t s) {
           hipLaunchKernelGGL((attn_fwd_kernel<T, 64, C, false, true, false>), grid, dim3(256), 0, s, a)));
       return (int)hipGetLastError();
     }
+  }
+  // double-buffered loop where it measured faster (profiles/r2_attn_fwd_db_ab.txt, same box): D >= 128
+  // (Megatron s2048 d128: 213 -> 195 us p = 0, 279 -> 269 p = 0.1) and D = 64 without dropout at 3
+  // waves/SIMD (GPT-2 s1024: 104 -> 90 us); D = 64 with dropout keeps the two-barrier loop (the
+  // Philox temporaries spill at 168 VGPRs: 145 -> 187 us, and at 2 waves/SIMD DB is 3 % slower)
+  if (attn_fwd_db() && a.Sk > 2 * kFwdKB && (D >= 128 || (D == 64 && !drop))) {
+    ATTN_DISPATCH(dt, T, ATTN_DISPATCH_B(a.causal, C, ATTN_DISPATCH_B(drop, DR, ATTN_DISPATCH_B(a.bias != nullptr, BI,
+        hipLaunchKernelGGL((attn_fwd_kernel<T, D, C, DR, false, BI, true>), grid, dim3(256), 0, s, a)))));
+    return (int)hipGetLastError();
   }
   ATTN_DISPATCH(dt, T, ATTN_DISPATCH_B(a.causal, C, ATTN_DISPATCH_B(drop, DR, ATTN_DISPATCH_B(a.bias != nullptr, BI,
       hipLaunchKernelGGL((attn_fwd_kernel<T, D, C, DR, false, BI>), grid, dim3(256), 0, s, a)))));
