@@ -496,8 +496,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
   __shared__ __attribute__((aligned(16))) T lds_do[kBwdBQ * LDQ];
   __shared__ __attribute__((aligned(16))) T lds_k[LDSK];
   __shared__ __attribute__((aligned(16))) T lds_ds[kBwdBQ * LDS_S];
-  __shared__ float lds_lse[kBwdBQ], lds_delta[kBwdBQ];
-  __shared__ uint32_t lds_mask[4 * kBwdBQ];  // [wave's 32-key block][q]: bit k <-> key 32 wid + k
+  __shared__ __attribute__((aligned(16))) float lds_lse[kBwdBQ], lds_delta[kBwdBQ];
+  __shared__ __attribute__((aligned(16))) uint32_t lds_mask[4 * kBwdBQ];  // [wave's 32-key block][q]: bit k <-> key 32 wid + k
 
   // wid through readfirstlane: wave-uniform in SGPRs, so tile-level conditions become scalar branches
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -644,8 +644,26 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
     }
     if (threadIdx.x < kBwdBQ) lds_lse[threadIdx.x] = P.lse * kLog2e;  // +inf stays +inf
     if (DROPOUT && threadIdx.x < 4 * kBwdBQ) lds_mask[threadIdx.x] = P.mask;
-    if (qb + AHEAD * kBwdBQ < nq && !(a.dbg & 8)) fetch(P, qb + AHEAD * kBwdBQ);
+    if (qb + AHEAD * kBwdBQ < nq) fetch(P, qb + AHEAD * kBwdBQ);
     lds_barrier();
+
+    // D >= 128 (one wave per SIMD): lse / delta / dropout words of this lane's 16 query rows
+    // (8g + 4hl + e, e = 0..3) as 16-byte LDS reads issued ahead of the S / dP products, so their
+    // latency hides behind the MFMAs (a scalar read + wait per element exposed ~16 LDS round trips
+    // per step with no partner wave to cover them). D <= 64 runs two waves per SIMD and has no
+    // 48 spare VGPRs: it reads the scalars in the elementwise loop.
+    constexpr bool VROWS = D >= 128;
+    f32x4 lse4[4], del4[4];
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 msk4[4];
+    if constexpr (VROWS) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        lse4[g] = *(const f32x4*)(lds_lse + 8 * g + 4 * hl);
+        del4[g] = *(const f32x4*)(lds_delta + 8 * g + 4 * hl);
+        if (DROPOUT) msk4[g] = *(const u32x4*)(lds_mask + wid * kBwdBQ + 8 * g + 4 * hl);
+      }
+    }
 
     // S = Q . K^T  [32 q x 32 keys]: A = Q rows (LDS), B = K rows (regs)
     f32x16 sacc = f32x16{}, dpacc = f32x16{};
@@ -661,40 +679,48 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
     // ds = P * (dP * keep / (1-p) - delta) (the softmax scale of dK / dQ likewise).
     float pd[16], ds[16];
     const bool interior = (k0 + 32 * wid + 31 < Sk) && (qb + kBwdBQ <= nq) && (!CAUSAL || k0 + 32 * wid + 31 <= qb);
-    // exp2 is the bare v_exp_f32 (no denormal range reduction)
+    // exp2 is the bare v_exp_f32 (no denormal range reduction). One wave-uniform branch picks the
+    // boundary variant for the whole tile (a per-element branch split the section into 16 blocks
+    // the scheduler could not interleave).
+    auto elementwise = [&](auto bound_tag) {
+      constexpr bool BOUND = decltype(bound_tag)::value;
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int qr0 = (g * 8) + 4 * hl;
+      for (int g = 0; g < 4; ++g) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int i = 4 * g + e;
-        const int qi = qr0 + e;
-        float lterm = -lds_lse[qi];
-        if constexpr (BIAS) {
-          const int q = qb + qi;
-          if (q < nq && mykey < Sk) lterm = fmaf(to_f(bcol[(int64_t)q * a.bias_qs]), kLog2e, lterm);
+        for (int e = 0; e < 4; ++e) {
+          const int i = 4 * g + e;
+          const int qi = 8 * g + 4 * hl + e;
+          float lterm = -(VROWS ? lse4[g][e] : lds_lse[qi]);
+          if constexpr (BIAS) {
+            const int q = qb + qi;
+            if (q < nq && mykey < Sk) lterm = fmaf(to_f(bcol[(int64_t)q * a.bias_qs]), kLog2e, lterm);
+          }
+          float p = __builtin_amdgcn_exp2f(fmaf(sacc[i], a.scale_log2, lterm));
+          if constexpr (BOUND) {
+            const int q = qb + qi;
+            const bool valid = (mykey < Sk) && (q < nq) && !(CAUSAL && mykey > q);
+            p = valid ? p : 0.f;
+          }
+          float dpv = dpacc[i];
+          float pk = p;
+          if constexpr (DROPOUT) {
+            const int m = __builtin_amdgcn_sbfe((int)(VROWS ? msk4[g][e] : lds_mask[wid * kBwdBQ + qi]), r, 1);
+            pk = __builtin_bit_cast(float, __builtin_bit_cast(int, p) & m);
+            dpv = __builtin_bit_cast(float, __builtin_bit_cast(int, dpv) & m);
+          }
+          pd[i] = pk;
+          ds[i] = p * fmaf(dpv, rkeep, -(VROWS ? del4[g][e] : lds_delta[qi]));
         }
-        float p = __builtin_amdgcn_exp2f(fmaf(sacc[i], a.scale_log2, lterm));
-        if (!interior) {
-          const int q = qb + qi;
-          const bool valid = (mykey < Sk) && (q < nq) && !(CAUSAL && mykey > q);
-          p = valid ? p : 0.f;
-        }
-        float dpv = dpacc[i];
-        float pk = p;
-        if (DROPOUT) {
-          const int m = __builtin_amdgcn_sbfe((int)lds_mask[wid * kBwdBQ + qi], r, 1);
-          pk = __builtin_bit_cast(float, __builtin_bit_cast(int, p) & m);
-          dpv = __builtin_bit_cast(float, __builtin_bit_cast(int, dpv) & m);
-        }
-        pd[i] = pk;
-        ds[i] = p * fmaf(dpv, rkeep, -lds_delta[qi]);
       }
-    }
+    };
+    if (interior)
+      elementwise(std::false_type{});
+    else
+      elementwise(std::true_type{});
     // dV += P^T . dO : accumulator-as-A (contraction over q = rows), B = dO via tr reads
     // dK += dS^T . Q : same with Q
 #pragma unroll
-    for (int s2 = 0; s2 < 2 && !(a.dbg & 2); ++s2) {
+    for (int s2 = 0; s2 < 2; ++s2) {
       const V8 pa = pack8<T, V8>(pd + 8 * s2);
       const V8 sa = pack8<T, V8>(ds + 8 * s2);
       const int kq = 16 * s2 + 4 * hl + ((lane & 15) >> 2);
@@ -707,7 +733,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
         dk[db] = M::mma(sa, qbf, dk[db]);
       }
     }
-    if (DQ && !(a.dbg & 1)) {
+    if constexpr (DQ) {
     // dS to LDS as [q][key] (bf16) for dQ = dS . K
 #pragma unroll
     for (int i = 0; i < 16; ++i) {

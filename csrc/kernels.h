@@ -96,7 +96,7 @@ struct AttnArgs {
   uint16_t* dmask;       // dropout keep bits [B*H, Sq, mask_words] (fwd writes, bwd reads): one
                          // 32-bit word per (row, 32-key block), bit k <-> key 32 blk + k
   int64_t mask_words;    // 2 * ceil(Sk / 32) (uint16 units)
-  int dbg;               // diagnostics only (tools/attn_bench.py --dbg): bits skip backward sections
+  int dbg;               // unused by the kernels (the runtime section-skip branches forced accumulator copies)
   float* dsum;           // optional, zeroed [B][3][H][D]: bwd adds the column sums (over positions)
                          // of dq, dk, dv — the packed-QKV projection's bias gradient, per batch
   const void* bias;      // optional additive score bias (input dtype), element (b, h, q, key) at
