@@ -619,6 +619,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
     uint4 (&pf_q)[NLD] = P.q;
     uint4 (&pf_do)[NLD] = P.d;
     uint4 (&pf_o)[NLD] = P.o;
+    if constexpr (D >= 128) {
+      // keep dK / dV in AGPRs across the step (else the allocator parks two of them in VGPRs while
+      // the S / dP products use their AGPRs: 64 accvgpr moves per step)
+#pragma unroll
+      for (int i = 0; i < D / 32; ++i) asm volatile("" : "+a"(dk[i]), "+a"(dv[i]));
+    }
     lds_barrier();
     // stage the prefetched tiles; delta = rowsum(dO * O) is computed here from O
     // (CPR consecutive threads own one row -> xor-shuffle reduce), no separate pass.
@@ -952,6 +958,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
   if (ntiles > 0) gload(kva, 0);
   if (KV2 && ntiles > 1) gload(kvb, 1);
   auto tile = [&](KV& R, const int kt) {
+    if constexpr (D >= 128) {
+      // pin the dQ accumulators to AGPRs at the tile boundary: without it the allocator copied all
+      // 64 of them to VGPRs and back every tile so the S / dP products could use their AGPRs
+#pragma unroll
+      for (int i = 0; i < D / 32; ++i) asm volatile("" : "+a"(dq[i]));
+    }
     lds_barrier();  // previous tile fully consumed
     lstore(R);
     const uint32_t mcur[2] = {R.m[0] >> (4 * hl), R.m[1] >> (4 * hl)};
