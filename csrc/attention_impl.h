@@ -478,12 +478,35 @@ constexpr int kBwdWaves = 4;
 constexpr int kBwdBK = 32 * kBwdWaves;  // 128 keys per workgroup
 constexpr int kBwdBQ = 32;              // queries per inner step
 
+// delta = rowsum(dO * O) per query row, once (attn_bwd_delta_kernel), for the two-kernel backward:
+// every dK/dV workgroup of a query block used to recompute it from O (a third 32 x D tile load,
+// its unpack and a shuffle reduction per step, Sk / 128 times per row).
+template <typename T, int D>
+__global__ void __launch_bounds__(256) attn_bwd_delta_kernel(AttnArgs a, const void* dout, float* delta) {
+  constexpr int CPR = D / 8;  // 16-byte chunks per row (4..32 lanes, a power of two)
+  const int bh = blockIdx.y;
+  const int b = bh / a.H, h = bh % a.H;
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  const int q = idx / CPR, col = (idx % CPR) * 8;
+  float part = 0.f;
+  if (q < a.Sq) {
+    float ov[8], dov[8];
+    load_f<T, 8>((const T*)a.o + b * a.o_bs + h * a.o_hs + (int64_t)q * a.o_ss + col, ov);
+    load_f<T, 8>((const T*)dout + b * a.do_bs + h * a.do_hs + (int64_t)q * a.do_ss + col, dov);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) part += ov[e] * dov[e];
+  }
+#pragma unroll
+  for (int o = CPR / 2; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+  if (q < a.Sq && (idx % CPR) == 0) delta[(int64_t)bh * a.Sq + q] = part;
+}
+
 // DQ = true (Sk <= 128: the workgroup holds every key, so it is the sole owner of dQ for its
-// query rows and writes it directly). DQ = false (longer key ranges): dK/dV only; the key-block-0
-// workgroups also store delta = rowsum(dO * O) into delta_out, and attn_bwd_dq_kernel computes dQ
-// from a query-stationary loop (no cross-workgroup fp32 atomics; see the kernel below).
+// query rows and writes it directly; delta is computed here from O). DQ = false (longer key
+// ranges): dK/dV only, delta read from attn_bwd_delta_kernel's output, and attn_bwd_dq_kernel
+// computes dQ from a query-stationary loop (no cross-workgroup fp32 atomics; see the kernel below).
 template <typename T, int D, bool CAUSAL, bool DROPOUT, bool DSUM, bool DQ, bool BIAS>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2 : 1, D <= 64 ? 2 : 1))) attn_bwd_kernel(AttnArgs a, const void* dout, float* delta_out,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2 : 1, D <= 64 ? 2 : 1))) attn_bwd_kernel(AttnArgs a, const void* dout, const float* delta_in,
                                                          void* dk_out, void* dv_out) {
   using M = MfmaT<T>;
   using V8 = typename M::V8;
@@ -514,6 +537,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
   const T* dop = (const T*)dout + b * a.do_bs + h * a.do_hs;
   const T* op = (const T*)a.o + b * a.o_bs + h * a.o_hs;
   const float* lsep = a.lse + (int64_t)bh * a.Sq;
+  const float* dlp = DQ ? nullptr : delta_in + (int64_t)bh * a.Sq;
   // BIAS: this lane's key column of the bias, bcol[q * bias_qs]
   const T* bcol = BIAS ? (const T*)a.bias + b * a.bias_bs + h * a.bias_hs + min(mykey, a.Sk - 1) : nullptr;
 
@@ -538,8 +562,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
   constexpr int NCHK = kBwdBQ * CPR;                // 16-byte chunks per 32-row tile
   constexpr int NLD = NCHK >= 256 ? NCHK / 256 : 1;  // per thread (D = 32: half the threads)
   struct Pf {
-    uint4 q[NLD], d[NLD], o[NLD];
-    float lse;
+    uint4 q[NLD], d[NLD], o[DQ ? NLD : 1];
+    float lse, dl;
     uint32_t mask;
   };
   // two register sets where they fit (dK/dV-only kernel at D = 64); one set (prefetch one step
@@ -550,22 +574,26 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
   auto fetch = [&](Pf& P, int qb) {
     uint4 (&pf_q)[NLD] = P.q;
     uint4 (&pf_do)[NLD] = P.d;
-    uint4 (&pf_o)[NLD] = P.o;
     float& pf_lse = P.lse;
     uint32_t& pf_mask = P.mask;
     pf_lse = INFINITY;
     pf_mask = 0u;
+    // block base pointers are wave-uniform (scalar 64-bit math); the per-lane part is a 32-bit
+    // offset (row < 32 rows of one block) that the compiler hoists out of the loop
+    const T* qbase = qp + (int64_t)qb * a.q_ss;
+    const T* dbase = dop + (int64_t)qb * a.do_ss;
 #pragma unroll
     for (int c = 0; c < NLD; ++c) {
       const int idx = threadIdx.x + 256 * c;
       const int row = idx / CPR, col = (idx % CPR) * 8;
       const int q = qb + row;
       if (q < nq && idx < NCHK) {
-        pf_q[c] = *(const uint4*)(qp + (int64_t)q * a.q_ss + col);
-        pf_do[c] = *(const uint4*)(dop + (int64_t)q * a.do_ss + col);
-        pf_o[c] = *(const uint4*)(op + (int64_t)q * a.o_ss + col);
+        pf_q[c] = *(const uint4*)(qbase + (row * (int)a.q_ss + col));
+        pf_do[c] = *(const uint4*)(dbase + (row * (int)a.do_ss + col));
+        if constexpr (DQ) P.o[c] = *(const uint4*)(op + (int64_t)q * a.o_ss + col);
       } else {
-        pf_q[c] = pf_do[c] = pf_o[c] = make_uint4(0, 0, 0, 0);
+        pf_q[c] = pf_do[c] = make_uint4(0, 0, 0, 0);
+        if constexpr (DQ) P.o[c] = make_uint4(0, 0, 0, 0);
       }
     }
     // raw values only: any arithmetic on a loaded value here would make the compiler wait for
@@ -573,6 +601,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
     if (threadIdx.x < kBwdBQ) {
       const int q = qb + threadIdx.x;
       if (q < nq) pf_lse = lsep[q];  // natural log; x log2(e) at staging
+    }
+    if (!DQ && threadIdx.x >= 128 && threadIdx.x < 128 + kBwdBQ) {
+      const int q = qb + threadIdx.x - 128;
+      P.dl = q < nq ? dlp[q] : 0.f;
     }
     if (DROPOUT && threadIdx.x < 4 * kBwdBQ) {
       // dropout words written by the forward: one per (query, 32-key block), bit k <-> key k
@@ -618,7 +650,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
   auto body = [&](Pf& P, const int qb) {
     uint4 (&pf_q)[NLD] = P.q;
     uint4 (&pf_do)[NLD] = P.d;
-    uint4 (&pf_o)[NLD] = P.o;
     if constexpr (D >= 128) {
       // keep dK / dV in AGPRs across the step (else the allocator parks two of them in VGPRs while
       // the S / dP products use their AGPRs: 64 accvgpr moves per step)
@@ -633,22 +664,22 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
       const int idx = threadIdx.x + 256 * c;
       if (NCHK < 256 && idx >= NCHK) break;  // (wave-uniform: D = 32 leaves waves 2, 3 out)
       const int row = idx / CPR, col = (idx % CPR) * 8;
-      float ov[8], dov[8];
-      load_f<T, 8>((const T*)&pf_o[c], ov);
-      load_f<T, 8>((const T*)&pf_do[c], dov);
-      float part = 0.f;
+      if constexpr (DQ) {
+        float ov[8], dov[8];
+        load_f<T, 8>((const T*)&P.o[c], ov);
+        load_f<T, 8>((const T*)&pf_do[c], dov);
+        float part = 0.f;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) part += ov[e] * dov[e];
+        for (int e = 0; e < 8; ++e) part += ov[e] * dov[e];
 #pragma unroll
-      for (int o = CPR / 2; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
-      if ((idx % CPR) == 0) {
-        lds_delta[row] = part;
-        if (!DQ && blockIdx.x == 0 && qb + row < nq) delta_out[(int64_t)bh * a.Sq + qb + row] = part;
+        for (int o = CPR / 2; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+        if ((idx % CPR) == 0) lds_delta[row] = part;
       }
       *(uint4*)(lds_q + row * LDQ + col) = pf_q[c];
       *(uint4*)(lds_do + row * LDQ + col) = pf_do[c];
     }
     if (threadIdx.x < kBwdBQ) lds_lse[threadIdx.x] = P.lse * kLog2e;  // +inf stays +inf
+    if (!DQ && threadIdx.x >= 128 && threadIdx.x < 128 + kBwdBQ) lds_delta[threadIdx.x - 128] = P.dl;
     if (DROPOUT && threadIdx.x < 4 * kBwdBQ) lds_mask[threadIdx.x] = P.mask;
     if (qb + AHEAD * kBwdBQ < nq) fetch(P, qb + AHEAD * kBwdBQ);
     lds_barrier();
@@ -1136,6 +1167,10 @@ int attn_bwd_impl(const AttnArgs& a, const void* dout, float* delta_ws, void* dk
   if (a.bias && a.dsum) return -5;  // (not instantiated: the packed-QKV bias-grad fusion runs without a score bias)
   dim3 grid((a.Sk + kBwdBK - 1) / kBwdBK, a.B * a.H);
   dim3 qgrid((a.Sq + kFwdBQ - 1) / kFwdBQ, a.B * a.H);
+  if (multi) {
+    dim3 dgrid((a.Sq * (D / 8) + 255) / 256, a.B * a.H);
+    ATTN_DISPATCH(dt, T, hipLaunchKernelGGL((attn_bwd_delta_kernel<T, D>), dgrid, dim3(256), 0, s, a, dout, delta_ws));
+  }
   ATTN_DISPATCH(dt, T, ATTN_DISPATCH_B(a.causal, C, ATTN_DISPATCH_B(drop, DR, {
     if (a.bias) {
       if (multi) {

@@ -415,7 +415,7 @@ void flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor 
     a.dmask = (uint16_t*)dmask->data_ptr();
   }
   const int64_t rows = (int64_t)a.B * a.H * a.Sq;
-  Tensor delta_ws;  // rowsum(dO * O) handed from the dK/dV kernel to the dQ kernel
+  Tensor delta_ws;  // rowsum(dO * O), one pre-pass kernel, read by the dK/dV and dQ kernels
   if (apex::attn_bwd_needs_dq_acc(a)) delta_ws = at::empty({rows}, q.options().dtype(at::kFloat));
   check(apex::attn_bwd(a, dout.data_ptr(), delta_ws.defined() ? delta_ws.data_ptr<float>() : nullptr,
                        dk.data_ptr(), dv.data_ptr(), dt_code(q.scalar_type()), cur_stream()),
