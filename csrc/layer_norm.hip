@@ -198,6 +198,108 @@ __global__ void __launch_bounds__(kLnBlock) ln_bwd_fast(const T* __restrict__ dy
   }
 }
 
+// Wide rows (VPT 5..8 vectors per lane, e.g. Megatron's H = 2560 / 4096): the register-resident
+// fast kernel would need 4 x VPT x 8 fp32 row/partial registers, so this one keeps only the
+// dgamma / dbeta partials in registers and reads each row twice (the second pass hits L1/L2: a row
+// is 5-8 KB), with gamma from cache. Same per-block partial rows as ln_bwd_fast (replaces the
+// block-per-row dx kernel + strided column kernel of the slow path).
+template <typename T, typename W, int VPT, bool RMS>
+__global__ void __launch_bounds__(kLnBlock) ln_bwd_wide(const T* __restrict__ dy,
+                                                       const T* __restrict__ x,
+                                                       const W* __restrict__ gamma,
+                                                       const float* __restrict__ mean,
+                                                       const float* __restrict__ rstd,
+                                                       T* __restrict__ dx, float* __restrict__ ws,
+                                                       int64_t rows, int cols, int rpw) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // [4 waves][cols]
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nvec = cols >> 3;
+  const float inv_n = 1.f / (float)cols;
+  float dg[VPT][8], db[VPT][8];
+#pragma unroll
+  for (int j = 0; j < VPT; ++j)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dg[j][k] = db[j][k] = 0.f;
+  auto gam = [&](int vi, float (&g)[8]) {
+    if (gamma) load_f<W, 8>(gamma + vi * 8, g);
+    else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) g[k] = 1.f;
+    }
+  };
+  const int64_t r0 = (int64_t)blockIdx.x * rpw * (kLnBlock / 64);
+  for (int rr = 0; rr < rpw; ++rr) {
+    const int64_t row = r0 + (int64_t)rr * (kLnBlock / 64) + wid;
+    if (row >= rows) break;
+    const float mu = RMS ? 0.f : mean[row];
+    const float rs = rstd[row];
+    const T* xr = x + row * cols;
+    const T* dyr = dy + row * cols;
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int vi = j * 64 + lane;
+      if (vi < nvec) {
+        float xv[8], dv[8], g[8];
+        load_f<T, 8>(xr + vi * 8, xv);
+        load_f<T, 8>(dyr + vi * 8, dv);
+        gam(vi, g);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float xh = (xv[k] - mu) * rs;
+          const float dyg = dv[k] * g[k];
+          s1 += dyg;
+          s2 += dyg * xh;
+          dg[j][k] += dv[k] * xh;
+          db[j][k] += dv[k];
+        }
+      }
+    }
+    s2 = wave_sum(s2) * inv_n;
+    if (!RMS) s1 = wave_sum(s1) * inv_n;
+    T* dxr = dx + row * cols;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int vi = j * 64 + lane;
+      if (vi < nvec) {
+        float xv[8], dv[8], g[8], o[8];
+        load_f<T, 8>(xr + vi * 8, xv);
+        load_f<T, 8>(dyr + vi * 8, dv);
+        gam(vi, g);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float xh = (xv[k] - mu) * rs;
+          const float dyg = dv[k] * g[k];
+          o[k] = RMS ? rs * (dyg - xh * s2) : rs * (dyg - s1 - xh * s2);
+        }
+        store_f<T, 8>(dxr + vi * 8, o);
+      }
+    }
+  }
+  // combine the 4 waves' partials through LDS, dgamma then dbeta ([4 waves][cols] each: <= 64 KB)
+  float* mine = lds + wid * cols;
+  float* out = ws + (int64_t)blockIdx.x * 2 * cols;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    if (half) __syncthreads();
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int vi = j * 64 + lane;
+      if (vi < nvec) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) mine[vi * 8 + k] = half ? db[j][k] : dg[j][k];
+      }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < cols; c += kLnBlock) {
+      float a = 0.f;
+#pragma unroll
+      for (int w = 0; w < kLnBlock / 64; ++w) a += lds[w * cols + c];
+      out[half * cols + c] = a;
+    }
+  }
+}
+
 // ------------------------------ slow path ----------------------------------
 template <typename T, typename W, bool RMS>
 __global__ void __launch_bounds__(kLnBlock) ln_fwd_slow(const T* __restrict__ x,
@@ -359,6 +461,9 @@ int layer_norm_bwd(const void* dy, const void* x, const void* gamma, const float
   if (rows == 0) return 0;
   if (!gamma) wdt = xdt;
   const bool fast = ln_fast_ok(x, dy, dx, gamma, cols) && ln_vpt(cols) <= 4;
+  // wide rows: 5..8 16-byte vectors per lane (cols 2056 .. 4096)
+  const int wvpt = (cols % 8 == 0 && cols / 8 > 256 && cols / 8 <= 512) ? (cols / 8 + 63) / 64 : 0;
+  const bool wide = !fast && wvpt > 0 && ln_fast_ok(x, dy, dx, gamma, cols);
   const bool need_gb = dgamma || dbeta;
   LN_DISPATCH_T(xdt, T, LN_DISPATCH_T(wdt, W, LN_DISPATCH_RMS(rms, RMS, {
     int parts;
@@ -372,6 +477,21 @@ int layer_norm_bwd(const void* dy, const void* x, const void* gamma, const float
           hipLaunchKernelGGL((ln_bwd_fast<T, W, VPT, RMS>), dim3(parts), dim3(kLnBlock), lds, s,
                              (const T*)dy, (const T*)x, (const W*)gamma, mean, rstd, (T*)dx, ws,
                              rows, cols, rpw));
+    } else if (wide) {
+      const int rpw = ln_bwd_rpw(rows);
+      const int64_t rpb = (int64_t)rpw * (kLnBlock / 64);
+      parts = (int)((rows + rpb - 1) / rpb);
+      const size_t lds = (size_t)4 * cols * sizeof(float);
+      switch (wvpt) {
+        case 5: hipLaunchKernelGGL((ln_bwd_wide<T, W, 5, RMS>), dim3(parts), dim3(kLnBlock), lds, s, (const T*)dy,
+                                   (const T*)x, (const W*)gamma, mean, rstd, (T*)dx, ws, rows, cols, rpw); break;
+        case 6: hipLaunchKernelGGL((ln_bwd_wide<T, W, 6, RMS>), dim3(parts), dim3(kLnBlock), lds, s, (const T*)dy,
+                                   (const T*)x, (const W*)gamma, mean, rstd, (T*)dx, ws, rows, cols, rpw); break;
+        case 7: hipLaunchKernelGGL((ln_bwd_wide<T, W, 7, RMS>), dim3(parts), dim3(kLnBlock), lds, s, (const T*)dy,
+                                   (const T*)x, (const W*)gamma, mean, rstd, (T*)dx, ws, rows, cols, rpw); break;
+        default: hipLaunchKernelGGL((ln_bwd_wide<T, W, 8, RMS>), dim3(parts), dim3(kLnBlock), lds, s, (const T*)dy,
+                                    (const T*)x, (const W*)gamma, mean, rstd, (T*)dx, ws, rows, cols, rpw); break;
+      }
     } else {
       hipLaunchKernelGGL((ln_bwd_dx_slow<T, W, RMS>), dim3((unsigned)rows), dim3(kLnBlock), 0, s,
                          (const T*)dy, (const T*)x, (const W*)gamma, mean, rstd, (T*)dx, cols);

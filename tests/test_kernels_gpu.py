@@ -145,13 +145,14 @@ def test_fused_lamb_optimizer_matches_reference(nvlamb):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
-@pytest.mark.parametrize("cols", [1024, 1600, 768, 64, 100, 4096, 5000])
+@pytest.mark.parametrize("cols,rows", [(1024, 333), (1600, 333), (768, 333), (64, 333), (100, 333), (4096, 333),
+                                       (5000, 333), (2560, 333), (2056, 333), (3072, 333), (2560, 7000)])
 @pytest.mark.parametrize("rms", [False, True])
-def test_layer_norm_fwd_bwd(dt, cols, rms):
+def test_layer_norm_fwd_bwd(dt, cols, rows, rms):
+    """cols 2056..4096 run the wide-row backward (ln_bwd_wide), rows 7000 several rows per wave."""
     from apex.normalization import FusedLayerNorm, FusedRMSNorm
 
     torch.manual_seed(cols)
-    rows = 333
     x = torch.randn(rows, cols, device=DEV).to(dt).requires_grad_(True)
     mod = (FusedRMSNorm if rms else FusedLayerNorm)(cols).to(DEV).to(dt)
     with torch.no_grad():
