@@ -95,6 +95,29 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// Cross-lane exchanges without an LDS round trip (__shfl_xor lowers to ds_bpermute + a wait):
+// the lane ^ 32 partner through gfx950's v_permlane32_swap, and sums over aligned groups of
+// 4 / 8 / 16 lanes through DPP (quad_perm, row_half_mirror, row_mirror).
+__device__ __forceinline__ uint32_t xor32_u(uint32_t v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return (__lane_id() & 32) ? r[0] : r[1];
+}
+__device__ __forceinline__ float xor32_f(float v) { return __uint_as_float(xor32_u(__float_as_uint(v))); }
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int N>  // every lane of each aligned N-lane group ends with the group's sum
+__device__ __forceinline__ float group_sum(float v) {
+  static_assert(N == 1 || N == 2 || N == 4 || N == 8 || N == 16 || N == 32, "group size");
+  if constexpr (N >= 2) v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]: lane ^ 1
+  if constexpr (N >= 4) v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]: lane ^ 2
+  if constexpr (N >= 8) v += dpp_f<0x141>(v);  // row_half_mirror: the other quad of the 8
+  if constexpr (N >= 16) v += dpp_f<0x140>(v); // row_mirror: the other 8 of the row
+  if constexpr (N >= 32) v += __shfl_xor(v, 16, 64);
+  return v;
+}
+
 template <typename V8>
 __device__ __forceinline__ V8 join4(s16x4 lo, s16x4 hi) {
   typedef short s16x8 __attribute__((ext_vector_type(8)));
@@ -279,7 +302,7 @@ attn_fwd_kernel(AttnArgs a) {
       for (int sb = 0; sb < 2; ++sb) {
         const int blk = (kt * kFwdKB >> 5) + sb;
         const uint32_t hb = dg.half_bits(bh, qrow, blk, hl, a.Sq);  // bits at 4 hl + {0-3, 8-11, ..}
-        const uint32_t word = hb | __shfl_xor(hb, 32, 64);
+        const uint32_t word = hb | xor32_u(hb);
         if (hl == 0 && mrow && blk * 32 < a.Sk) mrow[blk] = word;
         mcur[sb] = hb >> (4 * hl);
       }
@@ -363,7 +386,7 @@ attn_fwd_kernel(AttnArgs a) {
     for (int sb = 0; sb < 2; ++sb)
 #pragma unroll
       for (int i = 0; i < 16; ++i) tmax = fmaxf(tmax, st[sb][i]);
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    tmax = fmaxf(tmax, xor32_f(tmax));
     const float mnew = fmaxf(m, tmax);
     const float muse = mnew == -INFINITY ? 0.f : mnew;
     const float alpha = __builtin_amdgcn_exp2f((m - muse) * sl2);
@@ -451,7 +474,7 @@ attn_fwd_kernel(AttnArgs a) {
     for (int kt = 0; kt < ntiles; ++kt) tile(kva, kt);
   }
   // ---- epilogue
-  const float ltot = l + __shfl_xor(l, 32, 64);
+  const float ltot = l + xor32_f(l);
   if (qrow < a.Sq) {
     const float inv = ltot > 0.f ? (DROPOUT ? a.drop_scale : 1.f) / ltot : 0.f;
     T* op = (T*)a.o + b * a.o_bs + h * a.o_hs + (int64_t)qrow * a.o_ss;
@@ -496,8 +519,7 @@ __global__ void __launch_bounds__(256) attn_bwd_delta_kernel(AttnArgs a, const v
 #pragma unroll
     for (int e = 0; e < 8; ++e) part += ov[e] * dov[e];
   }
-#pragma unroll
-  for (int o = CPR / 2; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+  part = group_sum<CPR>(part);
   if (q < a.Sq && (idx % CPR) == 0) delta[(int64_t)bh * a.Sq + q] = part;
 }
 
@@ -671,8 +693,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
         float part = 0.f;
 #pragma unroll
         for (int e = 0; e < 8; ++e) part += ov[e] * dov[e];
-#pragma unroll
-        for (int o = CPR / 2; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+        part = group_sum<CPR>(part);
         if ((idx % CPR) == 0) lds_delta[row] = part;
       }
       *(uint4*)(lds_q + row * LDQ + col) = pf_q[c];
@@ -839,8 +860,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         v[i] = dqcs[t][i];
-#pragma unroll
-        for (int o = 8; o > 0; o >>= 1) v[i] += __shfl_xor(v[i], o, 64);  // all 16 lanes hold the sum
+        v[i] = group_sum<16>(v[i]);  // all 16 lanes hold the sum
       }
       // lane lq < 4 of each group adds dim 4 lg + lq: one atomic instruction (16 lanes) per tile
       // (atomics cost per instruction, so 4 single-lane instructions would cost 4x)
@@ -863,7 +883,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
         if constexpr (DSUM) sum += (k0 + kl < a.Sk) ? (float)v : 0.f;
       }
       if constexpr (DSUM) {
-        sum += __shfl_xor(sum, 32, 64);
+        sum += xor32_f(sum);
         if (hl == 0) atomicAdd(dsum_t + 32 * db + r, sum);
       }
     }
@@ -1096,8 +1116,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float t = qrow < a.Sq ? (float)w[e] : 0.f;
-#pragma unroll
-          for (int o = 16; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+          t = group_sum<32>(t);
           if (r == 0) atomicAdd(dsum + 32 * db + 8 * g + 4 * hl + e, t);
         }
       }
