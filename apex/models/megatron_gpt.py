@@ -157,7 +157,7 @@ class MegatronGPT(nn.Module):
         if labels is None:
             return logits
         shifted = torch.cat([labels[:, 1:], labels[:, -1:]], 1)
-        loss = tp.vocab_parallel_cross_entropy(logits.float(), shifted)
+        loss = tp.vocab_parallel_cross_entropy(logits, shifted)  # fp32 statistics inside
         return loss[:, :-1].mean()
 
 

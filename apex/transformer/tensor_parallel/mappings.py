@@ -80,13 +80,15 @@ class _CopyToModelParallelRegion(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        return _reduce(g.clone())
+        # the all-reduce runs in place, so it works on a copy of the incoming gradient; at TP = 1
+        # there is no collective and no copy (5 [tokens, hidden] clones per layer otherwise)
+        return g if ps.get_tensor_model_parallel_world_size() == 1 else _reduce(g.clone())
 
 
 class _ReduceFromModelParallelRegion(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x):
-        return _reduce(x.clone())
+        return x if ps.get_tensor_model_parallel_world_size() == 1 else _reduce(x.clone())
 
     @staticmethod
     def backward(ctx, g):
