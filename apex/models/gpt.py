@@ -11,6 +11,7 @@ Pre-LN decoder blocks; every hot op is an apex fused op on MI355X:
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -21,6 +22,9 @@ from ..normalization import FusedLayerNorm
 from ..ops import blocks as fblocks
 from ..ops import fused as fops
 
+
+# APEX_GPT_FUSED_LN=0: per-block forward (separate LayerNorms; A/B and fallback switch)
+_FUSED_LN = os.environ.get("APEX_GPT_FUSED_LN", "1") != "0"
 
 @dataclass
 class GPTConfig:
@@ -77,6 +81,24 @@ class GPTBlock(nn.Module):
             t = fops.fused_dense(h, self.mlp_proj.weight, None)
         return fops.bias_dropout_add(t, self.mlp_proj.bias, x, p)
 
+    def forward_fused(self, x, xn, nxt):
+        """The same block with its LayerNorms fused into the residual updates before them: takes the
+        residual stream x and xn = ln_1(x), returns (x', nxt(x')) where nxt is the NEXT block's ln_1
+        (or the final ln_f). Each residual update + the LayerNorm after it is one bdaln kernel each
+        way (fops.bias_dropout_add_ln), so the stream is not re-read by a separate LayerNorm and its
+        two gradients are summed inside the LayerNorm backward."""
+        B, S, E = x.shape
+        p = self.p if self.training else 0.0
+        qkv = fops.fused_dense(xn, self.c_attn.weight, self.c_attn.bias).view(B, S, 3, self.h, self.d)
+        ctx = fops.attention_qkv_packed(qkv, None, p, causal=True).reshape(B, S, E)
+        x, xn = fops.bias_dropout_add_ln(fops.fused_dense(ctx, self.c_proj.weight, None), self.c_proj.bias, x,
+                                         self.ln_2.weight, self.ln_2.bias, p, self.ln_2.eps)
+        t = fblocks.mlp(xn, self.c_fc.weight, self.c_fc.bias, self.mlp_proj.weight, fops.ACT_GELU_TANH)
+        if t is None:
+            h = fops.dense_act(xn, self.c_fc.weight, self.c_fc.bias, fops.ACT_GELU_TANH)
+            t = fops.fused_dense(h, self.mlp_proj.weight, None)
+        return fops.bias_dropout_add_ln(t, self.mlp_proj.bias, x, nxt.weight, nxt.bias, p, nxt.eps)
+
 
 class GPTModel(nn.Module):
     def __init__(self, c: GPTConfig):
@@ -106,9 +128,17 @@ class GPTModel(nn.Module):
         pos = torch.arange(S, device=input_ids.device)
         x = self.wte(input_ids) + self.wpe(pos)[None]
         x = F.dropout(x, self.config.dropout, self.training)
-        for blk in self.blocks:
-            x = blk(x)
-        x = self.ln_f(x)
+        if len(self.blocks) and _FUSED_LN:
+            # residual stream with each LayerNorm fused into the residual update before it
+            xn = self.blocks[0].ln_1(x)
+            for i, blk in enumerate(self.blocks):
+                nxt = self.blocks[i + 1].ln_1 if i + 1 < len(self.blocks) else self.ln_f
+                x, xn = blk.forward_fused(x, xn, nxt)
+            x = xn
+        else:
+            for blk in self.blocks:
+                x = blk(x)
+            x = self.ln_f(x)
         logits = fops.fused_dense(x, self.wte.weight, None)
         if labels is None:
             return logits

@@ -351,6 +351,52 @@ def dense_bias_dropout_add_ln(x, weight, bias, residual, gamma, beta, p=0.0, eps
     return F.layer_norm(s, (s.shape[-1],), gamma, beta, eps)
 
 
+class _BDAPreLN(torch.autograd.Function):
+    """Pre-LN residual stream step (GPT): s = res + dropout(x + b) and y = LN(s), both outputs used
+    (s is the next residual, y the next sublayer's input). One bdaln kernel each way: the forward
+    writes s and y in one pass (no separate LayerNorm read of s), the backward adds the residual
+    stream's gradient of s (ds_extra) inside the LayerNorm backward instead of an autograd
+    accumulate pass over [tokens, hidden]."""
+
+    @staticmethod
+    def forward(ctx, x, b, res, gamma, beta, p, eps):
+        C = _ext.require()
+        seed, off = _seed(x.device) if p > 0 else (0, 0)
+        y, s, mean, rstd = C.bdaln_fwd(_2d(x).contiguous(), b, _2d(res).contiguous(), gamma, beta, float(eps),
+                                       float(p), seed, off)
+        ctx.save_for_backward(s, gamma, mean, rstd)
+        ctx.cfg = (p, seed, off, b is not None)
+        ctx.params = (b, gamma, beta)
+        ctx.shape = res.shape
+        return s.view(res.shape), y.view(res.shape)
+
+    @staticmethod
+    def backward(ctx, ds, dy):
+        C = _ext.require()
+        s, gamma, mean, rstd = ctx.saved_tensors
+        p, seed, off, has_b = ctx.cfg
+        pb, pg, pbeta = ctx.params
+        if dy is None:
+            dy = torch.zeros_like(s)
+        dres, dx, dg, dbeta, db = C.bdaln_bwd(_2d(dy), s, gamma, mean, rstd, float(p), seed, off, has_b,
+                                              dgamma_out=_gt(pg), dbeta_out=_gt(pbeta),
+                                              dbias_out=_gt(pb) if has_b else None,
+                                              ds_extra=_2d(ds) if ds is not None else None)
+        return (dx.view(ctx.shape), (db if has_b else None), dres.view(ctx.shape), dg, dbeta, None, None)
+
+
+def bias_dropout_add_ln(x, bias, residual, gamma, beta, p=0.0, eps=1e-5, training=True):
+    """(s, LayerNorm(s)) with s = residual + dropout(x + bias): a pre-LN block's residual update fused
+    with the next LayerNorm (GPT-2 / Megatron layer boundaries)."""
+    p = p if training else 0.0
+    if _native(x) and x.shape == residual.shape and _ext.require().bdaln_supported(x.shape[-1]) and \
+            gamma is not None and beta is not None:
+        return _BDAPreLN.apply(x, bias, residual, gamma, beta, float(p), float(eps))
+    t = x + bias if bias is not None else x
+    s = residual + (F.dropout(t, p, True) if p > 0 else t)
+    return s, F.layer_norm(s, (s.shape[-1],), gamma, beta, eps)
+
+
 class _BiasDropoutAdd(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, b, res, p):

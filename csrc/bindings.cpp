@@ -550,9 +550,15 @@ std::vector<Tensor> k_bdaln_fwd(Tensor x, const c10::optional<Tensor>& b, Tensor
 
 std::vector<Tensor> k_bdaln_bwd(Tensor dy, Tensor s, Tensor gamma, Tensor mean, Tensor rstd, double p,
                                 int64_t seed, int64_t offset, bool has_bias, const c10::optional<Tensor>& dgamma_out,
-                                const c10::optional<Tensor>& dbeta_out, const c10::optional<Tensor>& dbias_out) {
+                                const c10::optional<Tensor>& dbeta_out, const c10::optional<Tensor>& dbias_out,
+                                const c10::optional<Tensor>& ds_extra) {
   Tensor dyc = dy.contiguous();
   const int64_t cols = cols_of(s), rows = s.numel() / std::max<int64_t>(cols, 1);
+  Tensor dse;
+  if (ds_extra.has_value() && ds_extra->defined()) {
+    dse = ds_extra->contiguous();
+    TORCH_CHECK(dse.numel() == s.numel() && dse.scalar_type() == s.scalar_type(), "bdaln_bwd: ds_extra like s");
+  }
   Tensor dres = at::empty_like(s), dx = at::empty_like(s);
   Tensor dgamma = out_or_empty(dgamma_out, gamma.sizes(), gamma.options(), "bdaln_bwd dgamma");
   Tensor dbeta = out_or_empty(dbeta_out, gamma.sizes(), gamma.options(), "bdaln_bwd dbeta");
@@ -560,7 +566,8 @@ std::vector<Tensor> k_bdaln_bwd(Tensor dy, Tensor s, Tensor gamma, Tensor mean, 
   Tensor ws = at::empty({apex::bdaln_ws_floats(rows, (int)cols)}, s.options().dtype(at::kFloat));
   auto dp = drop_params(p);
   check(apex::bdaln_bwd(dyc.data_ptr(), s.data_ptr(), gamma.data_ptr(), mean.data_ptr<float>(),
-                        rstd.data_ptr<float>(), dres.data_ptr(), dx.data_ptr(), dgamma.data_ptr(),
+                        rstd.data_ptr<float>(), dse.defined() ? dse.data_ptr() : nullptr, dres.data_ptr(),
+                        dx.data_ptr(), dgamma.data_ptr(),
                         dbeta.data_ptr(), has_bias ? dbias.data_ptr() : nullptr, ws.data_ptr<float>(), rows,
                         (int)cols, (uint64_t)seed, (uint64_t)offset, dp.first, dp.second,
                         dt_code(s.scalar_type()), dt_code(gamma.scalar_type()), cur_stream()),
@@ -1258,7 +1265,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out") = py::none());
   m.def("bdaln_bwd", &k_bdaln_bwd, py::arg("dy"), py::arg("s"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"),
         py::arg("p"), py::arg("seed"), py::arg("offset"), py::arg("has_bias"), py::arg("dgamma_out") = py::none(),
-        py::arg("dbeta_out") = py::none(), py::arg("dbias_out") = py::none());
+        py::arg("dbeta_out") = py::none(), py::arg("dbias_out") = py::none(), py::arg("ds_extra") = py::none());
   m.def("input_normalize", &k_input_normalize);
   m.def("gemm_supported", &k_gemm_supported);
   m.def("gemm", &k_gemm, py::arg("a"), py::arg("b"), py::arg("epi") = 0, py::arg("bias") = py::none(),

@@ -12,6 +12,8 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <type_traits>
+
 namespace apex {
 
 constexpr int kEwBlock = 256;
@@ -273,11 +275,14 @@ __global__ void __launch_bounds__(kEwBlock) bdaln_fwd_kernel(const T* __restrict
 // loaded into registers (raw 16-byte packs) before the current row's reduction and stores, so every
 // wave keeps two rows of loads in flight — with one row per wave the kernel was latency-bound at
 // ~4.2 TB/s (rocprofv3 FETCH/WRITE_SIZE, profiles/r2_pmc_bw_kernels.json).
-template <typename T, typename W, int VPT, bool DROP>
+// EXTRA (pre-LN residual streams, GPT): s also feeds the next residual add, so its gradient is
+// LN_bwd(dy) + dse — dse is added here instead of by a separate autograd accumulate pass.
+template <typename T, typename W, int VPT, bool DROP, bool EXTRA = false>
 __global__ void __launch_bounds__(kEwBlock) bdaln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ s,
                                                             const W* __restrict__ gamma,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ rstd,
+                                                            const T* __restrict__ dse,
                                                             T* __restrict__ dres, T* __restrict__ dx,
                                                             float* __restrict__ part, int64_t rows, int cols,
                                                             int rows_per_wave, uint64_t seed,
@@ -298,7 +303,7 @@ __global__ void __launch_bounds__(kEwBlock) bdaln_bwd_kernel(const T* __restrict
   }
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_wave * 4;
   typedef Pack<T, 8> P8;
-  P8 ns[VPT], nd[VPT];
+  P8 ns[VPT], nd[VPT], ne[EXTRA ? VPT : 1];
   auto fetch = [&](int64_t row) {
 #pragma unroll
     for (int j = 0; j < VPT; ++j) {
@@ -306,6 +311,7 @@ __global__ void __launch_bounds__(kEwBlock) bdaln_bwd_kernel(const T* __restrict
       if (vi < nvec && row < rows) {
         ns[j] = *reinterpret_cast<const P8*>(s + row * cols + vi * 8);
         nd[j] = *reinterpret_cast<const P8*>(dy + row * cols + vi * 8);
+        if constexpr (EXTRA) ne[j] = *reinterpret_cast<const P8*>(dse + row * cols + vi * 8);
       }
     }
   };
@@ -313,13 +319,14 @@ __global__ void __launch_bounds__(kEwBlock) bdaln_bwd_kernel(const T* __restrict
   for (int rr = 0; rr < rows_per_wave; ++rr) {
     const int64_t row = r0 + (int64_t)rr * 4 + wid;
     if (row >= rows) break;
-    float xh[VPT][8], dv[VPT][8];
+    float xh[VPT][8], dv[VPT][8], ev[EXTRA ? VPT : 1][8];
 #pragma unroll
     for (int j = 0; j < VPT; ++j)
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         xh[j][k] = to_f(ns[j].v[k]);
         dv[j][k] = to_f(nd[j].v[k]);
+        if constexpr (EXTRA) ev[j][k] = to_f(ne[j].v[k]);
       }
     if (rr + 1 < rows_per_wave) fetch(row + 4);
     const float mu = mean[row], rs = rstd[row];
@@ -348,7 +355,10 @@ __global__ void __launch_bounds__(kEwBlock) bdaln_bwd_kernel(const T* __restrict
         const int64_t e = row * cols + vi * 8;
         float ds[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) ds[k] = rs * (dv[j][k] * g[j][k] - s1 - xh[j][k] * s2);
+        for (int k = 0; k < 8; ++k) {
+          ds[k] = rs * (dv[j][k] * g[j][k] - s1 - xh[j][k] * s2);
+          if constexpr (EXTRA) ds[k] += ev[j][k];
+        }
         store_f<T, 8>(dres + e, ds);
         bool keep[8];
         if (DROP) drop_mask8(seed, offset, e >> 3, thresh, keep);
@@ -814,23 +824,27 @@ int64_t bdaln_ws_floats(int64_t rows, int cols) {
 }
 
 int bdaln_bwd(const void* dy, const void* s_in, const void* gamma, const float* mean, const float* rstd,
-              void* dres, void* dx, void* dgamma, void* dbeta, void* dbias, float* ws, int64_t rows,
-              int cols, uint64_t seed, uint64_t offset, uint32_t thresh, float scale, int xdt, int wdt,
-              hipStream_t s) {
+              const void* dse, void* dres, void* dx, void* dgamma, void* dbeta, void* dbias, float* ws,
+              int64_t rows, int cols, uint64_t seed, uint64_t offset, uint32_t thresh, float scale, int xdt,
+              int wdt, hipStream_t s) {
   if (rows == 0) return 0;
   const int vpt = bdaln_vpt(cols);
   const int rpw = bdaln_rpw(rows);
   const int parts = (int)((rows + 4 * rpw - 1) / (4 * rpw));
   const size_t lds = (size_t)4 * 3 * cols * sizeof(float);
   EW_DISPATCH(xdt, T, EW_DISPATCH(wdt, W, EW_VPT(vpt, VPT, {
-    if (thresh)
-      hipLaunchKernelGGL((bdaln_bwd_kernel<T, W, VPT, true>), dim3(parts), dim3(kEwBlock), lds, s,
-                         (const T*)dy, (const T*)s_in, (const W*)gamma, mean, rstd, (T*)dres, (T*)dx, ws,
-                         rows, cols, rpw, seed, offset, thresh, scale);
-    else
-      hipLaunchKernelGGL((bdaln_bwd_kernel<T, W, VPT, false>), dim3(parts), dim3(kEwBlock), lds, s,
-                         (const T*)dy, (const T*)s_in, (const W*)gamma, mean, rstd, (T*)dres, (T*)dx, ws,
-                         rows, cols, rpw, seed, offset, thresh, scale);
+    auto launch = [&](auto drop_tag, auto extra_tag) {
+      hipLaunchKernelGGL((bdaln_bwd_kernel<T, W, VPT, decltype(drop_tag)::value, decltype(extra_tag)::value>),
+                         dim3(parts), dim3(kEwBlock), lds, s, (const T*)dy, (const T*)s_in, (const W*)gamma, mean,
+                         rstd, (const T*)dse, (T*)dres, (T*)dx, ws, rows, cols, rpw, seed, offset, thresh, scale);
+    };
+    if (thresh) {
+      if (dse) launch(std::true_type{}, std::true_type{});
+      else launch(std::true_type{}, std::false_type{});
+    } else {
+      if (dse) launch(std::false_type{}, std::true_type{});
+      else launch(std::false_type{}, std::false_type{});
+    }
     const int64_t ld = 3 * (int64_t)cols;
     launch_partial_colsum3<W>(ws, parts, ld, cols, (W*)dgamma, (W*)dbeta, (W*)dbias, s);
   })));

@@ -27,6 +27,23 @@ def test_gpt_tiny_loss_matches_reference():
     assert GPTConfig().padded_vocab == 50304
 
 
+def test_gpt_fused_prenorm_path_matches_per_block_cpu():
+    """GPTModel.forward's fused residual-stream path (forward_fused) against the per-block forward."""
+    from apex.models import GPTConfig, GPTModel
+
+    torch.manual_seed(0)
+    c = GPTConfig.tiny()
+    c.dropout = 0.0
+    m = GPTModel(c)
+    ids = torch.randint(0, c.vocab_size, (2, 16))
+    logits = m(ids)
+    x = m.wte(ids) + m.wpe(torch.arange(16))[None]
+    for blk in m.blocks:
+        x = blk(x)
+    ref = m.ln_f(x) @ m.wte.weight.t()
+    torch.testing.assert_close(logits, ref, rtol=1e-5, atol=1e-5)
+
+
 @pytest.mark.parametrize("cl", [False, True])
 def test_resnet_forward_backward(cl):
     from apex.models import resnet18, resnet50
