@@ -9,7 +9,10 @@ read-only at start-up, so no tuning happens inside a timed run. Shapes missing f
 use the library default.
 
 Regenerate (on an MI355X):  APEX_TUNABLEOP_TUNE=1 python bench.py --steps 3 --warmup 2
-then copy ``tuning/tunableop_results0.csv`` to ordinals 1..7.
+then copy ``tuning/tunableop_results0.csv`` to ordinals 1..7. The file also holds the GPT-2 1.5B
+and Megatron GPT (micro-batch 4 x 2048) shapes, tuned over hipBLASLt by tools/gpu_tune_one.sh
+and merged (profiles/r2_tunableop_models_ab.jsonl: GPT-2 72.3k -> 77.2k tokens/s, Megatron
+45.5k -> 46.7k, same box).
 """
 from __future__ import annotations
 
