@@ -9,7 +9,7 @@ export PYTHONUNBUFFERED=1
 cp ${START:-tuning/tunableop_results0.csv} $O/tune/tunableop_results0.csv
 ( while true; do sleep 30; echo "tick $(date +%s) $(wc -l < $O/tune/tunableop_results0.csv)"; done ) &
 TICK=$!
-PYTORCH_TUNABLEOP_FILENAME=$PWD/$O/tune/tunableop_results%d.csv APEX_TUNABLEOP_TUNE=1 PYTORCH_TUNABLEOP_ROCBLAS_ENABLED=0 \
+PYTORCH_TUNABLEOP_FILENAME=$PWD/$O/tune/tunableop_results%d.csv APEX_TUNABLEOP_TUNE=1 PYTORCH_TUNABLEOP_ROCBLAS_ENABLED=${ROCBLAS:-0} \
   timeout -k 10 ${TLIM:-1000} python $BENCH > $O/tune.json 2> $O/tune.err
 rc=$?
 kill $TICK
