@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import contextlib
 import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -26,6 +27,9 @@ from ..ops import fused as fops
 from ..transformer import parallel_state as ps
 from ..transformer import tensor_parallel as tp
 
+
+# APEX_MEGATRON_FUSED_LN=0: per-layer forward (separate LayerNorms; A/B and fallback switch)
+_FUSED_LN = os.environ.get("APEX_MEGATRON_FUSED_LN", "1") != "0"
 
 @dataclass
 class MegatronGPTConfig:
@@ -107,6 +111,35 @@ class ParallelTransformerLayer(nn.Module):
         out, bias = f2(h)
         return fops.bias_dropout_add(out, bias, x, ph)
 
+    def forward_fused(self, x, xn, nxt):
+        """forward() with each residual update fused with the LayerNorm after it (one bdaln kernel
+        each way, fops.bias_dropout_add_ln): takes x and xn = input_layernorm(x), returns
+        (x', nxt(x')) with nxt the next layer's input_layernorm / the final LayerNorm, or (x', None)
+        at a pipeline-stage boundary (the next stage normalises its own input)."""
+        B, S, _ = x.shape
+        ph = self.p_hidden if self.training else 0.0
+        pa = self.p_attn if self.training else 0.0
+        qkv, _ = self.query_key_value(xn)
+        qkv = qkv.view(B, S, 3, self.heads_local, self.d)
+        with _tp_rng():
+            ctx = fops.attention_qkv_packed(qkv, None, pa, causal=True)
+        out, bias = self.dense(ctx.reshape(B, S, -1))
+        ln2 = self.post_attention_layernorm
+        x, xn = fops.bias_dropout_add_ln(out, bias, x, ln2.weight, ln2.bias, ph, ln2.eps)
+        f1, f2 = self.dense_h_to_4h, self.dense_4h_to_h
+        t = bias2 = None
+        if not (f1.sequence_parallel_enabled or f2.sequence_parallel_enabled) and f1.bias is not None:
+            t = fblocks.mlp(tp.copy_to_tensor_model_parallel_region(xn), f1.weight, f1.bias, f2.weight)
+            if t is not None:
+                t, bias2 = tp.reduce_from_tensor_model_parallel_region(t), f2.bias
+        if t is None:
+            h, b1 = f1(xn)
+            h = fops.bias_gelu(h, b1) if b1 is not None else F.gelu(h)
+            t, bias2 = f2(h)
+        if nxt is None:
+            return fops.bias_dropout_add(t, bias2, x, ph), None
+        return fops.bias_dropout_add_ln(t, bias2, x, nxt.weight, nxt.bias, ph, nxt.eps)
+
 
 class MegatronGPT(nn.Module):
     """One pipeline stage of the GPT (pre_process: embeddings, post_process: head + loss)."""
@@ -148,11 +181,25 @@ class MegatronGPT(nn.Module):
             x = F.dropout(x, self.config.hidden_dropout, self.training)
         else:
             x = self.input_tensor
+        if _FUSED_LN and len(self.layers):
+            # residual stream with each LayerNorm fused into the residual update before it
+            xn = self.layers[0].input_layernorm(x)
+            for i, layer in enumerate(self.layers):
+                if i + 1 < len(self.layers):
+                    nxt = self.layers[i + 1].input_layernorm
+                else:
+                    nxt = self.final_layernorm if self.post_process else None
+                x, xn = layer.forward_fused(x, xn, nxt)
+            if self.post_process:
+                return self._head(xn, labels)
+            return x
         for layer in self.layers:
             x = layer(x)
         if not self.post_process:
             return x
-        x = self.final_layernorm(x)
+        return self._head(self.final_layernorm(x), labels)
+
+    def _head(self, x, labels):
         logits = fops.fused_dense(tp.copy_to_tensor_model_parallel_region(x), self.word_embeddings.weight, None)
         if labels is None:
             return logits

@@ -389,8 +389,8 @@ def bias_dropout_add_ln(x, bias, residual, gamma, beta, p=0.0, eps=1e-5, trainin
     """(s, LayerNorm(s)) with s = residual + dropout(x + bias): a pre-LN block's residual update fused
     with the next LayerNorm (GPT-2 / Megatron layer boundaries)."""
     p = p if training else 0.0
-    if _native(x) and x.shape == residual.shape and _ext.require().bdaln_supported(x.shape[-1]) and \
-            gamma is not None and beta is not None:
+    if _native(x) and x.shape == residual.shape and gamma is not None and beta is not None and \
+            (_ext.require().bdaln_supported(x.shape[-1]) or _ext.require().bdaln_wide_supported(x.shape[-1])):
         return _BDAPreLN.apply(x, bias, residual, gamma, beta, float(p), float(eps))
     t = x + bias if bias is not None else x
     s = residual + (F.dropout(t, p, True) if p > 0 else t)

@@ -531,6 +531,7 @@ Tensor k_splitk_reduce(Tensor slabs, at::ScalarType out_dtype, const c10::option
 }
 
 bool k_bdaln_supported(int64_t cols) { return apex::bdaln_supported((int)cols) != 0; }
+bool k_bdaln_wide_supported(int64_t cols) { return apex::bdaln_wide_supported((int)cols) != 0; }
 
 std::vector<Tensor> k_bdaln_fwd(Tensor x, const c10::optional<Tensor>& b, Tensor res, Tensor gamma,
                                 Tensor beta, double eps, double p, int64_t seed, int64_t offset) {
@@ -1255,6 +1256,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("colsum", &k_colsum, py::arg("x"), py::arg("out_dtype"), py::arg("out") = py::none());
   m.def("splitk_reduce", &k_splitk_reduce, py::arg("slabs"), py::arg("out_dtype"), py::arg("out") = py::none());
   m.def("bdaln_supported", &k_bdaln_supported);
+  m.def("bdaln_wide_supported", &k_bdaln_wide_supported);
   m.def("bdaln_fwd", &k_bdaln_fwd);
   m.def("embed_ln_fwd", &k_embed_ln_fwd);
   m.def("embed_ln_bwd", &k_embed_ln_bwd, py::arg("dy"), py::arg("s"), py::arg("gamma"), py::arg("mean"),

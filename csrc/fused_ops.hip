@@ -390,6 +390,104 @@ __global__ void __launch_bounds__(kEwBlock) bdaln_bwd_kernel(const T* __restrict
     out[c] = lds[c] + lds[3 * cols + c] + lds[6 * cols + c] + lds[9 * cols + c];
 }
 
+// Wide rows (2056..4096 cols, VPT 5..8 vectors per lane: Megatron H = 2560): the fast kernel's
+// register-resident rows + gamma + three partial rows would spill, so this variant keeps only the
+// dgamma / dbeta / dbias partials in registers and reads each row twice (second pass from L1/L2;
+// a row is 5-8 KB), gamma from cache; the partials combine through LDS one third at a time
+// ([4 waves][cols] floats <= 64 KB). Same ws layout as bdaln_bwd_kernel.
+template <typename T, typename W, int VPT, bool DROP, bool EXTRA>
+__global__ void __launch_bounds__(kEwBlock) bdaln_bwd_wide_kernel(const T* __restrict__ dy, const T* __restrict__ s,
+                                                                 const W* __restrict__ gamma,
+                                                                 const float* __restrict__ mean,
+                                                                 const float* __restrict__ rstd,
+                                                                 const T* __restrict__ dse, T* __restrict__ dres,
+                                                                 T* __restrict__ dx, float* __restrict__ part,
+                                                                 int64_t rows, int cols, int rows_per_wave,
+                                                                 uint64_t seed, uint64_t offset, uint32_t thresh,
+                                                                 float scale) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // [4][cols]
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nvec = cols >> 3;
+  const float inv_n = 1.f / (float)cols;
+  float dg[VPT][8], dbt[VPT][8], dbi[VPT][8];
+#pragma unroll
+  for (int j = 0; j < VPT; ++j)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dg[j][k] = dbt[j][k] = dbi[j][k] = 0.f;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_wave * 4;
+  for (int rr = 0; rr < rows_per_wave; ++rr) {
+    const int64_t row = r0 + (int64_t)rr * 4 + wid;
+    if (row >= rows) break;
+    const float mu = mean[row], rs = rstd[row];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int vi = j * 64 + lane;
+      if (vi < nvec) {
+        const int64_t e = row * cols + vi * 8;
+        float xv[8], dv[8], g[8];
+        load_f<T, 8>(s + e, xv);
+        load_f<T, 8>(dy + e, dv);
+        load_f<W, 8>(gamma + vi * 8, g);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float xh = (xv[k] - mu) * rs;
+          const float dyg = dv[k] * g[k];
+          s1 += dyg;
+          s2 += dyg * xh;
+          dg[j][k] += dv[k] * xh;
+          dbt[j][k] += dv[k];
+        }
+      }
+    }
+    s1 = wave_sum(s1) * inv_n;
+    s2 = wave_sum(s2) * inv_n;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int vi = j * 64 + lane;
+      if (vi < nvec) {
+        const int64_t e = row * cols + vi * 8;
+        float xv[8], dv[8], g[8], ev[8], ds[8];
+        load_f<T, 8>(s + e, xv);
+        load_f<T, 8>(dy + e, dv);
+        load_f<W, 8>(gamma + vi * 8, g);
+        if constexpr (EXTRA) load_f<T, 8>(dse + e, ev);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          ds[k] = rs * (dv[k] * g[k] - s1 - (xv[k] - mu) * rs * s2);
+          if constexpr (EXTRA) ds[k] += ev[k];
+        }
+        store_f<T, 8>(dres + e, ds);
+        bool keep[8];
+        if (DROP) drop_mask8(seed, offset, e >> 3, thresh, keep);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          if (DROP) ds[k] = keep[k] ? ds[k] * scale : 0.f;
+          dbi[j][k] += ds[k];
+        }
+        store_f<T, 8>(dx + e, ds);
+      }
+    }
+  }
+  float* mine = lds + wid * cols;
+  float* out = part + (int64_t)blockIdx.x * 3 * cols;
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    if (t) __syncthreads();
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int vi = j * 64 + lane;
+      if (vi < nvec) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) mine[vi * 8 + k] = t == 0 ? dg[j][k] : t == 1 ? dbt[j][k] : dbi[j][k];
+      }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < cols; c += kEwBlock)
+      out[t * cols + c] = lds[c] + lds[cols + c] + lds[2 * cols + c] + lds[3 * cols + c];
+  }
+}
+
 // ------------------------- BERT embeddings (gather-sum + LayerNorm + dropout) -------------
 // forward, one wave per token row (row = b*S + pos):
 //   s = Ww[id] + Wp[pos] + Wt[type]; y = dropout(LN(s))     (s stored for the backward)
@@ -783,6 +881,23 @@ static inline int bdaln_vpt(int cols) {
 
 int bdaln_supported(int cols) { return bdaln_vpt(cols) > 0; }
 
+// 2056..4096 columns: forward with 5..8 vectors per lane, backward through bdaln_bwd_wide_kernel
+static inline int bdaln_wide_vpt(int cols) {
+  if (cols % 8) return 0;
+  const int nvec = cols / 8;
+  return (nvec > 256 && nvec <= 512) ? (nvec + 63) / 64 : 0;
+}
+int bdaln_wide_supported(int cols) { return bdaln_wide_vpt(cols) > 0; }
+
+#define EW_VPT_WIDE(V, VPT, ...)                            \
+  switch (V) {                                              \
+    case 5: { constexpr int VPT = 5; __VA_ARGS__; } break;  \
+    case 6: { constexpr int VPT = 6; __VA_ARGS__; } break;  \
+    case 7: { constexpr int VPT = 7; __VA_ARGS__; } break;  \
+    case 8: { constexpr int VPT = 8; __VA_ARGS__; } break;  \
+    default: return -2;                                     \
+  }
+
 #define EW_VPT(V, VPT, ...)                                 \
   switch (V) {                                              \
     case 1: { constexpr int VPT = 1; __VA_ARGS__; } break;  \
@@ -797,6 +912,20 @@ int bdaln_fwd(const void* x, const void* b, const void* res, const void* gamma, 
   if (rows == 0) return 0;
   const int vpt = bdaln_vpt(cols);
   const dim3 grid((unsigned)((rows + 3) / 4));
+  if (!vpt) {
+    const int wv = bdaln_wide_vpt(cols);
+    EW_DISPATCH(xdt, T, EW_DISPATCH(wdt, W, EW_VPT_WIDE(wv, VPT, {
+      if (thresh)
+        hipLaunchKernelGGL((bdaln_fwd_kernel<T, W, VPT, true>), grid, dim3(kEwBlock), 0, s, (const T*)x,
+                           (const W*)b, (const T*)res, (const W*)gamma, (const W*)beta, (T*)y, (T*)s_out,
+                           mean, rstd, rows, cols, eps, seed, offset, thresh, scale);
+      else
+        hipLaunchKernelGGL((bdaln_fwd_kernel<T, W, VPT, false>), grid, dim3(kEwBlock), 0, s, (const T*)x,
+                           (const W*)b, (const T*)res, (const W*)gamma, (const W*)beta, (T*)y, (T*)s_out,
+                           mean, rstd, rows, cols, eps, seed, offset, thresh, scale);
+    })));
+    return (int)hipGetLastError();
+  }
   EW_DISPATCH(xdt, T, EW_DISPATCH(wdt, W, EW_VPT(vpt, VPT, {
     if (thresh)
       hipLaunchKernelGGL((bdaln_fwd_kernel<T, W, VPT, true>), grid, dim3(kEwBlock), 0, s, (const T*)x,
@@ -831,6 +960,27 @@ int bdaln_bwd(const void* dy, const void* s_in, const void* gamma, const float* 
   const int vpt = bdaln_vpt(cols);
   const int rpw = bdaln_rpw(rows);
   const int parts = (int)((rows + 4 * rpw - 1) / (4 * rpw));
+  if (!vpt) {
+    const int wv = bdaln_wide_vpt(cols);
+    const size_t wlds = (size_t)4 * cols * sizeof(float);
+    EW_DISPATCH(xdt, T, EW_DISPATCH(wdt, W, EW_VPT_WIDE(wv, VPT, {
+      auto launch = [&](auto drop_tag, auto extra_tag) {
+        hipLaunchKernelGGL((bdaln_bwd_wide_kernel<T, W, VPT, decltype(drop_tag)::value, decltype(extra_tag)::value>),
+                           dim3(parts), dim3(kEwBlock), wlds, s, (const T*)dy, (const T*)s_in, (const W*)gamma,
+                           mean, rstd, (const T*)dse, (T*)dres, (T*)dx, ws, rows, cols, rpw, seed, offset, thresh,
+                           scale);
+      };
+      if (thresh) {
+        if (dse) launch(std::true_type{}, std::true_type{});
+        else launch(std::true_type{}, std::false_type{});
+      } else {
+        if (dse) launch(std::false_type{}, std::true_type{});
+        else launch(std::false_type{}, std::false_type{});
+      }
+      launch_partial_colsum3<W>(ws, parts, 3 * (int64_t)cols, cols, (W*)dgamma, (W*)dbeta, (W*)dbias, s);
+    })));
+    return (int)hipGetLastError();
+  }
   const size_t lds = (size_t)4 * 3 * cols * sizeof(float);
   EW_DISPATCH(xdt, T, EW_DISPATCH(wdt, W, EW_VPT(vpt, VPT, {
     auto launch = [&](auto drop_tag, auto extra_tag) {

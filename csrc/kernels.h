@@ -132,6 +132,7 @@ int colsum(const void* x, void* out, float* ws, int64_t rows, int cols, int xdt,
 int splitk_reduce(const float* slabs, void* out, int64_t n, int nsplit, int odt, hipStream_t s);
 int64_t colsum_parts(int64_t rows);
 int bdaln_supported(int cols);
+int bdaln_wide_supported(int cols);  // 2056..4096 columns (bdaln fwd/bwd only, not the embedding block)
 int bdaln_fwd(const void* x, const void* b, const void* res, const void* gamma, const void* beta, void* y,
               void* s_out, float* mean, float* rstd, int64_t rows, int cols, float eps, uint64_t seed,
               uint64_t offset, uint32_t thresh, float scale, int xdt, int wdt, hipStream_t s);
