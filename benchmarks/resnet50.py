@@ -26,7 +26,12 @@ def main():
     ap.add_argument("--no-syncbn", action="store_true")
     ap.add_argument("--nchw", action="store_true", help="keep NCHW activations")
     ap.add_argument("--fp32", action="store_true")
+    ap.add_argument("--conv-search", action="store_true",
+                    help="MIOpen Find (time every conv algorithm per shape in warmup) instead of immediate mode")
     args = ap.parse_args()
+    # measured (profiles/r2_resnet50_conv_search_ab.json): the search gains nothing over MIOpen's
+    # immediate-mode choice at this configuration (5775 vs 5816 img/s) and costs minutes of warmup
+    torch.backends.cudnn.benchmark = args.conv_search
 
     from apex.utils.bench import emit, finish, init_distributed, instrumented_steps
 
