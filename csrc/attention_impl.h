@@ -215,9 +215,9 @@ attn_fwd_kernel(AttnArgs a) {
   // wid through readfirstlane: wave-uniform in SGPRs, so tile-level conditions become scalar branches
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 31, hl = lane >> 5;
-  const int bh = blockIdx.y;
+  const int bh = blockIdx.x;  // grid (B*H, query blocks): see attn_fwd_impl
   const int b = bh / a.H, h = bh % a.H;
-  const int q0 = blockIdx.x * kFwdBQ;
+  const int q0 = (CAUSAL ? gridDim.y - 1 - blockIdx.y : blockIdx.y) * kFwdBQ;
   const int qrow = q0 + 32 * wid + r;
   const int Sk = a.k_lens ? min(a.k_lens[b], a.Sk) : a.Sk;
   // BIAS: scores are taken to the natural domain s' = s * scale + bias, so the exp2 factor is log2(e)
@@ -547,9 +547,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
   // wid through readfirstlane: wave-uniform in SGPRs, so tile-level conditions become scalar branches
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 31, hl = lane >> 5;
-  const int bh = blockIdx.y;
+  const int bh = blockIdx.x;  // grid (B*H, key blocks): key block 0 (the most queries when causal) first
   const int b = bh / a.H, h = bh % a.H;
-  const int k0 = blockIdx.x * kBwdBK;
+  const int k0 = blockIdx.y * kBwdBK;
   const int Sk = a.k_lens ? min(a.k_lens[b], a.Sk) : a.Sk;
   const int mykey = k0 + 32 * wid + r;  // key row this lane holds as K/V operand
 
@@ -918,9 +918,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
   // wid through readfirstlane: wave-uniform in SGPRs, so tile-level conditions become scalar branches
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 31, hl = lane >> 5;
-  const int bh = blockIdx.y;
+  const int bh = blockIdx.x;  // grid (B*H, query blocks), heaviest (causal: last) query blocks first
   const int b = bh / a.H, h = bh % a.H;
-  const int q0 = blockIdx.x * kFwdBQ;
+  const int q0 = (CAUSAL ? gridDim.y - 1 - blockIdx.y : blockIdx.y) * kFwdBQ;
   const int qrow = q0 + 32 * wid + r;
   const int Sk = a.k_lens ? min(a.k_lens[b], a.Sk) : a.Sk;
 
@@ -1149,7 +1149,10 @@ inline bool attn_fwd_db() {
 
 template <int D>
 int attn_fwd_impl(const AttnArgs& a, int dt, hipStream_t s) {
-  dim3 grid((a.Sq + kFwdBQ - 1) / kFwdBQ, a.B * a.H);
+  // grid (B*H, query blocks), dispatched x-fastest: every head's block of one query range goes out
+  // together, and with a causal mask the heaviest ranges (the last query blocks, which see the most
+  // keys) go first, so the short blocks fill the tail (longest-first list scheduling)
+  dim3 grid(a.B * a.H, (a.Sq + kFwdBQ - 1) / kFwdBQ);
   const bool drop = a.drop_thresh > 0;
   // SHORT: single LDS stage (k_lens <= Sk). Without dropout only: measured at the BERT shape
   // (tools/attn_bench.py, b256 s128 h16) p = 0 fwd 61.1 -> 56.1 us, but p = 0.1 72.7 -> 73.8 us:
@@ -1184,8 +1187,9 @@ int attn_bwd_impl(const AttnArgs& a, const void* dout, float* delta_ws, void* dk
   const bool multi = a.Sk > kBwdBK;
   if (multi && !delta_ws) return -4;
   if (a.bias && a.dsum) return -5;  // (not instantiated: the packed-QKV bias-grad fusion runs without a score bias)
-  dim3 grid((a.Sk + kBwdBK - 1) / kBwdBK, a.B * a.H);
-  dim3 qgrid((a.Sq + kFwdBQ - 1) / kFwdBQ, a.B * a.H);
+  // (B*H, blocks) grids, heaviest blocks first under a causal mask (see attn_fwd_impl)
+  dim3 grid(a.B * a.H, (a.Sk + kBwdBK - 1) / kBwdBK);
+  dim3 qgrid(a.B * a.H, (a.Sq + kFwdBQ - 1) / kFwdBQ);
   if (multi) {
     dim3 dgrid((a.Sq * (D / 8) + 255) / 256, a.B * a.H);
     ATTN_DISPATCH(dt, T, hipLaunchKernelGGL((attn_bwd_delta_kernel<T, D>), dgrid, dim3(256), 0, s, a, dout, delta_ws));
