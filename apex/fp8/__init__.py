@@ -79,6 +79,8 @@ class Fp8State:
 
     def __init__(self, recipe: Fp8Recipe | None = None, device=None):
         self.recipe = recipe or Fp8Recipe()
+        self._next_key = 0
+        self._free: list = []  # slot indices released by dead tensors, reused lowest first
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
         self.device = torch.device(device)
@@ -109,13 +111,48 @@ class Fp8State:
             setattr(self, k, t)
         self._cap = cap
 
+    def key_of(self, w) -> int:
+        """Stable slot key of a weight tensor: a counter stored on the tensor at first sight (not
+        ``id(w)``, which CPython recycles — a new tensor would inherit a dead one's scale history).
+        When the tensor dies its slots return to a free list; replicas that run the same forward
+        allocate and release in the same order, so slot i is the same role on every rank of the
+        amax reduction group. A weight re-created every step (an O1 cast) thus reuses its slots
+        instead of growing the buffers without bound."""
+        k = getattr(w, "_apex_fp8_key", None)
+        if k is None or k[0] is not self:
+            k = (self, self._next_key)
+            self._next_key += 1
+            w._apex_fp8_key = k
+            weakref.finalize(w, Fp8State._release, weakref.ref(self), k[1])
+        return k[1]
+
+    @staticmethod
+    def _release(ref, key):
+        st = ref()
+        if st is None:
+            return
+        for role in ("w", "x", "dy"):
+            s = st.slots.pop((key, role), None)
+            if s is not None:
+                st._fresh.discard(s)
+                st._free.append(s)
+        st._wcache.pop(key, None)
+
     def slot(self, key, fmt) -> int:
         s = self.slots.get(key)
         if s is None:
-            if self.n == self._cap:
-                self._grow(2 * self._cap)
-            s = self.n
-            self.n += 1
+            if self._free:
+                self._free.sort()
+                s = self._free.pop(0)
+                self.hist[s].zero_()
+                self.amax[s] = 0.0
+                self.scale[s] = 1.0
+                self.scale_inv[s] = 1.0
+            else:
+                if self.n == self._cap:
+                    self._grow(2 * self._cap)
+                s = self.n
+                self.n += 1
             self.slots[key] = s
             self.fmax[s] = FMT_MAX[fmt]
             self._fresh.add(s)
@@ -148,14 +185,15 @@ class Fp8State:
         return y, self._view("scale_inv", s)
 
     def _weight_entry(self, w):
-        e = self._wcache.get(id(w))
+        k = self.key_of(w)
+        e = self._wcache.get(k)
         if e is not None and e[0]() is w and e[1] == self.gen:
             return e
-        s = self.slot((id(w), "w"), self._fwd)
+        s = self.slot((k, "w"), self._fwd)
         self._fresh.discard(s)
         w8 = self._current(w.detach().contiguous(), s, self._fwd)
         e = [weakref.ref(w), self.gen, s, w8, None]
-        self._wcache[id(w)] = e
+        self._wcache[k] = e
         return e
 
     def weight(self, w):
@@ -187,7 +225,7 @@ class Fp8State:
         """a [M, K] @ w[N, K]^T with epilogue ``epi`` on the fp8 kernel -> (out, extra) or None."""
         if not self._fits(a, w, bias, aux, w.shape[1], w.shape[0]):
             return None
-        a8, ia = self.quantize(a, (id(w), "x"), self._fwd)
+        a8, ia = self.quantize(a, (self.key_of(w), "x"), self._fwd)
         w8, iw = self.weight(w)
         return _C().gemm_f8(a8, w8, ia, iw, self._fwd, epi, bias, aux, None, a.dtype)
 
@@ -195,7 +233,7 @@ class Fp8State:
         """dy [M, N] @ w[N, K] with epilogue ``epi`` (dy e5m2 x W^T e4m3) -> (out, extra) or None."""
         if not self._fits(dy, w, None, aux, w.shape[0], w.shape[1]):
             return None
-        d8, id_ = self.quantize(dy, (id(w), "dy"), self._bwd)
+        d8, id_ = self.quantize(dy, (self.key_of(w), "dy"), self._bwd)
         wt8, iw = self.weight_t(w)
         return _C().gemm_f8(d8, wt8, id_, iw, self._bwd, epi, None, aux, bias_grad_dtype, dy.dtype)
 
@@ -211,19 +249,49 @@ class Fp8State:
             return
         r = self.recipe
         if r.reduce_amax and torch.distributed.is_available() and torch.distributed.is_initialized():
-            g = r.amax_reduction_group
+            g = self.reduction_group()
             if torch.distributed.get_world_size(g) > 1:
-                torch.distributed.all_reduce(self.amax[: self.n], op=torch.distributed.ReduceOp.MAX, group=g)
+                self._reduce_amax(g)
         _C().fp8_update_scales(self.hist, self.amax, self.scale, self.scale_inv, self.fmax, self.n, self.idx,
                                self.smax_scale)
         self.idx = (self.idx + 1) % r.amax_history_len
+
+    def reduction_group(self):
+        """``recipe.amax_reduction_group``, else the data-parallel group when apex.transformer's
+        model parallelism is initialised (pipeline stages hold different layers and tensor-parallel
+        ranks different shards: a WORLD reduction would max unrelated slots together), else WORLD."""
+        if self.recipe.amax_reduction_group is not None:
+            return self.recipe.amax_reduction_group
+        try:
+            from ..transformer import parallel_state as ps
+
+            if ps.model_parallel_is_initialized():
+                return ps.get_data_parallel_group()
+        except ImportError:  # pragma: no cover
+            pass
+        return None
+
+    def _reduce_amax(self, g):
+        """MAX all-reduce of this step's amaxes. During the first three steps the slot counts are
+        compared first (a 2-element MAX of (n, -n); a host sync that costs nothing there): ranks
+        whose slots differ would otherwise hang in, or silently cross-wire, the amax reduction."""
+        n = self.n
+        if self.steps <= 3:
+            t = torch.tensor([float(n), -float(n)], device=self.amax.device)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX, group=g)
+            hi, lo = float(t[0]), -float(t[1])
+            if hi != n or lo != n:
+                raise RuntimeError(f"fp8 amax reduction: slot counts differ across the group ({lo:g}..{hi:g}); "
+                                   "set Fp8Recipe.amax_reduction_group to a group whose ranks run the same layers")
+        torch.distributed.all_reduce(self.amax[:n], op=torch.distributed.ReduceOp.MAX, group=g)
 
     # ------------------------------------------------------------------ checkpoint
     def state_dict(self, model=None):
         """Scaling state by parameter name (``model`` given) — restorable in another process."""
         out = {"idx": self.idx, "steps": self.steps, "recipe": dataclasses.asdict(
             dataclasses.replace(self.recipe, amax_reduction_group=None)), "slots": {}}
-        names = {id(p): n for n, p in model.named_parameters()} if model is not None else {}
+        names = {getattr(p, "_apex_fp8_key", (None, None))[1]: n for n, p in model.named_parameters()
+                 if getattr(p, "_apex_fp8_key", (None,))[0] is self} if model is not None else {}
         for (pid, role), s in self.slots.items():
             name = names.get(pid)
             if model is not None and name is None:
@@ -242,7 +310,7 @@ class Fp8State:
             if name not in params:
                 continue
             fmt = E4M3 if v["fmax"] == FMT_MAX[E4M3] else E5M2
-            s = self.slot((id(params[name]), role), fmt)
+            s = self.slot((self.key_of(params[name]), role), fmt)
             self.hist[s].copy_(v["hist"])
             self.scale[s] = v["scale"]
             self.scale_inv[s] = v["scale_inv"]

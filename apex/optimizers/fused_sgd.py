@@ -68,3 +68,9 @@ class FusedSGD(FusedOptimizerBase):
                                         group["nesterov"], first_run, self.wd_after_momentum,
                                         scale_t if scale_t is not None else scale_f)
         return loss
+
+    def load_state_dict(self, state_dict):
+        # the loaded momentum buffers are the state now: a first-run flag left at 1 by an
+        # overflow-skipped first step would make the next step treat them as absent (buf = g)
+        super().load_state_dict(state_dict)
+        self._first_run_flags = {}

@@ -215,6 +215,36 @@ def grad_target(p):
     return flat.narrow(0, off, n).view(p.shape)
 
 
+def _lane_groups(process_group, k, backend):
+    """k communicators ("lanes") over the ranks of ``process_group``.
+
+    ``dist.new_group`` is collective over the DEFAULT group: every process must call it for every
+    group, with the same rank lists in the same order, or group names / store keys collide (a hang,
+    or communicators wired across the wrong ranks). With a subgroup (e.g. the data-parallel group
+    under TP/PP) each rank knows only its own group, so the rank lists of all groups are first
+    exchanged over the default group (every rank constructs its DDP at the same point, as with any
+    collective setup) and every rank then creates the k lanes of EVERY group, in sorted order,
+    keeping its own.
+    """
+    world = dist.get_world_size()
+    if process_group is None:
+        return [dist.new_group(ranks=list(range(world)), backend=backend) for _ in range(k)]
+    mine = tuple(dist.get_process_group_ranks(process_group))
+    allg = [None] * world
+    dist.all_gather_object(allg, mine)
+    groups = sorted(set(tuple(g) for g in allg))
+    covered = sorted(r for g in groups for r in g)
+    if covered != list(range(world)):
+        raise ValueError("num_allreduce_streams > 1 with a process_group needs disjoint groups covering "
+                         "every rank; pass allreduce_communicators instead")
+    lanes = None
+    for g in groups:
+        made = [dist.new_group(ranks=list(g), backend=backend) for _ in range(k)]
+        if g == mine:
+            lanes = made
+    return lanes
+
+
 class DistributedDataParallel(Module):
     """Bucketed, backward-overlapped data parallelism over RCCL.
 
@@ -284,9 +314,7 @@ class DistributedDataParallel(Module):
         if allreduce_communicators is not None:
             self._groups = list(allreduce_communicators)
         elif num_allreduce_streams > 1:
-            ranks = dist.get_process_group_ranks(process_group) if process_group is not None else \
-                list(range(dist.get_world_size()))
-            self._groups = [dist.new_group(ranks=ranks, backend=backend) for _ in range(num_allreduce_streams)]
+            self._groups = _lane_groups(process_group, num_allreduce_streams, backend)
         else:
             self._groups = [process_group]
         self.num_allreduce_streams = len(self._groups)
@@ -403,6 +431,12 @@ class DistributedDataParallel(Module):
             else:
                 self._ensure_view(idx, p)
             return
+        if self._trigger is not None and self._trigger_seen == len(self._trigger):
+            # every bucket is already on the wire: writing this gradient into its slot would race
+            # with the collective and the value would never be reduced (replicas diverge)
+            raise RuntimeError("allreduce_trigger_params: a gradient arrived after the trigger params fired "
+                               "the all-reduce; the trigger params must be the LAST to receive gradients in "
+                               "backward (e.g. the first layer's weight)")
         self._ensure_view(idx, p)
         if self._trigger is not None:
             if idx in self._trigger:

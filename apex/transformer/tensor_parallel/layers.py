@@ -68,11 +68,18 @@ def copy_tensor_model_parallel_attributes(destination, source):
 
 
 def _initialize_affine_weight(weight, output_size, input_size, per_partition_size, partition_dim,
-                              init_method, stride=1, return_master_weight=False, params_dtype=torch.float32):
+                              init_method, stride=1, return_master_weight=False, params_dtype=torch.float32,
+                              use_cpu_initialization=True):
     """Initialise the FULL weight identically on every rank (seeded), keep this rank's slice:
-    results are independent of the TP degree (so TP runs match single-GPU runs)."""
+    results are independent of the TP degree (so TP runs match single-GPU runs).
+
+    ``use_cpu_initialization``: the fp32 master is generated on the host (torch's CPU generator,
+    bit-identical across machines); otherwise on the weight's device when that is a GPU (its seeded
+    device generator — no host-memory copy of the full matrix, which for a 50k x 8k embedding is
+    1.6 GB per rank)."""
     set_tensor_model_parallel_attributes(weight, True, partition_dim, stride)
-    master = torch.empty(output_size, input_size, dtype=torch.float32, requires_grad=False)
+    dev = weight.device if (not use_cpu_initialization and weight.device.type == "cuda") else torch.device("cpu")
+    master = torch.empty(output_size, input_size, dtype=torch.float32, requires_grad=False, device=dev)
     init_method(master)
     master = master.to(params_dtype)
     per_stride = divide(per_partition_size, stride)
@@ -85,9 +92,16 @@ def _initialize_affine_weight(weight, output_size, input_size, per_partition_siz
     return master if return_master_weight else None
 
 
-def _accumulate_main_grad(weight, dy2, x2):
-    """weight.main_grad (fp32) += dy2^T x2 without materialising a low-precision dW."""
+def _accumulate_main_grad(weight, dy2, x2, in_fp16=False):
+    """weight.main_grad += dy2^T x2 without materialising a separate dW: fp32 accumulation (the
+    GEMM's fp32 output with beta = 1) unless ``in_fp16`` (``accumulation_in_fp16``: main_grad kept
+    in the activation dtype, accumulated there)."""
     mg = weight.main_grad
+    if in_fp16 or mg.dtype != torch.float32:
+        if mg.dtype == torch.float32:
+            raise RuntimeError("accumulation_in_fp16 needs a 16-bit main_grad buffer")
+        mg.addmm_(dy2.t().to(mg.dtype), x2.to(mg.dtype))
+        return
     if dy2.is_cuda and dy2.dtype in (torch.bfloat16, torch.float16):
         try:
             torch.addmm(mg, dy2.t(), x2, out_dtype=torch.float32, out=mg)
@@ -101,10 +115,12 @@ class LinearWithGradAccumulationAndAsyncCommunication(torch.autograd.Function):
     """y = x W^T (+ b) for a tensor-parallel shard, with the backward overlap described above."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, gradient_accumulation_fusion, async_grad_allreduce, sequence_parallel):
+    def forward(ctx, x, weight, bias, gradient_accumulation_fusion, async_grad_allreduce, sequence_parallel,
+                accumulation_in_fp16=False):
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
         ctx.flags = (gradient_accumulation_fusion, async_grad_allreduce, sequence_parallel)
+        ctx.in_fp16 = bool(accumulation_in_fp16)
         total = _gather_seq(x) if sequence_parallel else x
         return fops.fused_dense(total, weight, bias)
 
@@ -129,14 +145,14 @@ class LinearWithGradAccumulationAndAsyncCommunication(torch.autograd.Function):
                 handle = dist.all_reduce(dx, group=tp_group, async_op=True)
         # weight gradient while the input-gradient collective is in flight
         if fusion and hasattr(weight, "main_grad"):
-            _accumulate_main_grad(weight, dy2, t2)
+            _accumulate_main_grad(weight, dy2, t2, ctx.in_fp16)
             dw = None
         else:
             dw = fops._wgrad(dy2, t2) if dy2.is_cuda else dy2.t().mm(t2)
         db = dy2.sum(0) if ctx.has_bias else None
         if handle is not None:
             handle.wait()
-        return out, dw, db, None, None, None
+        return out, dw, db, None, None, None, None
 
 
 def _gather_seq(x):
@@ -150,9 +166,11 @@ def _gather_seq(x):
 
 
 def linear_with_grad_accumulation_and_async_allreduce(x, weight, bias, gradient_accumulation_fusion,
-                                                      async_grad_allreduce, sequence_parallel_enabled):
+                                                      async_grad_allreduce, sequence_parallel_enabled,
+                                                      accumulation_in_fp16=False):
     return LinearWithGradAccumulationAndAsyncCommunication.apply(x, weight, bias, gradient_accumulation_fusion,
-                                                                 async_grad_allreduce, sequence_parallel_enabled)
+                                                                 async_grad_allreduce, sequence_parallel_enabled,
+                                                                 accumulation_in_fp16)
 
 
 class VocabParallelEmbedding(nn.Module):
@@ -171,7 +189,8 @@ class VocabParallelEmbedding(nn.Module):
         self.weight = Parameter(torch.empty(self.num_embeddings_per_partition, embedding_dim,
                                             dtype=params_dtype, device=device))
         _initialize_affine_weight(self.weight, num_embeddings, embedding_dim, self.num_embeddings_per_partition,
-                                  0, init_method, params_dtype=params_dtype)
+                                  0, init_method, params_dtype=params_dtype,
+                                  use_cpu_initialization=use_cpu_initialization)
 
     def forward(self, input_):
         if self.tensor_model_parallel_size > 1:
@@ -203,6 +222,7 @@ class ColumnParallelLinear(nn.Module):
         self.skip_bias_add = skip_bias_add
         self.sequence_parallel_enabled = sequence_parallel_enabled
         self.gradient_accumulation_fusion = gradient_accumulation_fusion
+        self.accumulation_in_fp16 = accumulation_in_fp16
         # async dX all-reduce only where a backward all-reduce exists (TP > 1, no sequence parallel)
         self.async_tensor_model_parallel_allreduce = (not no_async_tensor_model_parallel_allreduce and ws > 1
                                                       and not sequence_parallel_enabled)
@@ -210,7 +230,8 @@ class ColumnParallelLinear(nn.Module):
                                             device=device))
         self.master_weight = _initialize_affine_weight(self.weight, output_size, input_size,
                                                        self.output_size_per_partition, 0, init_method, stride,
-                                                       keep_master_weight_for_test, params_dtype)
+                                                       keep_master_weight_for_test, params_dtype,
+                                                       use_cpu_initialization)
         if bias:
             self.bias = Parameter(torch.zeros(self.output_size_per_partition, dtype=params_dtype, device=device))
             set_tensor_model_parallel_attributes(self.bias, True, 0, stride)
@@ -221,9 +242,15 @@ class ColumnParallelLinear(nn.Module):
         bias = self.bias if not self.skip_bias_add else None
         if self.async_tensor_model_parallel_allreduce or self.sequence_parallel_enabled or \
                 self.gradient_accumulation_fusion:
+            # the fused Function all-reduces (or reduce-scatters) dX itself only when async
+            # all-reduce or sequence parallelism is on; with fusion alone the input goes through the
+            # identity-forward / all-reduce-backward region first (Megatron's column-parallel rule)
+            x = input_ if (self.async_tensor_model_parallel_allreduce or self.sequence_parallel_enabled) \
+                else copy_to_tensor_model_parallel_region(input_)
             out = linear_with_grad_accumulation_and_async_allreduce(
-                input_, self.weight, bias, self.gradient_accumulation_fusion,
-                self.async_tensor_model_parallel_allreduce, self.sequence_parallel_enabled)
+                x, self.weight, bias, self.gradient_accumulation_fusion,
+                self.async_tensor_model_parallel_allreduce, self.sequence_parallel_enabled,
+                self.accumulation_in_fp16)
         else:
             out = fops.fused_dense(copy_to_tensor_model_parallel_region(input_), self.weight, bias)
         if self.gather_output:
@@ -249,13 +276,15 @@ class RowParallelLinear(nn.Module):
         self.skip_bias_add = skip_bias_add
         self.sequence_parallel_enabled = sequence_parallel_enabled
         self.gradient_accumulation_fusion = gradient_accumulation_fusion
+        self.accumulation_in_fp16 = accumulation_in_fp16
         if sequence_parallel_enabled and not input_is_parallel:
             raise RuntimeError("To enable `sequence_parallel_enabled`, `input_is_parallel` must be `True`")
         self.weight = Parameter(torch.empty(output_size, self.input_size_per_partition, dtype=params_dtype,
                                             device=device))
         self.master_weight = _initialize_affine_weight(self.weight, output_size, input_size,
                                                        self.input_size_per_partition, 1, init_method, stride,
-                                                       keep_master_weight_for_test, params_dtype)
+                                                       keep_master_weight_for_test, params_dtype,
+                                                       use_cpu_initialization)
         if bias:
             self.bias = Parameter(torch.zeros(output_size, dtype=params_dtype, device=device))
             setattr(self.bias, "sequence_parallel_enabled", sequence_parallel_enabled)
@@ -265,7 +294,8 @@ class RowParallelLinear(nn.Module):
     def forward(self, input_):
         x = input_ if self.input_is_parallel else scatter_to_tensor_model_parallel_region(input_)
         if self.gradient_accumulation_fusion:
-            partial = linear_with_grad_accumulation_and_async_allreduce(x, self.weight, None, True, False, False)
+            partial = linear_with_grad_accumulation_and_async_allreduce(x, self.weight, None, True, False, False,
+                                                                        self.accumulation_in_fp16)
         else:
             partial = fops.fused_dense(x, self.weight, None)
         if self.sequence_parallel_enabled:

@@ -269,3 +269,41 @@ def test_allreduce_sweep_tool_gloo():
     assert r.returncode == 0, r.stderr[-2000:]
     rows = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(rows) == 4 and all(x["busbw_gbs"] > 0 and x["world"] == 2 for x in rows), rows
+
+
+def _subgroup_lanes_worker(rank, world, port, q):
+    """Two disjoint DP groups {0,1} and {2,3}, each DDP with 2 communicator lanes: every rank
+    must create every group's lanes (dist.new_group is collective over the default group), and
+    each group's gradients average only over its own two ranks."""
+    try:
+        _init(rank, world, port)
+        from apex.parallel import DistributedDataParallel as DDP
+
+        groups = [dist.new_group([0, 1]), dist.new_group([2, 3])]
+        mine = groups[rank // 2]
+        torch.manual_seed(rank // 2)  # the two DP groups hold different models
+        net = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.Tanh(), torch.nn.Linear(16, 4))
+        ref = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.Tanh(), torch.nn.Linear(16, 4))
+        ref.load_state_dict(net.state_dict())
+        model = DDP(net, message_size=40, process_group=mine, num_allreduce_streams=2)
+        assert model.comm_stats()["num_communicators"] == 2
+        g = torch.Generator().manual_seed(7 + rank // 2)
+        for _ in range(2):
+            xs = torch.randn(8, 8, generator=g)
+            model.zero_grad()
+            model(xs[(rank % 2) * 4:(rank % 2 + 1) * 4]).pow(2).sum().backward()
+            ref.zero_grad()
+            (ref(xs).pow(2).sum() / 2).backward()
+            for p, r in zip(net.parameters(), ref.parameters()):
+                torch.testing.assert_close(p.grad, r.grad, rtol=1e-5, atol=1e-6)
+        q.put((rank, "ok"))
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ddp_lanes_on_dp_subgroups():
+    _run(4, _subgroup_lanes_worker)

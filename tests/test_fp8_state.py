@@ -81,8 +81,9 @@ def test_amp_initialize_fp8_flag_and_step_hook():
 def test_state_dict_by_parameter_name():
     lin = torch.nn.Linear(4, 4)
     st = fp8.Fp8State(device="cpu")
-    sw = st.slot((id(lin.weight), "w"), fp8.E4M3)
-    sx = st.slot((id(lin.weight), "x"), fp8.E4M3)
+    kw = st.key_of(lin.weight)
+    sw = st.slot((kw, "w"), fp8.E4M3)
+    sx = st.slot((kw, "x"), fp8.E4M3)
     st.slot((12345, "x"), fp8.E4M3)  # not a parameter of lin: dropped from the named dict
     st.scale[sx] = 3.0
     st.hist[sx, 0] = 7.0
@@ -91,7 +92,83 @@ def test_state_dict_by_parameter_name():
     assert set(sd["slots"]) == {"weight:w", "weight:x"}
     st2 = fp8.Fp8State(device="cpu")
     st2.load_state_dict(sd, lin)
-    s2 = st2.slots[(id(lin.weight), "x")]
+    k2 = st2.key_of(lin.weight)
+    s2 = st2.slots[(k2, "x")]
     assert float(st2.scale[s2]) == 3.0 and float(st2.hist[s2, 0]) == 7.0
-    assert s2 not in st2._fresh and st2.slots[(id(lin.weight), "w")] in st2._fresh
+    assert s2 not in st2._fresh and st2.slots[(k2, "w")] in st2._fresh
     del sw
+
+
+def test_slot_keys_survive_id_reuse_and_recycle():
+    """Slots are keyed by a counter stored on the tensor, not id(): a tensor re-created every
+    step (an O1 cast) reuses the freed slot instead of growing the buffers, and a new tensor never
+    inherits a dead one's scale history."""
+    st = fp8.Fp8State(device="cpu")
+    for step in range(50):
+        w = torch.randn(4, 4)  # a fresh per-step weight copy
+        s = st.slot((st.key_of(w), "x"), fp8.E4M3)
+        assert s in st._fresh  # new tensor: fresh (current scaling), no inherited history
+        st.scale[s] = 5.0
+        del w
+    assert st.n == 1  # one slot, recycled 50 times
+    keep = torch.randn(4, 4)
+    sk = st.slot((st.key_of(keep), "x"), fp8.E4M3)
+    assert float(st.scale[sk]) == 1.0  # the recycled slot was reset
+
+
+def test_amax_reduction_defaults_to_data_parallel_group(monkeypatch):
+    from apex.transformer import parallel_state as ps
+
+    st = fp8.Fp8State(device="cpu")
+    sentinel = object()
+    monkeypatch.setattr(ps, "model_parallel_is_initialized", lambda: True)
+    monkeypatch.setattr(ps, "get_data_parallel_group", lambda: sentinel)
+    assert st.reduction_group() is sentinel
+    explicit = object()
+    st2 = fp8.Fp8State(fp8.Fp8Recipe(amax_reduction_group=explicit), device="cpu")
+    assert st2.reduction_group() is explicit
+
+
+def _mismatch_worker(rank, world, port, q):
+    import os
+    import traceback
+
+    import torch.distributed as dist
+
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        st = fp8.Fp8State(device="cpu")
+        ws = [torch.randn(2, 2) for _ in range(2 + rank)]  # rank 1 quantises one tensor more
+        for w in ws:
+            st.slot((st.key_of(w), "x"), fp8.E4M3)
+        st.amax[: st.n] = torch.arange(st.n, dtype=torch.float32) + rank
+        try:
+            st._reduce_amax(None)
+            q.put((rank, "no error"))
+        except RuntimeError as e:
+            q.put((rank, "ok" if "slot counts differ" in str(e) else str(e)))
+    except Exception:
+        q.put((rank, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_amax_reduction_detects_slot_mismatch():
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_mismatch_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in ps]
+    for p in ps:
+        p.join(timeout=30)
+    assert all(r[1] == "ok" for r in res), res

@@ -5,7 +5,10 @@
 * ``gradient_accumulation_fusion`` accumulates dW into the fp32 ``main_grad`` across backward
   passes and leaves ``.grad`` unset;
 * sequence parallelism: a column -> row pair on a sequence-sharded activation ([s/tp, b, h])
-  matches the serial pair, output and input gradient still sharded.
+  matches the serial pair, output and input gradient still sharded;
+* ``fusion_sync``: gradient_accumulation_fusion with the async all-reduce OFF — the column layer
+  must still all-reduce dX (through copy_to_tensor_model_parallel_region);
+* ``fusion_fp16``: ``accumulation_in_fp16`` accumulates into a 16-bit main_grad.
 """
 import os
 import socket
@@ -59,12 +62,15 @@ def _pair(mode, seq_par=False):
     from apex.transformer import tensor_parallel as tp
 
     torch.manual_seed(0)
+    fusion = mode.startswith("fusion")
     col = tp.ColumnParallelLinear(8, 16, gather_output=False, keep_master_weight_for_test=True,
-                                  no_async_tensor_model_parallel_allreduce=(mode == "sync"),
-                                  gradient_accumulation_fusion=(mode == "fusion"), sequence_parallel_enabled=seq_par)
+                                  no_async_tensor_model_parallel_allreduce=(mode in ("sync", "fusion_sync")),
+                                  gradient_accumulation_fusion=fusion, sequence_parallel_enabled=seq_par,
+                                  accumulation_in_fp16=(mode == "fusion_fp16"))
     torch.manual_seed(1)
     row = tp.RowParallelLinear(16, 8, input_is_parallel=True, keep_master_weight_for_test=True,
-                               gradient_accumulation_fusion=(mode == "fusion"), sequence_parallel_enabled=seq_par)
+                               gradient_accumulation_fusion=fusion, sequence_parallel_enabled=seq_par,
+                               accumulation_in_fp16=(mode == "fusion_fp16"))
     with torch.no_grad():
         col.bias.uniform_(-1, 1)
         row.bias.uniform_(-1, 1)
@@ -83,9 +89,11 @@ def _overlap(rank, world, mode):
 
     ps.initialize_model_parallel(world, 1)
     col, row = _pair(mode)
-    if mode == "fusion":
+    fusion = mode.startswith("fusion")
+    mg_dtype = torch.float16 if mode == "fusion_fp16" else torch.float32
+    if fusion:
         for m in (col, row):
-            m.weight.main_grad = torch.zeros_like(m.weight, dtype=torch.float32)
+            m.weight.main_grad = torch.zeros_like(m.weight, dtype=mg_dtype)
     cb = _full_col_bias(col, world)
     gw_ref = torch.zeros_like(col.master_weight)
     for it in range(2):
@@ -103,14 +111,16 @@ def _overlap(rank, world, mode):
         gw_ref += wc.grad
     n = col.output_size_per_partition
     mine = gw_ref[rank * n:(rank + 1) * n]
-    if mode == "fusion":
+    if fusion:
         assert col.weight.grad is None and row.weight.grad is None
-        torch.testing.assert_close(col.weight.main_grad, mine, rtol=1e-5, atol=1e-5)
+        tol = 2e-2 if mode == "fusion_fp16" else 1e-5
+        assert col.weight.main_grad.dtype == mg_dtype
+        torch.testing.assert_close(col.weight.main_grad.float(), mine, rtol=tol, atol=tol)
     else:
         torch.testing.assert_close(col.weight.grad, mine, rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("mode", ["async", "sync", "fusion"])
+@pytest.mark.parametrize("mode", ["async", "sync", "fusion", "fusion_sync", "fusion_fp16"])
 def test_column_row_backward_overlap_modes(mode):
     _spawn(_overlap, 2, mode)
 

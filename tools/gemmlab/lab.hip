@@ -1,0 +1,194 @@
+// Standalone GEMM lab (no torch): times kernel variants of csrc/gemm.hip against each other on
+// random bf16 operands, interleaved in one process, and checks every variant's output against the
+// 8-wave reference kernel. Build + run (GPU box):
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Icsrc tools/gemmlab/lab.hip -o build/gemmlab
+//   build/gemmlab M N K [epi=0] [rounds=5] [reps=10]
+// Prints one JSON line per variant: us per call (min / median over rounds), PF/s, max |diff|.
+#include "../../csrc/gemm.hip"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+using namespace apex;
+
+#define CK(x)                                                                        \
+  do {                                                                               \
+    hipError_t e_ = (x);                                                             \
+    if (e_ != hipSuccess) {                                                          \
+      fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); \
+      exit(2);                                                                       \
+    }                                                                                \
+  } while (0)
+
+__global__ void fill_kernel(bf16* p, int64_t n, uint32_t seed, float scale) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+    h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
+    p[i] = (bf16)(((h & 0xFFFFFF) / 8388608.f - 1.f) * scale);
+  }
+}
+
+__global__ void maxdiff_kernel(const bf16* a, const bf16* b, int64_t n, float* out) {
+  float m = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float d = fabsf((float)a[i] - (float)b[i]);
+    if (!(d <= m)) m = d;  // NaN propagates
+  }
+  for (int o = 32; o; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) atomicMax((int*)out, __float_as_int(m));
+}
+
+// error census: count of |a - b| > thr per 16 x 16 fragment position inside the 256 x 256 tile
+__global__ void errmap_kernel(const bf16* a, const bf16* b, int M, int N, float thr, unsigned* hist) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (int64_t)M * N; i += (int64_t)gridDim.x * blockDim.x) {
+    const float d = fabsf((float)a[i] - (float)b[i]);
+    if (!(d <= thr)) {
+      const int r = (int)(i / N) & 255, c = (int)(i % N) & 255;
+      atomicAdd(&hist[(r >> 4) * 16 + (c >> 4)], 1u);
+    }
+  }
+}
+
+struct Bufs {
+  bf16 *A, *B, *bias, *aux, *C, *Cref, *aux_out, *aux_ref;
+  float* part;
+  int M, N, K;
+};
+
+typedef void (*Launch)(const Bufs&, int epi, hipStream_t);
+
+template <int EPI>
+void launch_old(const Bufs& b, hipStream_t s) {
+  const int tiles = ((b.M + 255) / 256) * ((b.N + 255) / 256);
+  hipLaunchKernelGGL((gemm_nt_kernel<bf16, EPI, false, false>), dim3(tiles), dim3(512), 0, s, b.A, b.B, b.C, b.M, b.N,
+                     b.K, (int64_t)b.K, (int64_t)b.K, (int64_t)b.N, b.bias, b.aux, (int64_t)b.N, b.aux_out, b.part, 0,
+                     nullptr, nullptr);
+}
+template <int EPI, int DBG = 0>
+void launch_w4(const Bufs& b, hipStream_t s) {
+  const int tiles = ((b.M + 255) / 256) * ((b.N + 255) / 256);
+  hipLaunchKernelGGL((gemm_w4_kernel<bf16, EPI, false, false, DBG>), dim3(tiles), dim3(256), 0, s, b.A, b.B, b.C, b.M, b.N,
+                     b.K, (int64_t)b.K, (int64_t)b.K, (int64_t)b.N, b.bias, b.aux, (int64_t)b.N, b.aux_out, b.part);
+}
+
+template <int EPI>
+void run_epi(Bufs& b, int rounds, int reps, hipStream_t s) {
+  struct V {
+    const char* name;
+    void (*fn)(const Bufs&, hipStream_t);
+  };
+  std::vector<V> vs = {{"w8", launch_old<EPI>}, {"w4", launch_w4<EPI>}, {"w4r", launch_w4<EPI, 256>}};
+  if (getenv("LAB_DBG")) {
+    vs.push_back({"w4_noglds", launch_w4<EPI, 32>});
+    vs.push_back({"w4_nobar", launch_w4<EPI, 64>});
+    vs.push_back({"w4_nodsread", launch_w4<EPI, 128>});
+    vs.push_back({"w4_nomem", launch_w4<EPI, 32 + 64 + 128>});
+  }
+  const int64_t MN = (int64_t)b.M * b.N;
+  float* dmax;
+  CK(hipMalloc(&dmax, 4));
+  // reference output from the 8-wave kernel
+  bf16* C0 = b.C;
+  bf16* AO0 = b.aux_out;
+  b.C = b.Cref;
+  b.aux_out = b.aux_ref;
+  vs[0].fn(b, s);
+  b.C = C0;
+  b.aux_out = AO0;
+  CK(hipStreamSynchronize(s));
+  std::vector<std::vector<float>> t(vs.size());
+  std::vector<float> diff(vs.size(), 0.f);
+  for (size_t v = 0; v < vs.size(); ++v) {
+    CK(hipMemsetAsync(b.C, 0, MN * 2, s));
+    vs[v].fn(b, s);
+    CK(hipMemsetAsync(dmax, 0, 4, s));
+    hipLaunchKernelGGL(maxdiff_kernel, dim3(1024), dim3(256), 0, s, b.C, b.Cref, MN, dmax);
+    CK(hipMemcpyAsync(&diff[v], dmax, 4, hipMemcpyDeviceToHost, s));
+    CK(hipStreamSynchronize(s));
+    if (getenv("LAB_ERRMAP") && diff[v] > 0.02f) {
+      unsigned* dh;
+      CK(hipMalloc(&dh, 256 * 4));
+      CK(hipMemsetAsync(dh, 0, 256 * 4, s));
+      hipLaunchKernelGGL(errmap_kernel, dim3(1024), dim3(256), 0, s, b.C, b.Cref, b.M, b.N, 0.02f, dh);
+      unsigned h[256];
+      CK(hipMemcpyAsync(h, dh, 256 * 4, hipMemcpyDeviceToHost, s));
+      CK(hipStreamSynchronize(s));
+      printf("errmap %s (rows: fragment row 0..15 of the tile; cols: fragment col 0..15)\n", vs[v].name);
+      for (int r = 0; r < 16; ++r) {
+        for (int c = 0; c < 16; ++c) printf("%7u", h[r * 16 + c]);
+        printf("\n");
+      }
+      CK(hipFree(dh));
+    }
+  }
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (int r = 0; r < rounds; ++r)
+    for (size_t v = 0; v < vs.size(); ++v) {
+      vs[v].fn(b, s);  // warm
+      CK(hipEventRecord(e0, s));
+      for (int i = 0; i < reps; ++i) vs[v].fn(b, s);
+      CK(hipEventRecord(e1, s));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      t[v].push_back(ms * 1000.f / reps);
+    }
+  const double flop = 2.0 * b.M * b.N * b.K;
+  for (size_t v = 0; v < vs.size(); ++v) {
+    std::vector<float> x = t[v];
+    std::sort(x.begin(), x.end());
+    printf("{\"M\": %d, \"N\": %d, \"K\": %d, \"epi\": %d, \"variant\": \"%s\", \"us_min\": %.1f, \"us_med\": %.1f, "
+           "\"pflops\": %.3f, \"maxdiff\": %g}\n",
+           b.M, b.N, b.K, EPI, vs[v].name, x[0], x[x.size() / 2], flop / (x[0] * 1e-6) / 1e15, diff[v]);
+  }
+  fflush(stdout);
+  CK(hipFree(dmax));
+}
+
+int main(int argc, char** argv) {
+  if (argc < 4) {
+    fprintf(stderr, "usage: %s M N K [epi] [rounds] [reps]\n", argv[0]);
+    return 1;
+  }
+  Bufs b;
+  b.M = atoi(argv[1]);
+  b.N = atoi(argv[2]);
+  b.K = atoi(argv[3]);
+  const int epi = argc > 4 ? atoi(argv[4]) : 0;
+  const int rounds = argc > 5 ? atoi(argv[5]) : 5;
+  const int reps = argc > 6 ? atoi(argv[6]) : 10;
+  const int64_t MK = (int64_t)b.M * b.K, NK = (int64_t)b.N * b.K, MN = (int64_t)b.M * b.N;
+  CK(hipMalloc(&b.A, MK * 2));
+  CK(hipMalloc(&b.B, NK * 2));
+  CK(hipMalloc(&b.bias, b.N * 2));
+  CK(hipMalloc(&b.aux, MN * 2));
+  CK(hipMalloc(&b.C, MN * 2));
+  CK(hipMalloc(&b.Cref, MN * 2));
+  CK(hipMalloc(&b.aux_out, MN * 2));
+  CK(hipMalloc(&b.aux_ref, MN * 2));
+  CK(hipMalloc(&b.part, (int64_t)((b.M + 255) / 256) * 2 * b.N * 4));
+  hipStream_t s;
+  CK(hipStreamCreate(&s));
+  hipLaunchKernelGGL(fill_kernel, dim3(2048), dim3(256), 0, s, b.A, MK, 1u, 1.f);
+  hipLaunchKernelGGL(fill_kernel, dim3(2048), dim3(256), 0, s, b.B, NK, 2u, 1.f / sqrtf((float)b.K));
+  hipLaunchKernelGGL(fill_kernel, dim3(64), dim3(256), 0, s, b.bias, (int64_t)b.N, 3u, 0.1f);
+  hipLaunchKernelGGL(fill_kernel, dim3(2048), dim3(256), 0, s, b.aux, MN, 4u, 1.f);
+  CK(hipStreamSynchronize(s));
+  switch (epi) {
+    case 0: run_epi<EPI_NONE>(b, rounds, reps, s); break;
+    case 1: run_epi<EPI_BIAS>(b, rounds, reps, s); break;
+    case 4: run_epi<EPI_RESID>(b, rounds, reps, s); break;
+    case 8: run_epi<EPI_BIAS_GELU_D>(b, rounds, reps, s); break;
+    case 10: run_epi<EPI_MUL>(b, rounds, reps, s); break;
+    default: fprintf(stderr, "epi %d not in the lab\n", epi); return 1;
+  }
+  return 0;
+}
