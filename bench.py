@@ -51,11 +51,17 @@ def parse():
     ap.add_argument("--fp8", action="store_true",
                     help="extra pass: the same step with amp fp8=True (NOT the headline: reported under extra.fp8)")
     ap.add_argument("--fp8-steps", type=int, default=10)
-    ap.add_argument("--message-size", type=int, default=int(os.environ.get("APEX_DDP_MESSAGE_SIZE", 25_000_000)))
+    # DDP bucket sizes (elements): at N>1 chosen by an in-job probe of the communicator unless
+    # given here (apex.parallel.preflight.select_bucket_sizes); at N=1 there is no communication
+    ap.add_argument("--message-size", type=int,
+                    default=int(os.environ["APEX_DDP_MESSAGE_SIZE"]) if "APEX_DDP_MESSAGE_SIZE" in os.environ else None)
+    ap.add_argument("--first-bucket-size", type=int, default=None)
+    ap.add_argument("--ddp-fp32-allreduce", action="store_true",
+                    help="reduce the bf16 gradient buckets in fp32 (A/B of the reduction precision)")
     return ap.parse_args()
 
 
-def build(env, cfg, fp32, message_size, fp8=False):
+def build(env, cfg, fp32, message_size, fp8=False, first_bucket_size=None, fp32_allreduce=False):
     from apex import amp
     from apex.amp._amp_state import _amp_state
     from apex.models.bert import BertForPreTraining, param_groups_for_lamb
@@ -72,7 +78,8 @@ def build(env, cfg, fp32, message_size, fp8=False):
     else:
         model, opt = amp.initialize(model, opt, opt_level="O2", cast_model_type=torch.bfloat16,
                                     verbosity=0, fp8=fp8)
-    model = DDP(model, message_size=message_size, comm_timing=True)
+    model = DDP(model, message_size=message_size, first_bucket_size=first_bucket_size, comm_timing=True,
+                allreduce_always_fp32=fp32_allreduce)
     return model, opt
 
 
@@ -128,7 +135,10 @@ def main():
     from apex.utils.bench import emit, finish, init_distributed, log, max_over_ranks, time_steps
     from apex.utils.gemm_tuning import DEFAULT_DIR, enable_tuned_gemms
 
+    from apex.parallel import preflight
+
     tuned = enable_tuned_gemms()  # committed hipBLASLt/rocBLAS selections, read-only
+    preflight.apply_channel_cap()  # APEX_DDP_CHANNELS -> NCCL_MAX_NCHANNELS, before any communicator
     env = init_distributed(single_rank_group=True)  # also reserves stdout for the result line
     if env.world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={env.world}; using WORLD_SIZE")
@@ -147,11 +157,33 @@ def main():
         g.manual_seed(42 + env.rank)
         return [synthetic_batch(cfg, n, args.seq, device=dev, generator=g) for _ in range(4)]
 
+    extra = {}
+    # multi-GPU pre-flight: known-value all-reduces on the DDP communicator (fails loudly), the
+    # RCCL settings in force, and the bucket sizes from an in-job probe of 3 candidate sizes
+    dist_info = {"nranks": world, "rccl_env": preflight.rccl_env()}
+    message_size, first_bucket = args.message_size, args.first_bucket_size
+    if world > 1:
+        dist_info["preflight"] = preflight.preflight_allreduce(None, dev)
+        if message_size is None:
+            probe = preflight.probe_bucket_sizes(None, dev)
+            message_size, auto_first = preflight.select_bucket_sizes(probe)
+            first_bucket = first_bucket if first_bucket is not None else auto_first
+            dist_info["bucket_probe"] = probe
+            dist_info["bucket_choice"] = "probe (smallest size within 90% of the best bus bandwidth)"
+        else:
+            dist_info["bucket_choice"] = "flag"
+    if message_size is None:
+        message_size = 25_000_000
+    dist_info.update(message_size=message_size, first_bucket_size=first_bucket,
+                     allreduce_dtype="fp32" if args.ddp_fp32_allreduce else "bf16")
+    extra["dist"] = dist_info
+    args.message_size = message_size
+
     sampler = telemetry.GpuSampler(dev.index or 0)
     idle = sampler.snapshot()
-    extra = {}
     if not args.fp32_only:
-        model, opt = build(env, cfg, False, args.message_size)
+        model, opt = build(env, cfg, False, args.message_size, first_bucket_size=first_bucket,
+                           fp32_allreduce=args.ddp_fp32_allreduce)
         batches = batches_for(args.batch)
         timer = telemetry.StepTimer()
         elapsed, loss = time_steps(env, make_step(model, opt, batches, 0), args.steps, args.warmup,
