@@ -20,10 +20,12 @@ from .scaler import LossScaler
 
 
 def _model_grads(optimizer):
+    from ..optimizers._base import grad_of
+
     stash = getattr(optimizer, "_amp_stash", None)
     if stash is not None and stash.master_weights:
-        return [p.grad for ps in stash.model_params for p in ps if p.grad is not None]
-    return [p.grad for g in optimizer.param_groups for p in g["params"] if p.grad is not None]
+        return [grad_of(p) for ps in stash.model_params for p in ps if grad_of(p) is not None]
+    return [grad_of(p) for g in optimizer.param_groups for p in g["params"] if grad_of(p) is not None]
 
 
 @contextlib.contextmanager
@@ -71,12 +73,14 @@ def scale_loss(loss, optimizers, loss_id=0, model=None, delay_unscale=False,
         # ---- non-fused optimizer: unscale into masters (or in place) + host decision
         scaler.clear_overflow_state()
         if stash.master_weights:
-            models = [m for m in stash.half_models if m.grad is not None]
-            masters = [ms for m, ms in zip(stash.half_models, stash.half_masters) if m.grad is not None]
+            from ..optimizers._base import grad_of
+
+            models = [m for m in stash.half_models if grad_of(m) is not None]
+            masters = [ms for m, ms in zip(stash.half_models, stash.half_masters) if grad_of(m) is not None]
             for ms, m in zip(masters, models):
                 if ms.grad is None:
                     ms.grad = torch.empty_like(ms)
-            scaler.unscale([m.grad for m in models], [ms.grad for ms in masters])
+            scaler.unscale([grad_of(m) for m in models], [ms.grad for ms in masters])
             fp32 = [p.grad for g in opt.param_groups for p in g["params"]
                     if p.grad is not None and all(p is not ms for ms in stash.half_masters)]
             if fp32:

@@ -223,10 +223,13 @@ def sync_embedding_grads(model):
         return
     if not (model.pre_process or model.post_process):
         return
-    g = model.word_embeddings.weight.grad
+    w = model.word_embeddings.weight
+    g = getattr(w, "main_grad", None)  # apex DDP fp32_main_grad mode: the fp32 accumulator
     if g is None:
-        g = torch.zeros_like(model.word_embeddings.weight)
-        model.word_embeddings.weight.grad = g
+        g = w.grad
+        if g is None:
+            g = torch.zeros_like(w)
+            w.grad = g
     dist.all_reduce(g, group=ps.get_embedding_group())
 
 

@@ -70,7 +70,7 @@ class _AttnSublayer(torch.autograd.Function):
                                                    dbias_out=_gt(pbo) if has_bo else None)
         f8 = ctx.f8
         dctx = G.dgrad(dt, wo, f8=f8).view(B, S, heads, d)
-        dwo = _wgrad(dt, o.view(B * S, E), out=_gt(pwo))
+        dwo = _wgrad(dt, o.view(B * S, E), param=pwo)
         q, k, v = qkv.view(B, S, 3, heads, d).unbind(2)
         dqkv = torch.empty_like(qkv)
         dq, dk, dv = dqkv.view(B, S, 3, heads, d).unbind(2)
@@ -81,7 +81,7 @@ class _AttnSublayer(torch.autograd.Function):
                          dmask, dsum)
         dbqkv = C.partial_colsum(dsum, bdt, _gt(pbqkv)) if has_bqkv else None
         dx = G.dgrad_resid(dqkv, wqkv, dres, f8=f8)  # residual grad accumulated in the GEMM epilogue
-        dwqkv = _wgrad(dqkv, x2, out=_gt(pqkv))
+        dwqkv = _wgrad(dqkv, x2, param=pqkv)
         return (dx.view(B, S, E), dwqkv, dbqkv, dwo, dbo if has_bo else None, dgamma, dbeta,
                 None, None, None, None, None, None)
 
@@ -130,9 +130,9 @@ class _FFNSublayer(torch.autograd.Function):
                 db1 = tb1.copy_(db1)  # a path that could not write the slot: keep the handed-out view valid
         else:
             dh, db1 = C.bias_act_bwd(G.dgrad(dt, w2, f8=f8), h, hb, act)
-        dw2 = _wgrad(dt, g, out=_gt(pw2))
+        dw2 = _wgrad(dt, g, param=pw2)
         dx = G.dgrad_resid(dh, w1, dres, f8=f8)  # residual grad accumulated in the GEMM epilogue
-        dw1 = _wgrad(dh, x2, out=_gt(pw1))
+        dw1 = _wgrad(dh, x2, param=pw1)
         return (dx.view_as(dy), dw1, db1 if b1dt is not None else None, dw2, db2 if has_b2 else None, dgamma,
                 dbeta, None, None, None)
 
@@ -170,9 +170,9 @@ class _MLP(torch.autograd.Function):
             dh, db1 = G.dgrad_dgelu(dt2, w2, gd, ctx.b1dt, act=ctx.act, f8=ctx.f8, bias_grad_out=tb1)
         if tb1 is not None and db1 is not None and db1.data_ptr() != tb1.data_ptr():
             db1 = tb1.copy_(db1)
-        dw2 = _wgrad(dt2, g, out=_gt(pw2))
+        dw2 = _wgrad(dt2, g, param=pw2)
         dx = G.dgrad(dh, w1, f8=ctx.f8).view(*dt.shape[:-1], w1.shape[1])
-        dw1 = _wgrad(dh, x2, out=_gt(pw1))
+        dw1 = _wgrad(dh, x2, param=pw1)
         return dx, dw1, db1, dw2, None
 
 

@@ -86,9 +86,37 @@ def _gt(p):
     return grad_target(p) if p is not None else None
 
 
-def _wgrad(dy2, x2, out=None):
+def accumulate_main_grad(mg, dy2, x2):
+    """mg (fp32) += dy2^T @ x2 with fp32 accumulation and no 16-bit rounding: the split-K batched
+    GEMM's fp32 slabs (one slab when the shape does not split) summed INTO mg by one HIP pass
+    (splitk_reduce accumulate) — the micro-batch gradient accumulation of DDP's fp32_main_grad
+    mode, with no separate add kernel and no bf16 dW tensor."""
+    M, N = dy2.shape
+    K = x2.shape[1]
+    if not (dy2.is_cuda and _native(dy2) and dy2.dtype in (torch.bfloat16, torch.float16)
+            and dy2.is_contiguous() and x2.is_contiguous() and mg.is_contiguous()):
+        mg.add_(dy2.t().float().mm(x2.float()))
+        return mg
+    s = _wgrad_splits(M, N, K)
+    slabs = torch.bmm(dy2.view(s, M // s, N).transpose(1, 2), x2.view(s, M // s, K), out_dtype=torch.float32)
+    _ext.require().splitk_reduce(slabs, torch.float32, mg, accumulate=True)
+    return mg
+
+
+def _wgrad(dy2, x2, out=None, param=None):
     """Weight gradient dy2^T @ x2 in dy2's dtype (split-K batched GEMM when it pays), written into
-    ``out`` when given (a gradient-bucket slot)."""
+    ``out`` when given (a gradient-bucket slot), or into ``param``'s bucket slot
+    (apex.parallel.grad_target). When ``param`` carries an fp32 ``main_grad`` (DDP
+    fp32_main_grad mode) the gradient is accumulated there instead and a placeholder is returned
+    for autograd (the DDP hook drops it: ``param.grad_added_to_main_grad``)."""
+    if param is not None:
+        mg = getattr(param, "main_grad", None)
+        if mg is not None:
+            accumulate_main_grad(mg, dy2, x2)
+            param.grad_added_to_main_grad = True
+            return torch.empty_like(param)
+        if out is None:
+            out = _gt(param)
     M, N = dy2.shape
     K = x2.shape[1]
     s = _wgrad_splits(M, N, K) if dy2.dtype in (torch.bfloat16, torch.float16) else 1
@@ -148,7 +176,7 @@ class _FusedDense(torch.autograd.Function):
 
             dx = G.dgrad(dy2, w, f8=ctx.f8).view(*dy.shape[:-1], w.shape[1])
         if ctx.needs_input_grad[1]:
-            dw = _wgrad(dy2, x2, out=_gt(ctx.params[0]))
+            dw = _wgrad(dy2, x2, param=ctx.params[0])
         if ctx.has_b and ctx.needs_input_grad[2]:
             db = _ext.require().colsum(dy2, ctx.bdtype, _gt(ctx.params[1]))
         return dx, dw, db
@@ -180,6 +208,7 @@ class _DenseAct(torch.autograd.Function):
             ctx.save_for_backward(x2, w, h, b)
             ctx.bdtype = None
         ctx.act = act
+        ctx.wparam = w
         return y.view(*x.shape[:-1], w.shape[0])
 
     @staticmethod
@@ -195,7 +224,7 @@ class _DenseAct(torch.autograd.Function):
         else:
             dh, db = C.bias_act_bwd(_2d(dy), h, b, ctx.act)
         dx = G.dgrad(dh, w, f8=ctx.f8).view(*dy.shape[:-1], w.shape[1]) if ctx.needs_input_grad[0] else None
-        dw = _wgrad(dh, x2) if ctx.needs_input_grad[1] else None
+        dw = _wgrad(dh, x2, param=ctx.wparam) if ctx.needs_input_grad[1] else None
         return dx, dw, (db if b is not None else None), None
 
 
@@ -336,7 +365,7 @@ class _DenseBDALN(torch.autograd.Function):
         from . import gemm as G
 
         dx = G.dgrad(dt, w, f8=ctx.f8).view(*dy.shape[:-1], w.shape[1]) if ctx.needs_input_grad[0] else None
-        dw = _wgrad(dt, x2, out=_gt(pw)) if ctx.needs_input_grad[1] else None
+        dw = _wgrad(dt, x2, param=pw) if ctx.needs_input_grad[1] else None
         return dx, dw, (db if has_b else None), dres.view_as(dy), dg, dbeta, None, None
 
 

@@ -18,6 +18,13 @@ from .. import _ext
 from ..multi_tensor_apply import PlanHolder
 
 
+def grad_of(p):
+    """The gradient an optimizer should apply for ``p``: its fp32 ``main_grad`` (apex DDP
+    fp32_main_grad mode; micro-batch gradients accumulated in fp32) or ``p.grad``."""
+    mg = getattr(p, "main_grad", None)
+    return mg if mg is not None else p.grad
+
+
 class FusedOptimizerBase(Optimizer):
     def __init__(self, params, defaults, set_grad_none=True):
         super().__init__(params, defaults)
@@ -62,16 +69,17 @@ class FusedOptimizerBase(Optimizer):
         return h.get(lists)
 
     def _group_tensors(self, gi, group):
-        """Returns (grads, params, model_copies or None) for group gi."""
+        """Returns (grads, params, model_copies or None) for group gi. A parameter's gradient is
+        its fp32 ``main_grad`` when it has one (apex DDP fp32_main_grad mode), else ``.grad``."""
         params = [p for p in group["params"]]
         if self._amp_model_params is not None:
             models = self._amp_model_params[gi]
-            sel = [(m.grad, p, m) for p, m in zip(params, models) if m.grad is not None]
+            sel = [(grad_of(m), p, m) for p, m in zip(params, models) if grad_of(m) is not None]
             if not sel:
                 return [], [], []
             g, p, m = zip(*sel)
             return list(g), list(p), list(m)
-        sel = [(p.grad, p) for p in params if p.grad is not None]
+        sel = [(grad_of(p), p) for p in params if grad_of(p) is not None]
         if not sel:
             return [], [], None
         g, p = zip(*sel)
@@ -81,6 +89,16 @@ class FusedOptimizerBase(Optimizer):
         set_none = self.set_grad_none if set_to_none is None else set_to_none
         groups = self._amp_model_params if self._amp_model_params is not None else \
             [g["params"] for g in self.param_groups]
+        # fp32 main_grad buffers (apex DDP fp32_main_grad): one fill per flat buffer
+        main_flats = {}
+        for ps in groups:
+            for p in ps:
+                f = getattr(p, "_apex_main_flat", None)
+                if f is not None and getattr(p, "main_grad", None) is not None:
+                    main_flats[id(f)] = f
+                    p.grad = None
+        for f in main_flats.values():
+            f.zero_()
         # grads that are views of an apex DDP bucket buffer: one fill per buffer instead of one
         # launch per parameter, when every parameter of that buffer belongs to this optimizer
         flats, members = {}, {}

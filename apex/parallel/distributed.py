@@ -270,6 +270,15 @@ class DistributedDataParallel(Module):
     * ``comm_timing``: record HIP events per bucket and per backward so ``comm_stats()`` reports
       bucket sizes, ready->reduced latency and the communication time the compute stream waited
       for at the end of backward (exposed comm).
+    * ``fp32_main_grad``: every parameter's gradient accumulates in an fp32 ``p.main_grad`` (views
+      of fp32 bucket buffers laid out in reverse registration order at construction) instead of
+      ``p.grad`` — Megatron's main_grad, for gradient accumulation over micro-batches of a 16-bit
+      model without bf16 rounding at every add (the reference's fp32 master-grad semantics,
+      ``/root/reference/apex/fp16_utils/fp16util.py:93-112``). The fused weight-gradient GEMMs
+      accumulate straight into main_grad (fp32 output, beta = 1; ``apex.ops.fused._wgrad``) and
+      hand autograd a placeholder; any other gradient is added into main_grad by the hook and
+      ``p.grad`` released. The buckets are reduced in fp32; the fused optimizers and amp read
+      ``main_grad``; ``zero_grad`` zero-fills the buffers.
     """
 
     def __init__(self, module, message_size=10000000, delay_allreduce=False, shared_param=None,
@@ -278,7 +287,7 @@ class DistributedDataParallel(Module):
                  allreduce_communicators=None, gradient_average=True,
                  gradient_predivide_factor=1.0, gradient_average_split_factor=None, prof=False,
                  first_bucket_size=None, process_group=None, broadcast_buffers=True,
-                 comm_timing=False):
+                 comm_timing=False, fp32_main_grad=False):
         super().__init__()
         if shared_param is not None:
             raise ValueError("shared_param is no longer supported as an option. It was misleadingly "
@@ -336,7 +345,14 @@ class DistributedDataParallel(Module):
         self._allreduce_enabled = True
         self._hooks = []
         self._iter_events = []     # (end-of-backward, comm-done) event pairs, comm_timing only
+        self.fp32_main_grad = fp32_main_grad
         self._sync_params()
+        if fp32_main_grad:
+            # static layout (no first-iteration recording): main_grad must exist before the first
+            # backward so the producers can accumulate into it; reverse registration order
+            # approximates the order gradients become ready in backward
+            self._layout_from_order(list(reversed(range(len(self._params)))), dtype=torch.float32)
+            self._layout_ready = True
         self._create_hooks()
 
     # ------------------------------------------------------------ setup
@@ -401,7 +417,12 @@ class DistributedDataParallel(Module):
             self._build_layout()
             self._layout_ready = True
         for i, p in enumerate(self._params):
-            self._ensure_view(i, p)
+            if self.fp32_main_grad:
+                if p.grad is not None:  # a gradient produced outside the hooks
+                    p.main_grad.add_(p.grad)
+                    p.grad = None
+            else:
+                self._ensure_view(i, p)
         for flat in self._flat.values():
             self._reduce_now(flat)
 
@@ -419,6 +440,12 @@ class DistributedDataParallel(Module):
 
     # ------------------------------------------------------------ hooks
     def _grad_hook(self, p):
+        if self.fp32_main_grad:
+            if getattr(p, "grad_added_to_main_grad", False):
+                p.grad_added_to_main_grad = False  # a fused producer accumulated it already
+            elif p.grad is not None:
+                p.main_grad.add_(p.grad)
+            p.grad = None
         if not self._allreduce_enabled:
             return
         if not self._callback_queued:
@@ -437,7 +464,8 @@ class DistributedDataParallel(Module):
             raise RuntimeError("allreduce_trigger_params: a gradient arrived after the trigger params fired "
                                "the all-reduce; the trigger params must be the LAST to receive gradients in "
                                "backward (e.g. the first layer's weight)")
-        self._ensure_view(idx, p)
+        if not self.fp32_main_grad:
+            self._ensure_view(idx, p)
         if self._trigger is not None:
             if idx in self._trigger:
                 self._trigger_seen += 1
@@ -456,6 +484,8 @@ class DistributedDataParallel(Module):
             self._launch_ready_in_order()
 
     def _ensure_view(self, idx, p):
+        if self.fp32_main_grad:
+            return  # main_grad is the bucket view; p.grad is never used
         v = self._views[idx]
         g = p.grad
         if g is None or g.data_ptr() != v.data_ptr():
@@ -556,20 +586,22 @@ class DistributedDataParallel(Module):
             return
         if self.delay_allreduce:
             for idx, p in enumerate(self._params):
-                if p.grad is None:  # no grad this step (zero_grad released the view)
+                if p.grad is None and not self.fp32_main_grad:  # no grad this step (view released)
                     self._views[idx].zero_()
                     p.grad = self._views[idx]
             for flat in self._flat.values():
                 self._reduce_now(flat)
         else:
-            # params that did not receive a grad this iteration: treat as ready (zero grads)
+            # params that did not receive a grad this iteration: treat as ready (zero grads; in
+            # main_grad mode the buffer already holds what was accumulated, zeros if nothing)
             for b in self._buckets:
                 if b.ready != len(b.params):
-                    for idx in b.params:
-                        p = self._params[idx]
-                        if p.grad is None:
-                            self._views[idx].zero_()
-                            p.grad = self._views[idx]
+                    if not self.fp32_main_grad:
+                        for idx in b.params:
+                            p = self._params[idx]
+                            if p.grad is None:
+                                self._views[idx].zero_()
+                                p.grad = self._views[idx]
                     b.ready = len(b.params)
             self._launch_ready_in_order()
             for b in self._buckets:
@@ -595,6 +627,7 @@ class DistributedDataParallel(Module):
                "message_size": self.message_size,
                "bucket_bytes": [b.numel * b.flat.element_size() for b in self._buckets],
                "allreduce_always_fp32": self.allreduce_always_fp32,
+               "fp32_main_grad": self.fp32_main_grad,
                "delay_allreduce": self.delay_allreduce}
         if self.comm_timing and self._cuda:
             torch.cuda.synchronize()
@@ -623,11 +656,11 @@ class DistributedDataParallel(Module):
             order = [int(x) for x in t.tolist()]
         self._layout_from_order(order)
 
-    def _layout_from_order(self, order):
+    def _layout_from_order(self, order, dtype=None):
         by_dtype = OrderedDict()
         for idx in order:
             p = self._params[idx]
-            by_dtype.setdefault(p.dtype, []).append(idx)
+            by_dtype.setdefault(dtype or p.dtype, []).append(idx)
         self._views = [None] * len(self._params)
         self._buckets = []
         self._param_bucket = {}
@@ -643,9 +676,22 @@ class DistributedDataParallel(Module):
                 p = self._params[i]
                 n = p.numel()
                 if p.is_contiguous() or not _dense_non_overlapping(p):
-                    v = flat[off:off + n].view_as(p)
+                    v = flat[off:off + n].view(p.shape)
                 else:  # e.g. channels_last conv weight: the grad view keeps the param's strides
                     v = flat[off:off + n].as_strided(p.shape, p.stride())
+                if dtype is not None:  # fp32 main_grad mode
+                    if p.grad is not None:
+                        v.copy_(p.grad)
+                        p.grad = None
+                    p.main_grad = v
+                    p._apex_main_flat = flat
+                    self._views[i] = v
+                    cur.append(i)
+                    off += n
+                    if off - start >= limit:
+                        self._buckets.append(_Bucket(dt, flat, start, off - start, cur))
+                        start, cur, limit = off, [], self.message_size
+                    continue
                 if p.grad is not None:
                     v.copy_(p.grad)
                 p.grad = v

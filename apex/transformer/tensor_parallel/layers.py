@@ -102,13 +102,7 @@ def _accumulate_main_grad(weight, dy2, x2, in_fp16=False):
             raise RuntimeError("accumulation_in_fp16 needs a 16-bit main_grad buffer")
         mg.addmm_(dy2.t().to(mg.dtype), x2.to(mg.dtype))
         return
-    if dy2.is_cuda and dy2.dtype in (torch.bfloat16, torch.float16):
-        try:
-            torch.addmm(mg, dy2.t(), x2, out_dtype=torch.float32, out=mg)
-            return
-        except (TypeError, RuntimeError):
-            pass
-    mg.add_(torch.mm(dy2.t().float(), x2.float()))
+    fops.accumulate_main_grad(mg, dy2, x2)
 
 
 class LinearWithGradAccumulationAndAsyncCommunication(torch.autograd.Function):
@@ -144,11 +138,17 @@ class LinearWithGradAccumulationAndAsyncCommunication(torch.autograd.Function):
             elif async_ar:
                 handle = dist.all_reduce(dx, group=tp_group, async_op=True)
         # weight gradient while the input-gradient collective is in flight
-        if fusion and hasattr(weight, "main_grad"):
+        if fusion and hasattr(weight, "main_grad") and weight.main_grad is not None:
             _accumulate_main_grad(weight, dy2, t2, ctx.in_fp16)
-            dw = None
+            if getattr(weight, "_apex_main_flat", None) is not None:
+                # main_grad owned by apex DDP (fp32_main_grad): its hook must still see this
+                # parameter become ready -> a placeholder gradient it drops
+                weight.grad_added_to_main_grad = True
+                dw = torch.empty_like(weight)
+            else:
+                dw = None
         else:
-            dw = fops._wgrad(dy2, t2) if dy2.is_cuda else dy2.t().mm(t2)
+            dw = fops._wgrad(dy2, t2, param=weight) if dy2.is_cuda else dy2.t().mm(t2)
         db = dy2.sum(0) if ctx.has_bias else None
         if handle is not None:
             handle.wait()

@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--global-batch", type=int, default=32)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--bf16-grad-accum", action="store_true",
+                    help="accumulate micro-batch gradients in bf16 .grad (the pre-r3 path) instead of "
+                         "the fp32 main_grad buffers")
     args = ap.parse_args()
 
     from apex.utils.bench import emit, finish, init_distributed, instrumented_steps
@@ -64,8 +67,12 @@ def main():
     # data-parallel gradient reduction on apex DDP buckets over the DP group; the pipeline schedule
     # keeps the hooks off (no_sync) until each chunk's last microbatch backward, whose bucket
     # all-reduces then overlap it
+    # micro-batch gradients accumulate in fp32 main_grad buffers (the weight-gradient GEMMs add
+    # their fp32 result straight in; Megatron's main_grad) — no bf16 rounding per micro-batch, no
+    # separate bf16 grad-add kernels
     model = DDP(model, message_size=int(os.environ.get("APEX_DDP_MESSAGE_SIZE", 25_000_000)),
-                process_group=ps.get_data_parallel_group(), comm_timing=True)
+                process_group=ps.get_data_parallel_group(), comm_timing=True,
+                fp32_main_grad=not args.bf16_grad_accum)
     stage = model.module
     n_local = args.global_batch // dp
     g = torch.Generator(device=env.device).manual_seed(7 + ps.get_data_parallel_rank())
@@ -91,7 +98,8 @@ def main():
          elapsed=elapsed, dtype="bf16", data="synthetic token ids; random-init weights",
          config={"model": f"GPT {args.layers}L H{args.hidden} {args.heads} heads", "global_batch": args.global_batch,
                  "micro_batch": args.micro_batch, "seq_len": args.seq,
-                 "parallelism": f"tp{args.tp}xpp{args.pp}xdp{dp}"},
+                 "parallelism": f"tp{args.tp}xpp{args.pp}xdp{dp}",
+                 "grad_accumulation": "bf16 .grad" if args.bf16_grad_accum else "fp32 main_grad"},
          extra=dict(extra, final_loss_last_stage_rank=loss))
     finish(env)
 

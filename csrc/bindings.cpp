@@ -518,14 +518,17 @@ Tensor k_colsum(Tensor x, at::ScalarType out_dtype, const c10::optional<Tensor>&
 }
 
 // split-K combine: slabs fp32 [S, ...] -> sum over S in out_dtype, shape slabs.shape[1:]
-Tensor k_splitk_reduce(Tensor slabs, at::ScalarType out_dtype, const c10::optional<Tensor>& out_opt) {
+Tensor k_splitk_reduce(Tensor slabs, at::ScalarType out_dtype, const c10::optional<Tensor>& out_opt,
+                       bool accumulate = false) {
   TORCH_CHECK(slabs.is_cuda() && slabs.scalar_type() == at::kFloat && slabs.dim() >= 2, "splitk_reduce: fp32 slabs");
   Tensor sc = slabs.contiguous();
   Tensor out = out_or_empty(out_opt, sc.sizes().slice(1), sc.options().dtype(out_dtype), "splitk_reduce");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(sc.data_ptr()) % 16 == 0 && (out.numel() % 4 == 0 || sc.size(0) == 1),
               "splitk_reduce: alignment");
+  TORCH_CHECK(!accumulate || (out_opt.has_value() && out_dtype == at::kFloat),
+              "splitk_reduce: accumulate needs an fp32 out");
   check(apex::splitk_reduce(sc.data_ptr<float>(), out.data_ptr(), out.numel(), (int)sc.size(0), dt_code(out_dtype),
-                            cur_stream()),
+                            cur_stream(), accumulate ? 1 : 0),
         "splitk_reduce");
   return out;
 }
@@ -1254,7 +1257,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bias_dropout_add_bwd", &k_bda_bwd, py::arg("dy"), py::arg("p"), py::arg("seed"), py::arg("offset"),
         py::arg("bias_like"), py::arg("dbias_out") = py::none());
   m.def("colsum", &k_colsum, py::arg("x"), py::arg("out_dtype"), py::arg("out") = py::none());
-  m.def("splitk_reduce", &k_splitk_reduce, py::arg("slabs"), py::arg("out_dtype"), py::arg("out") = py::none());
+  m.def("splitk_reduce", &k_splitk_reduce, py::arg("slabs"), py::arg("out_dtype"), py::arg("out") = py::none(),
+        py::arg("accumulate") = false);
   m.def("bdaln_supported", &k_bdaln_supported);
   m.def("bdaln_wide_supported", &k_bdaln_wide_supported);
   m.def("bdaln_fwd", &k_bdaln_fwd);

@@ -827,11 +827,25 @@ int colsum(const void* x, void* out, float* ws, int64_t rows, int cols, int xdt,
 // ---------------------------------------------------------------------------
 template <typename T>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ slabs, T* __restrict__ out,
-                                                            int64_t n, int nsplit) {
+                                                            int64_t n, int nsplit, int accumulate) {
+  // accumulate (fp32 out only): out += sum of the slabs — the weight gradient of one micro-batch
+  // added into an fp32 main_grad without a separate add pass
   const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
   if (i >= n) return;
   if (i + 8 <= n) {
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if constexpr (sizeof(T) == 4) {
+      if (accumulate) {
+        float a[4], b[4];
+        load_f<float, 4>(reinterpret_cast<const float*>(out) + i, a);
+        load_f<float, 4>(reinterpret_cast<const float*>(out) + i + 4, b);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          acc[e] = a[e];
+          acc[4 + e] = b[e];
+        }
+      }
+    }
     for (int s = 0; s < nsplit; ++s) {
       float a[4], b[4];
       load_f<float, 4>(slabs + (int64_t)s * n + i, a);
@@ -851,22 +865,24 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
     }
   } else {
     for (int64_t j = i; j < n; ++j) {
-      float acc = 0.f;
+      float acc = (sizeof(T) == 4 && accumulate) ? to_f(out[j]) : 0.f;
       for (int s = 0; s < nsplit; ++s) acc += slabs[(int64_t)s * n + j];
       out[j] = from_f<T>(acc);
     }
   }
 }
 
-int splitk_reduce(const float* slabs, void* out, int64_t n, int nsplit, int odt, hipStream_t s) {
+int splitk_reduce(const float* slabs, void* out, int64_t n, int nsplit, int odt, hipStream_t s, int accumulate) {
   if (n == 0) return 0;
+  if (accumulate && odt != kF32) return -2;
   const unsigned grid = (unsigned)((n / 8 + 256) / 256);
   if (odt == kF32)
-    hipLaunchKernelGGL((splitk_reduce_kernel<float>), dim3(grid), dim3(256), 0, s, slabs, (float*)out, n, nsplit);
+    hipLaunchKernelGGL((splitk_reduce_kernel<float>), dim3(grid), dim3(256), 0, s, slabs, (float*)out, n, nsplit,
+                       accumulate);
   else if (odt == kF16)
-    hipLaunchKernelGGL((splitk_reduce_kernel<f16>), dim3(grid), dim3(256), 0, s, slabs, (f16*)out, n, nsplit);
+    hipLaunchKernelGGL((splitk_reduce_kernel<f16>), dim3(grid), dim3(256), 0, s, slabs, (f16*)out, n, nsplit, 0);
   else
-    hipLaunchKernelGGL((splitk_reduce_kernel<bf16>), dim3(grid), dim3(256), 0, s, slabs, (bf16*)out, n, nsplit);
+    hipLaunchKernelGGL((splitk_reduce_kernel<bf16>), dim3(grid), dim3(256), 0, s, slabs, (bf16*)out, n, nsplit, 0);
   return (int)hipGetLastError();
 }
 

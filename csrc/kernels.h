@@ -129,7 +129,8 @@ int bias_dropout_add_bwd(const void* dy, void* dx, void* db, float* ws, int64_t 
                          uint64_t seed, uint64_t offset, uint32_t thresh, float scale, int xdt, int bdt,
                          hipStream_t s);
 int colsum(const void* x, void* out, float* ws, int64_t rows, int cols, int xdt, int odt, hipStream_t s);
-int splitk_reduce(const float* slabs, void* out, int64_t n, int nsplit, int odt, hipStream_t s);
+int splitk_reduce(const float* slabs, void* out, int64_t n, int nsplit, int odt, hipStream_t s,
+                  int accumulate = 0);
 int64_t colsum_parts(int64_t rows);
 int bdaln_supported(int cols);
 int bdaln_wide_supported(int cols);  // 2056..4096 columns (bdaln fwd/bwd only, not the embedding block)

@@ -1,0 +1,96 @@
+"""DDP fp32_main_grad mode on CPU/gloo (world 2): a bf16 model accumulates 8 micro-batches under
+no_sync(); every parameter's gradient lives in an fp32 ``main_grad`` (views of fp32 buckets),
+``.grad`` stays None, the last micro-batch's backward all-reduces the fp32 buckets, and the
+result equals the fp32 sum of the per-micro-batch gradients averaged over ranks (where plain
+bf16 ``.grad`` accumulation would have rounded after every add). The fused optimizer then
+consumes main_grad and zero_grad zero-fills it. GPU path (fused fp32-accumulating weight-gradient
+GEMMs): tests/test_main_grad_gpu.py."""
+import os
+import socket
+import traceback
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.set_num_threads(1)
+        from apex.optimizers import FusedAdam
+        from apex.parallel import DistributedDataParallel as DDP
+
+        torch.manual_seed(0)
+        net = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.Tanh(), torch.nn.Linear(32, 8)).to(torch.bfloat16)
+        ref_params = [p.detach().clone() for p in net.parameters()]
+        model = DDP(net, message_size=200, fp32_main_grad=True)
+        for p in net.parameters():
+            assert p.main_grad.dtype == torch.float32 and p.grad is None
+        g = torch.Generator().manual_seed(5)
+        xs = [torch.randn(world * 4, 16, generator=g).to(torch.bfloat16) for _ in range(8)]
+        # reference: fp32 sum of each micro-batch's bf16 gradient, averaged over ranks
+        ref = [torch.zeros(p.shape, dtype=torch.float32) for p in net.parameters()]
+        twin = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.Tanh(), torch.nn.Linear(32, 8)).to(torch.bfloat16)
+        with torch.no_grad():
+            for tp, rp in zip(twin.parameters(), ref_params):
+                tp.copy_(rp)
+        for mb, x in enumerate(xs):
+            for r in range(world):
+                twin.zero_grad()
+                twin(x[r * 4:(r + 1) * 4]).float().pow(2).sum().backward()
+                for a, tp in zip(ref, twin.parameters()):
+                    a.add_(tp.grad.float() / world)
+        for mb, x in enumerate(xs):
+            last = mb == len(xs) - 1
+            ctx = model.no_sync() if not last else torch.autograd.graph.saved_tensors_hooks(lambda t: t, lambda t: t)
+            with ctx:
+                model(x[rank * 4:(rank + 1) * 4]).float().pow(2).sum().backward()
+            for p in net.parameters():
+                assert p.grad is None
+        for p, a in zip(net.parameters(), ref):
+            torch.testing.assert_close(p.main_grad, a, rtol=1e-5, atol=1e-5)
+        # bf16 accumulation of the same micro-batch gradients differs (rounding at every add)
+        acc16 = [torch.zeros(p.shape, dtype=torch.bfloat16) for p in net.parameters()]
+        for x in xs:
+            for r in range(world):
+                twin.zero_grad()
+                twin(x[r * 4:(r + 1) * 4]).float().pow(2).sum().backward()
+                for a, tp in zip(acc16, twin.parameters()):
+                    a.add_(tp.grad / world)
+        worst16 = max(float((a.float() - r_).abs().max()) for a, r_ in zip(acc16, ref))
+        worst32 = max(float((p.main_grad - r_).abs().max()) for p, r_ in zip(net.parameters(), ref))
+        assert worst32 < worst16, (worst32, worst16)
+        opt = FusedAdam(net.parameters(), lr=1e-3)
+        before = [p.detach().clone() for p in net.parameters()]
+        opt.step()
+        assert any(not torch.equal(b, p.detach()) for b, p in zip(before, net.parameters()))
+        opt.zero_grad()
+        assert all(float(p.main_grad.abs().max()) == 0.0 for p in net.parameters())
+        q.put((rank, "ok"))
+    except Exception:
+        q.put((rank, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_fp32_main_grad_accumulation():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=180) for _ in ps]
+    for p in ps:
+        p.join(timeout=30)
+    assert all(r[1] == "ok" for r in res), res
