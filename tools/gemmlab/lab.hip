@@ -63,11 +63,11 @@ struct Bufs {
 
 typedef void (*Launch)(const Bufs&, int epi, hipStream_t);
 
-template <int EPI>
+template <int EPI, int DBG = 0, int STAGGER = 0>
 void launch_old(const Bufs& b, hipStream_t s) {
   const int tiles = ((b.M + 255) / 256) * ((b.N + 255) / 256);
-  hipLaunchKernelGGL((gemm_nt_kernel<bf16, EPI, false, false>), dim3(tiles), dim3(512), 0, s, b.A, b.B, b.C, b.M, b.N,
-                     b.K, (int64_t)b.K, (int64_t)b.K, (int64_t)b.N, b.bias, b.aux, (int64_t)b.N, b.aux_out, b.part, 0,
+  hipLaunchKernelGGL((gemm_nt_kernel<bf16, EPI, false, false, bf16, -1, -1, DBG>), dim3(tiles), dim3(512), 0, s, b.A, b.B, b.C, b.M, b.N,
+                     b.K, (int64_t)b.K, (int64_t)b.K, (int64_t)b.N, b.bias, b.aux, (int64_t)b.N, b.aux_out, b.part, STAGGER,
                      nullptr, nullptr);
 }
 template <int EPI, int DBG = 0>
@@ -78,17 +78,35 @@ void launch_w4(const Bufs& b, hipStream_t s) {
 }
 
 template <int EPI>
+void launch_w2g(const Bufs& b, hipStream_t s) {
+  const int tiles = ((b.M + 255) / 256) * ((b.N + 127) / 128);
+  hipLaunchKernelGGL((gemm_w2g_kernel<bf16, EPI, false>), dim3(tiles), dim3(256), 0, s, b.A, b.B, b.C, b.M, b.N, b.K,
+                     (int64_t)b.K, (int64_t)b.K, (int64_t)b.N, b.bias, b.aux, (int64_t)b.N, b.aux_out, b.part);
+}
+
+template <int EPI>
 void run_epi(Bufs& b, int rounds, int reps, hipStream_t s) {
   struct V {
     const char* name;
     void (*fn)(const Bufs&, hipStream_t);
   };
-  std::vector<V> vs = {{"w8", launch_old<EPI>}, {"w4", launch_w4<EPI>}, {"w4r", launch_w4<EPI, 256>}};
+  std::vector<V> vs = {{"w8", launch_old<EPI>}, {"w2g", launch_w2g<EPI>}};
+  if (getenv("LAB_W4")) {
+    vs.push_back({"w4", launch_w4<EPI>});
+    vs.push_back({"w4r", launch_w4<EPI, 256>});
+  }
   if (getenv("LAB_DBG")) {
-    vs.push_back({"w4_noglds", launch_w4<EPI, 32>});
-    vs.push_back({"w4_nobar", launch_w4<EPI, 64>});
-    vs.push_back({"w4_nodsread", launch_w4<EPI, 128>});
-    vs.push_back({"w4_nomem", launch_w4<EPI, 32 + 64 + 128>});
+    vs.push_back({"w8_noglds", launch_old<EPI, 32>});
+    vs.push_back({"w8_nobar", launch_old<EPI, 64>});
+    vs.push_back({"w8_nodsread", launch_old<EPI, 128>});
+    vs.push_back({"w8_nomem", launch_old<EPI, 32 + 64 + 128>});
+    vs.push_back({"w8_noepi", launch_old<EPI, 512>});
+  }
+  if (getenv("LAB_STAGGER")) {
+    vs.push_back({"w8_st1", launch_old<EPI, 0, 1>});
+    vs.push_back({"w8_st2", launch_old<EPI, 0, 2>});
+    vs.push_back({"w8_st3", launch_old<EPI, 0, 3>});
+    vs.push_back({"w8_st5", launch_old<EPI, 0, 5>});
   }
   const int64_t MN = (int64_t)b.M * b.N;
   float* dmax;
