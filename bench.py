@@ -51,6 +51,10 @@ def parse():
     ap.add_argument("--fp8", action="store_true",
                     help="extra pass: the same step with amp fp8=True (NOT the headline: reported under extra.fp8)")
     ap.add_argument("--fp8-steps", type=int, default=10)
+    ap.add_argument("--fp16", action="store_true",
+                    help="extra pass: the same step as amp O2 fp16 with DYNAMIC loss scaling (the reference's O2; "
+                         "times the device-side overflow check / skip path; reported under extra.fp16)")
+    ap.add_argument("--fp16-steps", type=int, default=10)
     # DDP bucket sizes (elements): at N>1 chosen by an in-job probe of the communicator unless
     # given here (apex.parallel.preflight.select_bucket_sizes); at N=1 there is no communication
     ap.add_argument("--message-size", type=int,
@@ -61,7 +65,8 @@ def parse():
     return ap.parse_args()
 
 
-def build(env, cfg, fp32, message_size, fp8=False, first_bucket_size=None, fp32_allreduce=False):
+def build(env, cfg, fp32, message_size, fp8=False, first_bucket_size=None, fp32_allreduce=False,
+          half=torch.bfloat16):
     from apex import amp
     from apex.amp._amp_state import _amp_state
     from apex.models.bert import BertForPreTraining, param_groups_for_lamb
@@ -76,8 +81,8 @@ def build(env, cfg, fp32, message_size, fp8=False, first_bucket_size=None, fp32_
     if fp32:
         model, opt = amp.initialize(model, opt, opt_level="O0", verbosity=0)
     else:
-        model, opt = amp.initialize(model, opt, opt_level="O2", cast_model_type=torch.bfloat16,
-                                    verbosity=0, fp8=fp8)
+        kw = {"loss_scale": "dynamic"} if half == torch.float16 else {}
+        model, opt = amp.initialize(model, opt, opt_level="O2", cast_model_type=half, verbosity=0, fp8=fp8, **kw)
     model = DDP(model, message_size=message_size, first_bucket_size=first_bucket_size, comm_timing=True,
                 allreduce_always_fp32=fp32_allreduce)
     return model, opt
@@ -211,6 +216,24 @@ def main():
 
         _fp8.disable()
         del model, opt, batches, f8_loss
+        gc.collect()
+        torch.cuda.empty_cache()
+    if args.fp16 and not args.fp32_only:
+        # amp O2 fp16 with dynamic loss scaling (reference semantics: /root/reference/apex/amp/scaler.py:20-55);
+        # the overflow check + skip decision stay on the device (no host sync in the timed steps)
+        from apex.amp._amp_state import _amp_state
+
+        model, opt = build(env, cfg, False, args.message_size, first_bucket_size=first_bucket, half=torch.float16)
+        batches = batches_for(args.batch)
+        h_el, h_loss = time_steps(env, make_step(model, opt, batches, 0), args.fp16_steps, 3)
+        h_ms = max_over_ranks(env, h_el / args.fp16_steps * 1000.0)
+        sc = _amp_state.loss_scalers[0]
+        extra["fp16"] = {"ms_per_step": round(h_ms, 2), "seq_per_s": round(args.batch * world / h_ms * 1000.0, 2),
+                         "speedup_vs_bf16": round(ms / h_ms, 3) if not args.fp32_only else None,
+                         "final_loss": round(float(h_loss.float().item()), 4),
+                         "final_loss_scale": sc.loss_scale(), "steps": args.fp16_steps,
+                         "config": "amp O2 fp16, dynamic loss scale (init 2^16, window 2000), FusedLAMB"}
+        del model, opt, batches, h_loss
         gc.collect()
         torch.cuda.empty_cache()
     if world > 1 and not args.fp32_only:
