@@ -15,10 +15,13 @@ Every bf16/fp16 device call runs the MFMA flash-attention kernels in apex._C
   (True = attend) and becomes a 0 / -inf bias;
 * ``k_lens``: per-batch valid key lengths (right padding) skip whole key tiles.
 
-The reference composition (``attention_reference``: matmul -> softmax in fp32 -> dropout ->
-matmul) runs on CPU tensors, for fp32 inputs, head dims > 256, and when ``attn_bias`` itself
-requires a gradient (the kernels treat the bias as a constant). ``APEX_ATTN_BACKEND=reference``
-forces it (A/B, numerics checks).
+Device calls the flash kernels do not take — fp32 inputs, head dims > 256, an ``attn_bias`` that
+itself requires a gradient (the kernels treat the bias as a constant) — run the query-blocked
+memory-efficient path (``chunked.chunked_attention``: O(S * block) memory, backward by
+recomputation from the saved log-sum-exp, bias gradient = the score gradient), never the O(S^2)
+composition. The reference composition (``attention_reference``: matmul -> softmax in fp32 ->
+dropout -> matmul) runs on CPU tensors; ``APEX_ATTN_BACKEND=reference`` forces it (A/B, numerics
+checks).
 """
 from __future__ import annotations
 
@@ -120,6 +123,14 @@ def attention_packed(qkv, attn_bias=None, dropout_p=0.0, causal=False, scale=Non
         o = flash.flash_attention_packed(_pad_last(qkv, dp), dropout_p, causal, scale, k_lens, bias)
         return o[..., :d]
     q, k, v = qkv.unbind(2)
+    return _fallback(q, k, v, attn_bias, dropout_p, causal, scale, k_lens)
+
+
+def _fallback(q, k, v, attn_bias, dropout_p, causal, scale, k_lens):
+    if q.is_cuda and os.environ.get("APEX_ATTN_BACKEND", "native") != "reference":
+        from .chunked import chunked_attention
+
+        return chunked_attention(q, k, v, attn_bias, dropout_p, causal, scale, k_lens)
     return attention_reference(q, k, v, attn_bias, dropout_p, causal, scale, k_lens)
 
 
@@ -137,4 +148,4 @@ def attention(q, k, v, attn_bias=None, dropout_p=0.0, causal=False, scale=None, 
         o = flash.flash_attention(_pad_last(q, dp), _pad_last(k, dp), _pad_last(v, dp), dropout_p, causal, scale,
                                   k_lens, bias)
         return o[..., :d]
-    return attention_reference(q, k, v, attn_bias, dropout_p, causal, scale, k_lens)
+    return _fallback(q, k, v, attn_bias, dropout_p, causal, scale, k_lens)
