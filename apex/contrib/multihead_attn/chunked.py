@@ -21,7 +21,7 @@ import math
 import torch
 
 
-def _block_rows(B, H, Sk, budget_bytes=256 << 20):
+def _block_rows(B, H, Sk, budget_bytes=64 << 20):
     per_row = max(1, B * H * Sk * 4 * 4)  # ~4 fp32 [B, H, rows, Sk] temporaries alive per block
     rows = max(16, budget_bytes // per_row)
     return int(min(1024, 1 << (int(rows).bit_length() - 1)))

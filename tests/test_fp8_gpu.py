@@ -357,5 +357,5 @@ def test_state_dict_roundtrip(fp8_off):
     fp8.disable()
     st = fp8.state()
     st.load_state_dict(sd, lin)
-    s = st.slots[(id(lin.weight), "x")]
+    s = st.slots[(st.key_of(lin.weight), "x")]
     assert float(st.scale[s]) == scale_x and s not in st._fresh
