@@ -98,9 +98,26 @@ def accumulate_main_grad(mg, dy2, x2):
         mg.add_(dy2.t().float().mm(x2.float()))
         return mg
     s = _wgrad_splits(M, N, K)
+    if s == 1:
+        # enough output tiles to fill the chip: hipBLASLt accumulates straight into main_grad
+        # (fp32 C = D, beta = 1) — no slab round trip (tools/main_grad_ab.py, Megatron H2560
+        # shapes: 358 vs 441 us at 7680x2560, 529 vs 562 us at 2560x10240; same fp32 error)
+        torch.addmm(mg, dy2.t(), x2, out_dtype=torch.float32, out=mg)
+        return mg
     slabs = torch.bmm(dy2.view(s, M // s, N).transpose(1, 2), x2.view(s, M // s, K), out_dtype=torch.float32)
     _ext.require().splitk_reduce(slabs, torch.float32, mg, accumulate=True)
     return mg
+
+
+def main_grad_placeholder(param):
+    """The gradient a fused producer hands autograd after accumulating into ``param.main_grad``:
+    a storage-less ZeroTensor, so the parameter's AccumulateGrad (and the DDP readiness hook
+    behind it) still fires without a fill kernel or a parameter-sized allocation. When the
+    parameter has other uses (a tied embedding: the lookup's dense gradient), autograd sums them
+    with it and the hook sees an ordinary tensor, which it adds into main_grad — only a bare
+    placeholder is dropped (apex.parallel.DistributedDataParallel._grad_hook)."""
+    param.grad_added_to_main_grad = True
+    return torch._efficientzerotensor(param.shape, dtype=param.dtype, device=param.device)
 
 
 def _wgrad(dy2, x2, out=None, param=None):
@@ -108,13 +125,12 @@ def _wgrad(dy2, x2, out=None, param=None):
     ``out`` when given (a gradient-bucket slot), or into ``param``'s bucket slot
     (apex.parallel.grad_target). When ``param`` carries an fp32 ``main_grad`` (DDP
     fp32_main_grad mode) the gradient is accumulated there instead and a placeholder is returned
-    for autograd (the DDP hook drops it: ``param.grad_added_to_main_grad``)."""
+    for autograd (main_grad_placeholder: the DDP hook drops it)."""
     if param is not None:
         mg = getattr(param, "main_grad", None)
         if mg is not None:
             accumulate_main_grad(mg, dy2, x2)
-            param.grad_added_to_main_grad = True
-            return torch.empty_like(param)
+            return main_grad_placeholder(param)
         if out is None:
             out = _gt(param)
     M, N = dy2.shape

@@ -419,7 +419,8 @@ class DistributedDataParallel(Module):
         for i, p in enumerate(self._params):
             if self.fp32_main_grad:
                 if p.grad is not None:  # a gradient produced outside the hooks
-                    p.main_grad.add_(p.grad)
+                    if not p.grad._is_zerotensor():
+                        p.main_grad.add_(p.grad)
                     p.grad = None
             else:
                 self._ensure_view(i, p)
@@ -441,10 +442,13 @@ class DistributedDataParallel(Module):
     # ------------------------------------------------------------ hooks
     def _grad_hook(self, p):
         if self.fp32_main_grad:
-            if getattr(p, "grad_added_to_main_grad", False):
-                p.grad_added_to_main_grad = False  # a fused producer accumulated it already
-            elif p.grad is not None:
-                p.main_grad.add_(p.grad)
+            # a bare ZeroTensor placeholder: a fused producer accumulated into main_grad already;
+            # anything else (an unfused producer, or a tied weight's other uses summed with the
+            # placeholder by autograd) is added here
+            g = p.grad
+            if g is not None and not g._is_zerotensor():
+                p.main_grad.add_(g)
+            p.grad_added_to_main_grad = False
             p.grad = None
         if not self._allreduce_enabled:
             return

@@ -143,8 +143,7 @@ class LinearWithGradAccumulationAndAsyncCommunication(torch.autograd.Function):
             if getattr(weight, "_apex_main_flat", None) is not None:
                 # main_grad owned by apex DDP (fp32_main_grad): its hook must still see this
                 # parameter become ready -> a placeholder gradient it drops
-                weight.grad_added_to_main_grad = True
-                dw = torch.empty_like(weight)
+                dw = fops.main_grad_placeholder(weight)
             else:
                 dw = None
         else:

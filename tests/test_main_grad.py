@@ -94,3 +94,78 @@ def test_fp32_main_grad_accumulation():
     for p in ps:
         p.join(timeout=30)
     assert all(r[1] == "ok" for r in res), res
+
+
+class _FusedAccum(torch.autograd.Function):
+    """Stands in for a fused weight-gradient producer on the CPU: accumulates dW into
+    weight.main_grad and hands autograd the ZeroTensor placeholder (apex.ops.fused)."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return x @ w.t()
+
+    @staticmethod
+    def backward(ctx, dy):
+        from apex.ops.fused import main_grad_placeholder
+
+        x, w = ctx.saved_tensors
+        w.main_grad.add_(dy.t().float() @ x.float())
+        return dy @ w, main_grad_placeholder(w)
+
+
+def _tied_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.set_num_threads(1)
+        from apex.parallel import DistributedDataParallel as DDP
+
+        class Tied(torch.nn.Module):
+            def __init__(self):
+                super().__init__()
+                self.emb = torch.nn.Embedding(12, 8)
+
+            def forward(self, ids):
+                h = self.emb(ids)  # lookup: an ordinary dense gradient for the shared weight
+                return _FusedAccum.apply(h, self.emb.weight)  # tied head: fused main_grad producer
+
+        torch.manual_seed(0)
+        net = Tied()
+        twin = Tied()
+        twin.load_state_dict(net.state_dict())
+        model = DDP(net, message_size=50, fp32_main_grad=True)
+        g = torch.Generator().manual_seed(1)
+        ids = [torch.randint(0, 12, (world * 3,), generator=g) for _ in range(3)]
+        for mb, x in enumerate(ids):
+            with (model.no_sync() if mb < len(ids) - 1 else torch.enable_grad()):
+                model(x[rank * 3:(rank + 1) * 3]).pow(2).sum().backward()
+        ref = torch.zeros(12, 8)
+        for x in ids:
+            for r in range(world):
+                twin.zero_grad()
+                out = twin.emb(x[r * 3:(r + 1) * 3]) @ twin.emb.weight.t()
+                out.pow(2).sum().backward()
+                ref += twin.emb.weight.grad / world
+        torch.testing.assert_close(net.emb.weight.main_grad, ref, rtol=1e-5, atol=1e-5)
+        assert net.emb.weight.grad is None
+        q.put((rank, "ok"))
+    except Exception:
+        q.put((rank, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_fp32_main_grad_tied_weight_keeps_other_uses():
+    """A weight with a fused main_grad producer AND another use (tied embedding / LM head): the
+    other use's gradient is summed with the placeholder by autograd and must reach main_grad."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_tied_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=180) for _ in ps]
+    for p in ps:
+        p.join(timeout=30)
+    assert all(r[1] == "ok" for r in res), res
