@@ -50,6 +50,51 @@ __device__ __forceinline__ void store_f(T* __restrict__ p, const float (&in)[N])
   *reinterpret_cast<Pack<T, N>*>(p) = pk;
 }
 
+// Non-temporal variants for single-pass streams (optimizer states, gradients): the loads and
+// stores carry the nt hint, so a multi-GB sweep does not churn the L2 / Infinity Cache lines
+// the next kernel wants. Measured on the Adam stream (tools/bwlab/adam_lab.hip, 512 M params):
+// nt loads + stores with 4 lane-contiguous 16-B groups in flight 6.42 TB/s vs 5.84 plain.
+template <typename T, int N>
+__device__ __forceinline__ void load_f_nt(const T* __restrict__ p, float (&out)[N]) {
+  constexpr int B = (int)sizeof(T) * N;
+  if constexpr (B == 16 || B == 8) {
+    typedef unsigned V __attribute__((ext_vector_type(B / 4)));
+    const V v = __builtin_nontemporal_load(reinterpret_cast<const V*>(p));
+    Pack<T, N> pk;
+    __builtin_memcpy(&pk, &v, B);
+#pragma unroll
+    for (int i = 0; i < N; ++i) out[i] = to_f(pk.v[i]);
+  } else if constexpr (B == 4) {
+    const unsigned v = __builtin_nontemporal_load(reinterpret_cast<const unsigned*>(p));
+    Pack<T, N> pk;
+    __builtin_memcpy(&pk, &v, 4);
+#pragma unroll
+    for (int i = 0; i < N; ++i) out[i] = to_f(pk.v[i]);
+  } else {
+    load_f<T, N>(p, out);
+  }
+}
+
+template <typename T, int N>
+__device__ __forceinline__ void store_f_nt(T* __restrict__ p, const float (&in)[N]) {
+  constexpr int B = (int)sizeof(T) * N;
+  Pack<T, N> pk;
+#pragma unroll
+  for (int i = 0; i < N; ++i) pk.v[i] = from_f<T>(in[i]);
+  if constexpr (B == 16 || B == 8) {
+    typedef unsigned V __attribute__((ext_vector_type(B / 4)));
+    V v;
+    __builtin_memcpy(&v, &pk, B);
+    __builtin_nontemporal_store(v, reinterpret_cast<V*>(p));
+  } else if constexpr (B == 4) {
+    unsigned v;
+    __builtin_memcpy(&v, &pk, 4);
+    __builtin_nontemporal_store(v, reinterpret_cast<unsigned*>(p));
+  } else {
+    *reinterpret_cast<Pack<T, N>*>(p) = pk;
+  }
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);

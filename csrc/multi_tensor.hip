@@ -6,8 +6,10 @@
 //   apex/fp16_utils/fp16util.py:93-129 master<->model copies
 //   apex/parallel/LARC.py:79-82        per-param host-synced norms
 // Design: one launch per op over a device-resident chunk table (multi_tensor.h).
-// 256-thread blocks (4 x wave64), 8 elements per lane per iteration (16 B for
-// 16-bit types), grid capped at 8 blocks/CU and grid-strided over chunks.
+// 256-thread blocks (4 x wave64), grid capped at 8 blocks/CU and grid-strided over chunks; the
+// single-pass kernels (scale, l2norm, SGD, Adam, LAMB) sweep a chunk with stream_for (lane-
+// contiguous 4-element groups, 4 in flight per lane, non-temporal state traffic), the rest with
+// chunk_for (8 contiguous elements per lane).
 #include <type_traits>
 
 #include "common.h"
@@ -46,6 +48,31 @@ __device__ __forceinline__ void chunk_for(const MTMeta& m, int64_t n, Body&& bod
   for (int64_t i = nv + threadIdx.x; i < n; i += blockDim.x) body(I1{}, i);
 }
 
+// Streaming sweep of one chunk for the single-pass optimizer / scaler kernels: each lane owns
+// 4-element groups laid out lane-contiguously (one wave instruction = 1 KB of fp32 contiguous,
+// not every other 16 B of a 2 KB span), kStreamU groups per lane per iteration with all their
+// loads issued before any store (aliasing keeps the compiler from hoisting the next
+// iteration's loads above this one's stores, so the in-flight bytes have to be explicit).
+// body(IG<NG>, IG<NE>, j0, stride): NG groups of NE elements at j0 + g * stride, g < NG.
+// tools/bwlab/adam_lab.hip: the Adam stream at 6.42 TB/s with nt loads/stores (= the read-only
+// ceiling of the same four fp32 streams) vs 5.84 for the 8-contiguous-elements layout.
+template <int G>
+using IG = std::integral_constant<int, G>;
+constexpr int kStreamU = 4;
+constexpr int kGroup = 4;
+
+template <typename Body>
+__device__ __forceinline__ void stream_for(const MTMeta& m, int64_t n, Body&& body) {
+  const int64_t nv = m.aligned ? (n & ~int64_t(kGroup - 1)) : 0;
+  constexpr int64_t kStride = (int64_t)kBlock * kGroup;
+  constexpr int64_t kStep = kStride * kStreamU;
+  const int64_t t4 = (int64_t)threadIdx.x * kGroup;
+  int64_t base = 0;
+  for (; base + kStep <= nv; base += kStep) body(IG<kStreamU>{}, IG<kGroup>{}, base + t4, kStride);
+  for (int64_t j = base + t4; j < nv; j += kStride) body(IG<1>{}, IG<kGroup>{}, j, 0);
+  for (int64_t j = nv + threadIdx.x; j < n; j += kBlock) body(IG<1>{}, IG<1>{}, j, 0);
+}
+
 __device__ __forceinline__ float read_scale(const float* p, float v) { return p ? *p : v; }
 
 static inline int grid_for(int nchunks) {
@@ -64,16 +91,20 @@ __global__ void __launch_bounds__(kBlock) scale_kernel(MTMeta m, const float* sp
     const ChunkView cv = chunk_view(m, c);
     const TI* in = (const TI*)m.ptr(0, cv.t) + cv.start;
     TO* out = (TO*)m.ptr(1, cv.t) + cv.start;
-    chunk_for(m, cv.n, [&](auto NC, int64_t i) {
-      constexpr int N = decltype(NC)::value;
-      float x[N];
-      load_f<TI, N>(in + i, x);
+    stream_for(m, cv.n, [&](auto NGc, auto NEc, int64_t j0, int64_t st) {
+      constexpr int NG = decltype(NGc)::value, NE = decltype(NEc)::value;
+      float x[NG][NE];
 #pragma unroll
-      for (int k = 0; k < N; ++k) {
-        bad |= !__builtin_isfinite(x[k]);
-        x[k] *= s;
-      }
-      store_f<TO, N>(out + i, x);
+      for (int u = 0; u < NG; ++u) load_f_nt<TI, NE>(in + j0 + u * st, x[u]);
+#pragma unroll
+      for (int u = 0; u < NG; ++u)
+#pragma unroll
+        for (int k = 0; k < NE; ++k) {
+          bad |= !__builtin_isfinite(x[u][k]);
+          x[u][k] *= s;
+        }
+#pragma unroll
+      for (int u = 0; u < NG; ++u) store_f<TO, NE>(out + j0 + u * st, x[u]);
     });
   }
   if (bad && overflow) *overflow = 1;
@@ -120,15 +151,18 @@ __global__ void __launch_bounds__(kBlock) sumsq_kernel(MTMeta m, int list, float
     const ChunkView cv = chunk_view(m, c);
     const T* x = (const T*)m.ptr(list, cv.t) + cv.start;
     float acc = 0.f;
-    chunk_for(m, cv.n, [&](auto NC, int64_t i) {
-      constexpr int N = decltype(NC)::value;
-      float v[N];
-      load_f<T, N>(x + i, v);
+    stream_for(m, cv.n, [&](auto NGc, auto NEc, int64_t j0, int64_t st) {
+      constexpr int NG = decltype(NGc)::value, NE = decltype(NEc)::value;
+      float v[NG][NE];
 #pragma unroll
-      for (int k = 0; k < N; ++k) {
-        bad |= !__builtin_isfinite(v[k]);
-        acc += v[k] * v[k];
-      }
+      for (int u = 0; u < NG; ++u) load_f<T, NE>(x + j0 + u * st, v[u]);
+#pragma unroll
+      for (int u = 0; u < NG; ++u)
+#pragma unroll
+        for (int k = 0; k < NE; ++k) {
+          bad |= !__builtin_isfinite(v[u][k]);
+          acc += v[u][k] * v[u][k];
+        }
     });
     acc = block_sum(acc, red);
     if (threadIdx.x == 0) partial[c] = acc;
@@ -176,26 +210,34 @@ __global__ void __launch_bounds__(kBlock) sgd_kernel(MTMeta m, SgdArgs a) {
     P* p = (P*)m.ptr(1, cv.t) + cv.start;
     float* mom = a.momentum != 0.f ? (float*)m.ptr(2, cv.t) + cv.start : nullptr;
     C* cp = has_copy ? (C*)m.ptr(3, cv.t) + cv.start : nullptr;
-    chunk_for(m, cv.n, [&](auto NC, int64_t i) {
-      constexpr int N = decltype(NC)::value;
-      float gv[N], pv[N], mv[N];
-      load_f<G, N>(g + i, gv);
-      load_f<P, N>(p + i, pv);
-      if (mom && !a.first_run) load_f<float, N>(mom + i, mv);
+    stream_for(m, cv.n, [&](auto NGc, auto NEc, int64_t j0, int64_t st) {
+      constexpr int NG = decltype(NGc)::value, NE = decltype(NEc)::value;
+      float gv[NG][NE], pv[NG][NE], mv[NG][NE];
 #pragma unroll
-      for (int k = 0; k < N; ++k) {
-        float gg = gv[k] * gs;
-        if (a.wd != 0.f && !a.wd_after_momentum) gg += a.wd * pv[k];
-        if (mom) {
-          mv[k] = a.first_run ? gg : a.momentum * mv[k] + (1.f - a.dampening) * gg;
-          gg = a.nesterov ? gg + a.momentum * mv[k] : mv[k];
-        }
-        if (a.wd != 0.f && a.wd_after_momentum) gg += a.wd * pv[k];
-        pv[k] -= a.lr * gg;
+      for (int u = 0; u < NG; ++u) {
+        load_f_nt<G, NE>(g + j0 + u * st, gv[u]);
+        load_f_nt<P, NE>(p + j0 + u * st, pv[u]);
+        if (mom && !a.first_run) load_f_nt<float, NE>(mom + j0 + u * st, mv[u]);
       }
-      store_f<P, N>(p + i, pv);
-      if (mom) store_f<float, N>(mom + i, mv);
-      if (cp) store_f<C, N>(cp + i, pv);
+#pragma unroll
+      for (int u = 0; u < NG; ++u)
+#pragma unroll
+        for (int k = 0; k < NE; ++k) {
+          float gg = gv[u][k] * gs;
+          if (a.wd != 0.f && !a.wd_after_momentum) gg += a.wd * pv[u][k];
+          if (mom) {
+            mv[u][k] = a.first_run ? gg : a.momentum * mv[u][k] + (1.f - a.dampening) * gg;
+            gg = a.nesterov ? gg + a.momentum * mv[u][k] : mv[u][k];
+          }
+          if (a.wd != 0.f && a.wd_after_momentum) gg += a.wd * pv[u][k];
+          pv[u][k] -= a.lr * gg;
+        }
+#pragma unroll
+      for (int u = 0; u < NG; ++u) {
+        store_f_nt<P, NE>(p + j0 + u * st, pv[u]);
+        if (mom) store_f_nt<float, NE>(mom + j0 + u * st, mv[u]);
+        if (cp) store_f<C, NE>(cp + j0 + u * st, pv[u]);
+      }
     });
   }
 }
@@ -232,28 +274,36 @@ __global__ void __launch_bounds__(kBlock) adam_kernel(MTMeta m, AdamArgs a) {
     float* mm = (float*)m.ptr(2, cv.t) + cv.start;
     float* vv = (float*)m.ptr(3, cv.t) + cv.start;
     C* cp = has_copy ? (C*)m.ptr(4, cv.t) + cv.start : nullptr;
-    chunk_for(m, cv.n, [&](auto NC, int64_t i) {
-      constexpr int N = decltype(NC)::value;
-      float gv[N], pv[N], mv[N], vv2[N];
-      load_f<G, N>(g + i, gv);
-      load_f<P, N>(p + i, pv);
-      load_f<float, N>(mm + i, mv);
-      load_f<float, N>(vv + i, vv2);
+    stream_for(m, cv.n, [&](auto NGc, auto NEc, int64_t j0, int64_t st) {
+      constexpr int NG = decltype(NGc)::value, NE = decltype(NEc)::value;
+      float gv[NG][NE], pv[NG][NE], mv[NG][NE], vq[NG][NE];
 #pragma unroll
-      for (int k = 0; k < N; ++k) {
-        float gg = gv[k] * gs;
-        if (!a.adamw && a.wd != 0.f) gg += a.wd * pv[k];
-        mv[k] = b1 * mv[k] + (1.f - b1) * gg;
-        vv2[k] = b2 * vv2[k] + (1.f - b2) * gg * gg;
-        const float denom = sqrtf(vv2[k] * rbc2) + a.eps;
-        float upd = (mv[k] * rbc1) / denom;
-        if (a.adamw && a.wd != 0.f) upd += a.wd * pv[k];
-        pv[k] -= a.lr * upd;
+      for (int u = 0; u < NG; ++u) {
+        load_f_nt<G, NE>(g + j0 + u * st, gv[u]);
+        load_f_nt<P, NE>(p + j0 + u * st, pv[u]);
+        load_f_nt<float, NE>(mm + j0 + u * st, mv[u]);
+        load_f_nt<float, NE>(vv + j0 + u * st, vq[u]);
       }
-      store_f<P, N>(p + i, pv);
-      store_f<float, N>(mm + i, mv);
-      store_f<float, N>(vv + i, vv2);
-      if (cp) store_f<C, N>(cp + i, pv);
+#pragma unroll
+      for (int u = 0; u < NG; ++u)
+#pragma unroll
+        for (int k = 0; k < NE; ++k) {
+          float gg = gv[u][k] * gs;
+          if (!a.adamw && a.wd != 0.f) gg += a.wd * pv[u][k];
+          mv[u][k] = b1 * mv[u][k] + (1.f - b1) * gg;
+          vq[u][k] = b2 * vq[u][k] + (1.f - b2) * gg * gg;
+          const float denom = sqrtf(vq[u][k] * rbc2) + a.eps;
+          float upd = (mv[u][k] * rbc1) / denom;
+          if (a.adamw && a.wd != 0.f) upd += a.wd * pv[u][k];
+          pv[u][k] -= a.lr * upd;
+        }
+#pragma unroll
+      for (int u = 0; u < NG; ++u) {
+        store_f_nt<P, NE>(p + j0 + u * st, pv[u]);
+        store_f_nt<float, NE>(mm + j0 + u * st, mv[u]);
+        store_f_nt<float, NE>(vv + j0 + u * st, vq[u]);
+        if (cp) store_f<C, NE>(cp + j0 + u * st, pv[u]);
+      }
     });
   }
 }
@@ -322,62 +372,34 @@ __global__ void __launch_bounds__(kBlock) lamb_stage1_kernel(MTMeta m, LambArgs 
     float* mm = (float*)m.ptr(2, cv.t) + cv.start;
     float* vv = (float*)m.ptr(3, cv.t) + cv.start;
     float sp = 0.f, su = 0.f;
-    auto body = [&](auto NC, int64_t i) {
-      constexpr int N = decltype(NC)::value;
-      float gv[N], pv[N], mv[N], vv2[N], u[N];
-      load_f<G, N>(g + i, gv);
-      load_f<P, N>(p + i, pv);
-      load_f<float, N>(mm + i, mv);
-      load_f<float, N>(vv + i, vv2);
+    stream_for(m, cv.n, [&](auto NGc, auto NEc, int64_t j0, int64_t st) {
+      constexpr int NG = decltype(NGc)::value, NE = decltype(NEc)::value;
+      float gv[NG][NE], pv[NG][NE], mv[NG][NE], vq[NG][NE];
 #pragma unroll
-      for (int k = 0; k < N; ++k) {
-        float gg = gv[k] * gs;
-        if (!a.adamw && a.wd != 0.f) gg += a.wd * pv[k];
-        mv[k] = b1 * mv[k] + b3 * gg;
-        vv2[k] = b2 * vv2[k] + (1.f - b2) * gg * gg;
-        u[k] = lamb_u(mv[k], vv2[k], pv[k], rbc1, rbc2, a);
-        sp += pv[k] * pv[k];
-        su += u[k] * u[k];
+      for (int u = 0; u < NG; ++u) {
+        load_f_nt<G, NE>(g + j0 + u * st, gv[u]);
+        load_f_nt<P, NE>(p + j0 + u * st, pv[u]);
+        load_f_nt<float, NE>(mm + j0 + u * st, mv[u]);
+        load_f_nt<float, NE>(vv + j0 + u * st, vq[u]);
       }
-      store_f<float, N>(mm + i, mv);
-      store_f<float, N>(vv + i, vv2);
-    };
-    // two vector groups per iteration with every load issued before the first store: the
-    // compiler cannot move the next group's loads above this group's stores (possible aliasing),
-    // so one group per iteration kept only one set of loads in flight per thread
-    const int64_t nv = m.aligned ? (cv.n & ~int64_t(7)) : 0;
-    const int64_t stride = (int64_t)blockDim.x * 8;
-    int64_t i = threadIdx.x * 8;
-    for (; i + stride < nv; i += 2 * stride) {
-      const int64_t j = i + stride;
-      float gv[2][8], pv[2][8], mv[2][8], vq[2][8];
-      load_f<G, 8>(g + i, gv[0]);
-      load_f<G, 8>(g + j, gv[1]);
-      load_f<P, 8>(p + i, pv[0]);
-      load_f<P, 8>(p + j, pv[1]);
-      load_f<float, 8>(mm + i, mv[0]);
-      load_f<float, 8>(mm + j, mv[1]);
-      load_f<float, 8>(vv + i, vq[0]);
-      load_f<float, 8>(vv + j, vq[1]);
 #pragma unroll
-      for (int h = 0; h < 2; ++h)
+      for (int u = 0; u < NG; ++u)
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          float gg = gv[h][k] * gs;
-          if (!a.adamw && a.wd != 0.f) gg += a.wd * pv[h][k];
-          mv[h][k] = b1 * mv[h][k] + b3 * gg;
-          vq[h][k] = b2 * vq[h][k] + (1.f - b2) * gg * gg;
-          const float u = lamb_u(mv[h][k], vq[h][k], pv[h][k], rbc1, rbc2, a);
-          sp += pv[h][k] * pv[h][k];
-          su += u * u;
+        for (int k = 0; k < NE; ++k) {
+          float gg = gv[u][k] * gs;
+          if (!a.adamw && a.wd != 0.f) gg += a.wd * pv[u][k];
+          mv[u][k] = b1 * mv[u][k] + b3 * gg;
+          vq[u][k] = b2 * vq[u][k] + (1.f - b2) * gg * gg;
+          const float uu = lamb_u(mv[u][k], vq[u][k], pv[u][k], rbc1, rbc2, a);
+          sp += pv[u][k] * pv[u][k];
+          su += uu * uu;
         }
-      store_f<float, 8>(mm + i, mv[0]);
-      store_f<float, 8>(mm + j, mv[1]);
-      store_f<float, 8>(vv + i, vq[0]);
-      store_f<float, 8>(vv + j, vq[1]);
-    }
-    for (; i < nv; i += stride) body(I8{}, i);
-    for (int64_t t = nv + threadIdx.x; t < cv.n; t += blockDim.x) body(I1{}, t);
+#pragma unroll
+      for (int u = 0; u < NG; ++u) {
+        store_f_nt<float, NE>(mm + j0 + u * st, mv[u]);
+        store_f_nt<float, NE>(vv + j0 + u * st, vq[u]);
+      }
+    });
     sp = block_sum(sp, red);
     su = block_sum(su, red);
     if (threadIdx.x == 0) {
@@ -404,43 +426,25 @@ __global__ void __launch_bounds__(kBlock) lamb_stage2_kernel(MTMeta m, LambArgs 
       const float pn = pnorm[cv.t], un = unorm[cv.t];
       if (pn != 0.f && un != 0.f) ratio = a.lr * (pn / un);
     }
-    auto body = [&](auto NC, int64_t i) {
-      constexpr int N = decltype(NC)::value;
-      float pv[N], mv[N], vv2[N];
-      load_f<P, N>(p + i, pv);
-      load_f<float, N>(mm + i, mv);
-      load_f<float, N>(vv + i, vv2);
+    stream_for(m, cv.n, [&](auto NGc, auto NEc, int64_t j0, int64_t st) {
+      constexpr int NG = decltype(NGc)::value, NE = decltype(NEc)::value;
+      float pv[NG][NE], mv[NG][NE], vq[NG][NE];
 #pragma unroll
-      for (int k = 0; k < N; ++k) pv[k] -= ratio * lamb_u(mv[k], vv2[k], pv[k], rbc1, rbc2, a);
-      store_f<P, N>(p + i, pv);
-      if (cp) store_f<C, N>(cp + i, pv);
-    };
-    // two vector groups per iteration, loads before stores (see stage 1)
-    const int64_t nv = m.aligned ? (cv.n & ~int64_t(7)) : 0;
-    const int64_t stride = (int64_t)blockDim.x * 8;
-    int64_t i = threadIdx.x * 8;
-    for (; i + stride < nv; i += 2 * stride) {
-      const int64_t j = i + stride;
-      float pv[2][8], mv[2][8], vq[2][8];
-      load_f<P, 8>(p + i, pv[0]);
-      load_f<P, 8>(p + j, pv[1]);
-      load_f<float, 8>(mm + i, mv[0]);
-      load_f<float, 8>(mm + j, mv[1]);
-      load_f<float, 8>(vv + i, vq[0]);
-      load_f<float, 8>(vv + j, vq[1]);
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int k = 0; k < 8; ++k) pv[h][k] -= ratio * lamb_u(mv[h][k], vq[h][k], pv[h][k], rbc1, rbc2, a);
-      store_f<P, 8>(p + i, pv[0]);
-      store_f<P, 8>(p + j, pv[1]);
-      if (cp) {
-        store_f<C, 8>(cp + i, pv[0]);
-        store_f<C, 8>(cp + j, pv[1]);
+      for (int u = 0; u < NG; ++u) {
+        load_f_nt<P, NE>(p + j0 + u * st, pv[u]);
+        load_f_nt<float, NE>(mm + j0 + u * st, mv[u]);
+        load_f_nt<float, NE>(vv + j0 + u * st, vq[u]);
       }
-    }
-    for (; i < nv; i += stride) body(I8{}, i);
-    for (int64_t t = nv + threadIdx.x; t < cv.n; t += blockDim.x) body(I1{}, t);
+#pragma unroll
+      for (int u = 0; u < NG; ++u)
+#pragma unroll
+        for (int k = 0; k < NE; ++k) pv[u][k] -= ratio * lamb_u(mv[u][k], vq[u][k], pv[u][k], rbc1, rbc2, a);
+#pragma unroll
+      for (int u = 0; u < NG; ++u) {
+        store_f_nt<P, NE>(p + j0 + u * st, pv[u]);
+        if (cp) store_f<C, NE>(cp + j0 + u * st, pv[u]);
+      }
+    });
   }
 }
 

@@ -87,10 +87,31 @@ def op_lamb(iters):
         p.grad = torch.randn_like(p) * 1e-3
     n = sum(p.numel() for p in ps)
     us = _time(lambda: opt.step(), iters)
-    # per parameter: read grad bf16 (2, twice: norm + update), fp32 master p, m, v (12); write p, m,
-    # v (12) and the bf16 model copy (2)
-    return [dict(op="fused_lamb_step", us=us, bytes=n * (4 + 12 + 12 + 2), params=n,
+    # per parameter: grad-norm pass reads the bf16 grad (2); stage 1 reads g, p, m, v (2 + 12) and
+    # writes m, v (8); stage 2 reads p, m, v (12) and writes p (4) + the bf16 model copy (2)
+    return [dict(op="fused_lamb_step", us=us, bytes=n * (2 + 14 + 8 + 12 + 6), params=n,
                  kernels="sumsq (grad norm) + lamb_stage1 + lamb_stage2")]
+
+
+def op_adam(iters):
+    """The Megatron GPT (H2560, 32 layers) Adam step: fp32 main_grad, fp32 master, fp32 m / v,
+    bf16 model copy — 30 B per parameter, one adam_kernel launch."""
+    from apex.multi_tensor_apply import multi_tensor_applier
+    from apex.multi_tensor_apply.ops import multi_tensor_adam
+
+    H = 2560
+    sizes = ([3 * H * H, 3 * H, H * H, H, 4 * H * H, 4 * H, 4 * H * H, H, H, H, H, H] * 32
+             + [50304 * H, 2048 * H, H, H])
+    gs = [torch.randn(s, device=DEV) * 1e-3 for s in sizes]
+    ps = [torch.randn(s, device=DEV) for s in sizes]
+    ms = [torch.zeros(s, device=DEV) for s in sizes]
+    vs = [torch.zeros(s, device=DEV) for s in sizes]
+    cs = [torch.empty(s, device=DEV, dtype=torch.bfloat16) for s in sizes]
+    noop = torch.zeros(1, dtype=torch.int32, device=DEV)
+    n = sum(sizes)
+    us = _time(lambda: multi_tensor_applier(multi_tensor_adam, noop, [gs, ps, ms, vs, cs], 1e-4, 0.9, 0.999, 1e-8,
+                                            1, 1, 1, 0.01), iters)
+    return [dict(op="fused_adam_step_megatron", us=us, bytes=n * 30, params=n, kernels="adam_kernel<f32,f32,bf16>")]
 
 
 def op_xent(iters):
@@ -140,7 +161,7 @@ def op_scale(iters):
     return [dict(op="multi_tensor_scale_bf16_to_fp32", us=us, bytes=n * 6, params=n, kernels="mt scale")]
 
 
-OPS = dict(ln=op_ln, bdaln=op_bdaln, lamb=op_lamb, xent=op_xent, syncbn=op_syncbn,
+OPS = dict(adam=op_adam, ln=op_ln, bdaln=op_bdaln, lamb=op_lamb, xent=op_xent, syncbn=op_syncbn,
            syncbn_nhwc=lambda it: op_syncbn(it, True), scale=op_scale)
 
 
