@@ -1,0 +1,358 @@
+"""Context parallelism: attention over a sequence sharded across a CP group.
+
+The reference has no sequence-length parallelism at all (its only sequence mechanism is
+the word LM's truncated BPTT, /root/reference/examples/word_language_model/main.py:119-124). This
+module adds the two standard long-context schemes on top of the flash-attention kernels
+(csrc/attention_impl.h) and torch.distributed (RCCL over xGMI on MI355X, gloo on CPU):
+
+* ``ring_attention``: every rank keeps its query shard; the K/V shards travel around the CP ring
+  (one P2P exchange per step, issued before that step's block attention so the transfer overlaps
+  the kernels). Partial results are merged exactly through their log-sum-exp. Backward replays the
+  ring: dQ stays home, the dK/dV partial of each K/V shard travels WITH that shard and arrives
+  back at its owner after the last step. Memory is O(S_local) per rank for any ring length.
+  Causal masking with the ``"zigzag"`` layout (rank r holds sequence chunks r and 2W-1-r of 2W) gives
+  every rank the same amount of work per step; ``"contiguous"`` (rank r holds chunk r) idles the
+  low ranks under a causal mask.
+* ``ulysses_attention``: two all-to-alls swap the sharded dimension from sequence to heads
+  ([B, S/W, H, D] -> [B, S, H/W, D]), attention runs on whole sequences for H/W heads, and the
+  inverse all-to-all restores the sequence sharding. On the 8-GPU xGMI full mesh every peer pair
+  has its own link, so all-to-all is the collective that loads all 7 links at once.
+
+Block math: on device (bf16/fp16, head dim 32..256 after padding) each block is one
+``flash_attn_fwd`` / ``flash_attn_bwd`` launch — the backward kernel is handed the MERGED output and
+log-sum-exp, so its delta = rowsum(dO * O) and P = exp(s - lse) are the global ones and the block
+gradients are exact. On CPU (gloo tests) the same block contract is evaluated in fp32 torch.
+
+Dropout (``dropout_p``) draws an independent mask per (step, block) and keeps it for the backward.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.distributed as dist
+
+from .. import _ext
+
+__all__ = ["ring_attention", "ulysses_attention", "shard_sequence", "gather_sequence", "chunk_ids"]
+
+
+# ----------------------------------------------------------------------------------------------
+# layouts
+# ----------------------------------------------------------------------------------------------
+def chunk_ids(rank, world, layout):
+    """Global sequence-chunk ids held by ``rank`` (in local order) and the chunk count."""
+    if layout == "zigzag":
+        return [rank, 2 * world - 1 - rank], 2 * world
+    if layout == "contiguous":
+        return [rank], world
+    raise ValueError("layout must be 'zigzag' or 'contiguous', got {!r}".format(layout))
+
+
+def _group_info(group):
+    if group is None:
+        from . import parallel_state as ps
+
+        group = ps.get_context_parallel_group()
+    if group is None:
+        return None, 1, 0, [dist.get_rank() if dist.is_initialized() else 0]
+    return group, dist.get_world_size(group), dist.get_rank(group), dist.get_process_group_ranks(group)
+
+
+def shard_sequence(x, group=None, layout="zigzag", dim=1):
+    """This rank's shard of a full sequence ``x`` (sequence along ``dim``)."""
+    _, W, r, _ = _group_info(group)
+    ids, n = chunk_ids(r, W, layout)
+    if x.shape[dim] % n:
+        raise ValueError("sequence length {} is not divisible into {} chunks".format(x.shape[dim], n))
+    parts = x.chunk(n, dim=dim)
+    return torch.cat([parts[i] for i in ids], dim=dim)
+
+
+def gather_sequence(x, group=None, layout="zigzag", dim=1):
+    """Inverse of shard_sequence: the full sequence from every rank's shard (all-gather)."""
+    g, W, _, _ = _group_info(group)
+    if W == 1:
+        return x
+    shards = [torch.empty_like(x) for _ in range(W)]
+    dist.all_gather(shards, x.contiguous(), group=g)
+    n = chunk_ids(0, W, layout)[1]
+    full = [None] * n
+    for rr, s in enumerate(shards):
+        ids, _ = chunk_ids(rr, W, layout)
+        for i, part in zip(ids, s.chunk(len(ids), dim=dim)):
+            full[i] = part
+    return torch.cat(full, dim=dim)
+
+
+# ----------------------------------------------------------------------------------------------
+# block attention: o, lse for one (query chunk, key chunk) pair, and its backward
+# ----------------------------------------------------------------------------------------------
+def _native(q):
+    if not (q.is_cuda and q.dtype in (torch.bfloat16, torch.float16) and q.shape[-1] in (32, 64, 128, 256)):
+        return False
+    C = _ext._load()
+    return C is not None and hasattr(C, "flash_attn_fwd")
+
+
+def _acc_dtype(t):
+    """Accumulation dtype of the torch block path and the merge: fp32, or fp64 for fp64 inputs."""
+    return torch.float64 if t.dtype == torch.float64 else torch.float32
+
+
+def _f(t):
+    return t.to(_acc_dtype(t))
+
+
+def _scores(q, k, causal, scale):
+    # q [B, Sq, H, D], k [B, Sk, H, D] -> fp32 [B, H, Sq, Sk]
+    s = torch.einsum("bqhd,bkhd->bhqk", _f(q), _f(k)) * scale
+    if causal:
+        Sq, Sk = s.shape[-2:]
+        s = s.masked_fill(torch.ones(Sq, Sk, dtype=torch.bool, device=s.device).triu(1), float("-inf"))
+    return s
+
+
+def _blk_fwd(q, k, v, causal, scale, p):
+    """(o [B, Sq, H, D] in q's dtype, lse fp32 [B, H, Sq] (natural log), aux for the backward)."""
+    if _native(q):
+        C = _ext.require()
+        seed, offset = (0, 0)
+        if p > 0:
+            from ..utils.rng import philox_seed_offset
+
+            seed, offset = philox_seed_offset(q.device)
+        o, lse, dmask = C.flash_attn_fwd(q, k, v, bool(causal), float(scale), float(p), seed, offset, None, None)
+        return o, lse, (seed, offset, dmask)
+    s = _scores(q, k, causal, scale)
+    lse = torch.logsumexp(s, dim=-1)
+    pr = torch.exp(s - lse[..., None])
+    keep = None
+    if p > 0:
+        keep = torch.rand(pr.shape, device=pr.device) >= p
+        pr = pr * keep / (1.0 - p)
+    o = torch.einsum("bhqk,bkhd->bqhd", pr, _f(v))
+    return o.to(q.dtype), lse, keep
+
+
+def _blk_bwd(do, q, k, v, o, lse, causal, scale, p, aux):
+    """(dq, dk, dv) of one block given the MERGED output ``o`` and log-sum-exp ``lse`` of the rows."""
+    if _native(q):
+        C = _ext.require()
+        seed, offset, dmask = aux
+        dq = torch.empty(q.shape, dtype=q.dtype, device=q.device)
+        dk = torch.empty(k.shape, dtype=k.dtype, device=k.device)
+        dv = torch.empty(v.shape, dtype=v.dtype, device=v.device)
+        C.flash_attn_bwd(do, q, k, v, o, lse.contiguous(), dq, dk, dv, bool(causal), float(scale), float(p), seed,
+                         offset, None, dmask if p > 0 else None, None, 0, None)
+        return dq, dk, dv
+    s = _scores(q, k, causal, scale)
+    pr = torch.exp(s - lse[..., None])
+    dof, vf = _f(do), _f(v)
+    delta = torch.einsum("bqhd,bqhd->bhq", dof, _f(o))
+    dp = torch.einsum("bqhd,bkhd->bhqk", dof, vf)
+    pd = pr
+    if p > 0:
+        pd = pr * aux / (1.0 - p)
+        dp = dp * aux / (1.0 - p)
+    dv = torch.einsum("bhqk,bqhd->bkhd", pd, dof)
+    ds = pr * (dp - delta[..., None])
+    dq = torch.einsum("bhqk,bkhd->bqhd", ds, _f(k)) * scale
+    dk = torch.einsum("bhqk,bqhd->bkhd", ds, _f(q)) * scale
+    return dq, dk, dv
+
+
+def _merge(acc_o, acc_lse, o, lse):
+    """Fold one block's (o, lse) into the running fp32 (acc_o [B, S, H, D], acc_lse [B, H, S])."""
+    lse = torch.where(torch.isposinf(lse), torch.full_like(lse, float("-inf")), lse)  # empty rows
+    if acc_o is None:
+        return _f(o), lse.clone()
+    new = torch.logaddexp(acc_lse, lse)
+    safe = torch.where(torch.isneginf(new), torch.zeros_like(new), new)
+    w_old = torch.exp(acc_lse - safe).transpose(1, 2).unsqueeze(-1)
+    w_new = torch.exp(lse - safe).transpose(1, 2).unsqueeze(-1)
+    return acc_o * w_old + _f(o) * w_new, new
+
+
+def _pairs(q_ids, k_ids, causal):
+    """(qi, ki, diag) over local query chunks x source key chunks that have visible keys."""
+    out = []
+    for qi, a in enumerate(q_ids):
+        for ki, b in enumerate(k_ids):
+            if causal and b > a:
+                continue
+            out.append((qi, ki, causal and a == b))
+    return out
+
+
+class _Ring:
+    """Async exchange with the ring neighbours (send to rank + 1, receive from rank - 1)."""
+
+    def __init__(self, group, ranks, r):
+        self.group = group
+        W = len(ranks)
+        self.nxt, self.prv = ranks[(r + 1) % W], ranks[(r - 1) % W]
+
+    def start(self, tensors):
+        recv = [torch.empty_like(t) for t in tensors]
+        ops = [dist.P2POp(dist.isend, t, self.nxt, self.group) for t in tensors]
+        ops += [dist.P2POp(dist.irecv, t, self.prv, self.group) for t in recv]
+        return dist.batch_isend_irecv(ops), recv
+
+    @staticmethod
+    def finish(handle):
+        reqs, recv = handle
+        for q in reqs:
+            q.wait()
+        return recv
+
+
+class _RingAttention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, group, ranks, r, causal, scale, p, layout):
+        W = len(ranks)
+        ring = _Ring(group, ranks, r)
+        q_ids, _ = chunk_ids(r, W, layout)
+        nq = len(q_ids)
+        qs = q.chunk(nq, dim=1)
+        acc = [[None, None] for _ in range(nq)]
+        aux = {}
+        cur = [k.contiguous(), v.contiguous()]
+        for step in range(W):
+            src = (r - step) % W
+            nxt = ring.start(cur) if step < W - 1 else None  # the transfer overlaps this step's blocks
+            k_ids, _ = chunk_ids(src, W, layout)
+            ks, vs = cur[0].chunk(len(k_ids), dim=1), cur[1].chunk(len(k_ids), dim=1)
+            for qi, ki, diag in _pairs(q_ids, k_ids, causal):
+                o, lse, a = _blk_fwd(qs[qi], ks[ki], vs[ki], diag, scale, p)
+                acc[qi][0], acc[qi][1] = _merge(acc[qi][0], acc[qi][1], o, lse)
+                aux[(step, qi, ki)] = a
+            if nxt is not None:
+                cur = _Ring.finish(nxt)
+        out = torch.cat([a[0] for a in acc], dim=1).to(q.dtype)
+        lse = torch.cat([a[1] for a in acc], dim=2)
+        ctx.save_for_backward(q, k, v, out, lse)
+        ctx.cfg = (group, ranks, r, causal, scale, p, layout)
+        ctx.aux = aux
+        return out
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, out, lse = ctx.saved_tensors
+        group, ranks, r, causal, scale, p, layout = ctx.cfg
+        W = len(ranks)
+        ring = _Ring(group, ranks, r)
+        q_ids, _ = chunk_ids(r, W, layout)
+        nq = len(q_ids)
+        do = do.contiguous()
+        qs, dos, outs = q.chunk(nq, dim=1), do.chunk(nq, dim=1), out.chunk(nq, dim=1)
+        lses = [t.contiguous() for t in lse.chunk(nq, dim=2)]
+        dq = torch.zeros(q.shape, dtype=_acc_dtype(q), device=q.device)
+        dqs = dq.chunk(nq, dim=1)
+        cur = [k.contiguous(), v.contiguous()]
+        dkv_pending = None  # the dK/dV partial of the shard arriving with `cur`, still in flight
+        for step in range(W):
+            src = (r - step) % W
+            nxt = ring.start(cur) if step < W - 1 else None
+            k_ids, _ = chunk_ids(src, W, layout)
+            ks, vs = cur[0].chunk(len(k_ids), dim=1), cur[1].chunk(len(k_ids), dim=1)
+            grads = []
+            for qi, ki, diag in _pairs(q_ids, k_ids, causal):
+                g = _blk_bwd(dos[qi], qs[qi], ks[ki], vs[ki], outs[qi], lses[qi], diag, scale, p,
+                             ctx.aux.get((step, qi, ki)))
+                dqs[qi].add_(g[0])
+                grads.append((ki, g[1], g[2]))
+            # the shard's dK/dV partial from the previous ranks (zero at step 0) + this rank's blocks
+            if dkv_pending is None:
+                dk_t = torch.zeros(k.shape, dtype=_acc_dtype(k), device=k.device)
+                dv_t = torch.zeros(v.shape, dtype=_acc_dtype(v), device=v.device)
+            else:
+                dk_t, dv_t = _Ring.finish(dkv_pending)
+            dks, dvs = dk_t.chunk(len(k_ids), dim=1), dv_t.chunk(len(k_ids), dim=1)
+            for ki, gk, gv in grads:
+                dks[ki].add_(gk)
+                dvs[ki].add_(gv)
+            # travels with its K/V shard; after the last step this send brings it home
+            dkv_pending = ring.start([dk_t, dv_t])
+            if nxt is not None:
+                cur = _Ring.finish(nxt)
+        dk, dv = _Ring.finish(dkv_pending)
+        ctx.aux = None
+        return dq.to(q.dtype), dk.to(k.dtype), dv.to(v.dtype), None, None, None, None, None, None, None
+
+
+def ring_attention(q, k, v, group=None, causal=False, scale=None, dropout_p=0.0, layout="zigzag"):
+    """Attention of this rank's query shard over the whole (sharded) key sequence.
+
+    q, k, v: [B, S_local, H, D] shards laid out by ``shard_sequence(..., layout)``; returns this
+    rank's [B, S_local, H, D] output shard. ``group``: the CP group (default: parallel_state's).
+    """
+    g, W, r, ranks = _group_info(group)
+    scale = 1.0 / math.sqrt(q.shape[-1]) if scale is None else float(scale)
+    if W == 1:
+        layout = "contiguous"
+    if layout == "zigzag" and q.shape[1] % 2:
+        raise ValueError("zigzag layout needs an even local sequence length")
+    return _RingAttention.apply(q, k, v, g, ranks, r, bool(causal), scale, float(dropout_p), layout)
+
+
+# ----------------------------------------------------------------------------------------------
+# Ulysses: sequence <-> head all-to-all
+# ----------------------------------------------------------------------------------------------
+def _seq_to_head(x, group, W):
+    # [B, S/W, H, D] -> [B, S, H/W, D]
+    B, s, H, D = x.shape
+    send = x.reshape(B, s, W, H // W, D).permute(2, 0, 1, 3, 4).contiguous()
+    recv = torch.empty_like(send)
+    dist.all_to_all_single(recv, send, group=group)
+    return recv.permute(1, 0, 2, 3, 4).reshape(B, W * s, H // W, D)
+
+
+def _head_to_seq(x, group, W):
+    # [B, S, H/W, D] -> [B, S/W, H, D]
+    B, S, h, D = x.shape
+    send = x.reshape(B, W, S // W, h, D).permute(1, 0, 2, 3, 4).contiguous()
+    recv = torch.empty_like(send)
+    dist.all_to_all_single(recv, send, group=group)
+    return recv.permute(1, 2, 0, 3, 4).reshape(B, S // W, W * h, D)
+
+
+class _SeqToHead(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, group, W):
+        ctx.cfg = (group, W)
+        return _seq_to_head(x, group, W)
+
+    @staticmethod
+    def backward(ctx, g):
+        group, W = ctx.cfg
+        return _head_to_seq(g.contiguous(), group, W), None, None
+
+
+class _HeadToSeq(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, group, W):
+        ctx.cfg = (group, W)
+        return _head_to_seq(x, group, W)
+
+    @staticmethod
+    def backward(ctx, g):
+        group, W = ctx.cfg
+        return _seq_to_head(g.contiguous(), group, W), None, None
+
+
+def ulysses_attention(q, k, v, group=None, causal=False, scale=None, dropout_p=0.0, k_lens=None):
+    """DeepSpeed-Ulysses-style attention over contiguous sequence shards [B, S/W, H, D]
+    (``shard_sequence(..., layout="contiguous")``); needs H % W == 0. The local attention is
+    apex.contrib.multihead_attn's (flash kernels on device)."""
+    from ..contrib.multihead_attn.attention import attention
+
+    g, W, _, _ = _group_info(group)
+    if W == 1:
+        return attention(q, k, v, dropout_p=dropout_p, causal=causal, scale=scale, k_lens=k_lens)
+    if q.shape[2] % W:
+        raise ValueError("ulysses_attention needs heads ({}) divisible by the CP size ({})".format(q.shape[2], W))
+    qh, kh, vh = (_SeqToHead.apply(t, g, W) for t in (q, k, v))
+    scale = 1.0 / math.sqrt(q.shape[-1]) if scale is None else scale
+    o = attention(qh, kh, vh, dropout_p=dropout_p, causal=causal, scale=scale, k_lens=k_lens)
+    return _HeadToSeq.apply(o, g, W)

@@ -23,6 +23,8 @@ _EMBEDDING_GLOBAL_RANKS = None
 _PIPELINE_GLOBAL_RANKS = None
 _DATA_PARALLEL_GLOBAL_RANKS = None
 _TENSOR_GLOBAL_RANKS = None
+_CONTEXT_PARALLEL_GROUP = None
+_CONTEXT_PARALLEL_GLOBAL_RANKS = None
 
 _VIRTUAL_PIPELINE_MODEL_PARALLEL_RANK = None
 _VIRTUAL_PIPELINE_MODEL_PARALLEL_WORLD_SIZE = None
@@ -41,8 +43,16 @@ def is_unitialized():
 def initialize_model_parallel(tensor_model_parallel_size_=1, pipeline_model_parallel_size_=1,
                               virtual_pipeline_model_parallel_size_=None,
                               pipeline_model_parallel_split_rank_=None, *, default_backend=None,
-                              p2p_backend=None):
-    """Create TP / PP / DP / embedding groups over the already-initialised default group."""
+                              p2p_backend=None, context_parallel_size_=1):
+    """Create TP / PP / DP / embedding groups over the already-initialised default group.
+
+    ``context_parallel_size_`` (cp > 1): each DP group is further cut into runs of ``cp``
+    consecutive DP ranks that shard the SEQUENCE of one sample (apex.transformer.context_parallel:
+    ring / Ulysses attention over these groups). The DP group keeps every CP rank, so the gradient
+    all-reduce over it sums the sequence shards' contributions (Megatron's dp x cp reduction); the
+    number of distinct data replicas is dp / cp. With TP = 4 the DP peers of a rank are 4 ranks
+    apart, each pair on its own direct xGMI link, so the CP ring's p2p hops never share a link
+    with the TP all-reduces."""
     assert dist.is_initialized()
     world_size = dist.get_world_size()
     tp = min(tensor_model_parallel_size_, world_size)
@@ -75,6 +85,19 @@ def initialize_model_parallel(tensor_model_parallel_size_=1, pipeline_model_para
             if rank in ranks:
                 _DATA_PARALLEL_GROUP = g
                 _DATA_PARALLEL_GLOBAL_RANKS = ranks
+
+    global _CONTEXT_PARALLEL_GROUP, _CONTEXT_PARALLEL_GLOBAL_RANKS
+    cp = int(context_parallel_size_ or 1)
+    if dp % cp != 0:
+        raise RuntimeError("data-parallel size ({}) is not divisible by context_parallel_size ({})".format(dp, cp))
+    assert _CONTEXT_PARALLEL_GROUP is None, "context parallel group is already initialized"
+    for dp_ranks in _dp_rank_table(world_size, tp, pp):
+        for c in range(0, dp, cp):
+            ranks = dp_ranks[c:c + cp]
+            g = dist.new_group(ranks, **kw) if cp > 1 else None
+            if rank in ranks:
+                _CONTEXT_PARALLEL_GROUP = g if cp > 1 else _SINGLETON
+                _CONTEXT_PARALLEL_GLOBAL_RANKS = ranks
 
     global _MODEL_PARALLEL_GROUP
     for i in range(dp):
@@ -117,6 +140,9 @@ def initialize_model_parallel(tensor_model_parallel_size_=1, pipeline_model_para
             _EMBEDDING_GLOBAL_RANKS = emb
         if rank in pos:
             _POSITION_EMBEDDING_GROUP = pg
+
+
+_SINGLETON = object()  # cp = 1: no group is created (every rank holds its whole sequence)
 
 
 def _dp_rank_table(world_size, tp, pp):
@@ -296,6 +322,27 @@ def get_pipeline_model_parallel_prev_rank():
     return _PIPELINE_GLOBAL_RANKS[(r - 1) % ws]
 
 
+def get_context_parallel_group():
+    """The CP group (None when cp = 1: the sequence is not sharded)."""
+    assert _CONTEXT_PARALLEL_GROUP is not None, "context parallel group is not initialized"
+    return None if _CONTEXT_PARALLEL_GROUP is _SINGLETON else _CONTEXT_PARALLEL_GROUP
+
+
+def get_context_parallel_global_ranks():
+    assert _CONTEXT_PARALLEL_GLOBAL_RANKS is not None, "context parallel group is not initialized"
+    return list(_CONTEXT_PARALLEL_GLOBAL_RANKS)
+
+
+def get_context_parallel_world_size():
+    g = get_context_parallel_group()
+    return 1 if g is None else dist.get_world_size(group=g)
+
+
+def get_context_parallel_rank():
+    g = get_context_parallel_group()
+    return 0 if g is None else dist.get_rank(group=g)
+
+
 def get_data_parallel_world_size():
     return dist.get_world_size(group=get_data_parallel_group())
 
@@ -311,7 +358,8 @@ def destroy_model_parallel():
     global _MPU_TENSOR_MODEL_PARALLEL_WORLD_SIZE, _MPU_PIPELINE_MODEL_PARALLEL_WORLD_SIZE
     global _MPU_TENSOR_MODEL_PARALLEL_RANK, _MPU_PIPELINE_MODEL_PARALLEL_RANK
     global _EMBEDDING_GLOBAL_RANKS, _PIPELINE_GLOBAL_RANKS, _DATA_PARALLEL_GLOBAL_RANKS, _TENSOR_GLOBAL_RANKS
-    global _PIPELINE_MODEL_PARALLEL_SPLIT_RANK
+    global _PIPELINE_MODEL_PARALLEL_SPLIT_RANK, _CONTEXT_PARALLEL_GROUP, _CONTEXT_PARALLEL_GLOBAL_RANKS
+    _CONTEXT_PARALLEL_GROUP = _CONTEXT_PARALLEL_GLOBAL_RANKS = None
     _MODEL_PARALLEL_GROUP = _TENSOR_MODEL_PARALLEL_GROUP = _PIPELINE_MODEL_PARALLEL_GROUP = None
     _DATA_PARALLEL_GROUP = _EMBEDDING_GROUP = _POSITION_EMBEDDING_GROUP = None
     _VIRTUAL_PIPELINE_MODEL_PARALLEL_RANK = _VIRTUAL_PIPELINE_MODEL_PARALLEL_WORLD_SIZE = None

@@ -1,0 +1,74 @@
+"""Ring-attention block contract on the flash kernels (apex.transformer.context_parallel).
+
+The ring's communication is covered on CPU/gloo (tests/test_context_parallel.py); here the device
+block math is checked in one process: the key sequence is cut into chunks, each (query chunk, key
+chunk) block runs flash_attn_fwd, the blocks are merged through their log-sum-exp, and the block
+backward (flash_attn_bwd fed the MERGED output and lse) is summed per chunk — exactly what each ring
+step does — against one full-sequence flash attention and the fp32 reference, causal (diagonal
+blocks causal, lower blocks full, upper skipped) and not.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref(q, k, v, causal, scale):
+    s = torch.einsum("bqhd,bkhd->bhqk", q.float(), k.float()) * scale
+    if causal:
+        S = s.shape[-1]
+        s = s.masked_fill(torch.ones(S, S, dtype=torch.bool, device=s.device).triu(1), float("-inf"))
+    return torch.einsum("bhqk,bkhd->bqhd", s.softmax(-1), v.float())
+
+
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("D", [64, 128])
+def test_ring_blocks_match_full(causal, D):
+    from apex.transformer import context_parallel as cp
+
+    torch.manual_seed(0)
+    B, S, H, n = 2, 1024, 4, 4
+    dev = "cuda"
+    q, k, v, do = (torch.randn(B, S, H, D, device=dev, dtype=torch.bfloat16) for _ in range(4))
+    scale = D ** -0.5
+    qs, ks, vs, dos = (t.chunk(n, dim=1) for t in (q, k, v, do))
+    outs, lses = [], []
+    aux = {}
+    for a in range(n):
+        acc = [None, None]
+        for b in range(n):
+            if causal and b > a:
+                continue
+            o, lse, x = cp._blk_fwd(qs[a], ks[b], vs[b], causal and a == b, scale, 0.0)
+            acc = list(cp._merge(acc[0], acc[1], o, lse))
+            aux[(a, b)] = x
+        outs.append(acc[0].to(q.dtype))
+        lses.append(acc[1])
+    out = torch.cat(outs, dim=1)
+    ref = _ref(q, k, v, causal, scale)
+    torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
+
+    dq = torch.zeros(q.shape, device=dev)
+    dk = torch.zeros(k.shape, device=dev)
+    dv = torch.zeros(v.shape, device=dev)
+    for (a, b), x in aux.items():
+        g = cp._blk_bwd(dos[a], qs[a], ks[b], vs[b], outs[a], lses[a], causal and a == b, scale, 0.0, x)
+        dq.chunk(n, dim=1)[a].add_(g[0].float())
+        dk.chunk(n, dim=1)[b].add_(g[1].float())
+        dv.chunk(n, dim=1)[b].add_(g[2].float())
+    qr, kr, vr = (t.float().requires_grad_() for t in (q, k, v))
+    _ref(qr, kr, vr, causal, scale).backward(do.float())
+    for got, want in ((dq, qr.grad), (dk, kr.grad), (dv, vr.grad)):
+        err = (got - want).abs().max().item() / want.abs().max().item()
+        assert err < 2e-2, err
+
+
+def test_ring_attention_single_rank_is_flash():
+    """CP size 1 (no group): ring_attention is one flash call."""
+    from apex.contrib.multihead_attn.flash import flash_attention
+    from apex.transformer import context_parallel as cp
+
+    torch.manual_seed(1)
+    q, k, v = (torch.randn(2, 256, 4, 64, device="cuda", dtype=torch.bfloat16) for _ in range(3))
+    out = cp._RingAttention.apply(q, k, v, None, [0], 0, True, 0.125, 0.0, "contiguous")
+    torch.testing.assert_close(out, flash_attention(q, k, v, causal=True, scale=0.125), atol=0, rtol=0)
