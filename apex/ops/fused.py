@@ -86,6 +86,26 @@ def _gt(p):
     return grad_target(p) if p is not None else None
 
 
+_MAIN_GRAD_GEMM = os.environ.get("APEX_MAIN_GRAD_GEMM", "auto")
+
+
+def _main_grad_tt(M, N, K):
+    """fp32 main_grad accumulation on the MFMA kernel (gemm_tt_acc) for this dW[N, K] shape?
+    ``APEX_MAIN_GRAD_GEMM``: auto, tt (always when supported), lib (hipBLASLt / split-K slabs only).
+    auto: when the 256x256 output tiles fill the 256 CUs' rounds to >= 75 % (one tile per CU and
+    round, unsplit). Measured at Megatron H2560, 8192 tokens (profiles/r3_main_grad_ab.jsonl):
+    10240x2560 and 2560x10240 (400 tiles, 78 %) 455 vs 531-538 us for hipBLASLt's fp32-output
+    addmm; 7680x2560 (300 tiles, 59 %) 455 vs 355 and 2560x2560 (100 tiles) 211 vs 127 — there the
+    library keeps them."""
+    if _MAIN_GRAD_GEMM == "lib":
+        return False
+    if _MAIN_GRAD_GEMM == "tt":
+        return True
+    tiles = (N // 256) * (K // 256)
+    rounds = -(-tiles // 256)
+    return tiles >= 192 and tiles >= 0.75 * rounds * 256
+
+
 def accumulate_main_grad(mg, dy2, x2):
     """mg (fp32) += dy2^T @ x2 with fp32 accumulation and no 16-bit rounding: the split-K batched
     GEMM's fp32 slabs (one slab when the shape does not split) summed INTO mg by one HIP pass
@@ -96,6 +116,11 @@ def accumulate_main_grad(mg, dy2, x2):
     if not (dy2.is_cuda and _native(dy2) and dy2.dtype in (torch.bfloat16, torch.float16)
             and dy2.is_contiguous() and x2.is_contiguous() and mg.is_contiguous()):
         mg.add_(dy2.t().float().mm(x2.float()))
+        return mg
+    if _main_grad_tt(M, N, K) and _ext.require().gemm_tt_supported(dy2, x2, 1):
+        # the transposed-read MFMA kernel with the fp32 read-modify-write epilogue: dW is added
+        # into main_grad in the GEMM's own epilogue (csrc/gemm.hip EPI_F32_ACC)
+        _ext.require().gemm_tt_acc(dy2, x2, mg)
         return mg
     s = _wgrad_splits(M, N, K)
     if s == 1:

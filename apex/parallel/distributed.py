@@ -41,6 +41,7 @@ import torch
 import torch.distributed as dist
 from torch.nn.modules import Module
 
+from .. import _ext
 from ..utils import prof
 
 # ----------------------------------------------------------------------------
@@ -341,6 +342,11 @@ class DistributedDataParallel(Module):
         self._param_bucket = {}    # param idx -> bucket idx
         self._ready_order = []
         self._callback_queued = False
+        # fp32_main_grad: 16-bit gradients of unfused producers (biases, norms, embeddings) awaiting
+        # ONE multi-tensor add into main_grad (torch's mixed-dtype add is a ~50 us launch per
+        # tensor: 2080 launches, 105 ms of a Megatron GPT step)
+        self._pending_mg = []
+        self._mg_flush_queued = False
         self._next_bucket = 0
         self._allreduce_enabled = True
         self._hooks = []
@@ -416,6 +422,7 @@ class DistributedDataParallel(Module):
         if not self._layout_ready:
             self._build_layout()
             self._layout_ready = True
+        self._flush_main_grad()
         for i, p in enumerate(self._params):
             if self.fp32_main_grad:
                 if p.grad is not None:  # a gradient produced outside the hooks
@@ -447,7 +454,13 @@ class DistributedDataParallel(Module):
             # placeholder by autograd) is added here
             g = p.grad
             if g is not None and not g._is_zerotensor():
-                p.main_grad.add_(g)
+                if g.is_cuda and g.dtype != p.main_grad.dtype and g.is_contiguous() and _ext.use_native(g):
+                    self._pending_mg.append((p.main_grad, g))
+                    if not self._mg_flush_queued:
+                        torch.autograd.Variable._execution_engine.queue_callback(self._flush_main_grad)
+                        self._mg_flush_queued = True
+                else:
+                    p.main_grad.add_(g)
             p.grad_added_to_main_grad = False
             p.grad = None
         if not self._allreduce_enabled:
@@ -487,6 +500,24 @@ class DistributedDataParallel(Module):
         if b.ready == len(b.params) and bi == self._next_bucket:
             self._launch_ready_in_order()
 
+    def _flush_main_grad(self):
+        """main_grad += g for every deferred 16-bit gradient: one fused multi-tensor axpby launch
+        (csrc/multi_tensor.hip, fp32 x + bf16/fp16 y -> fp32). Runs before any bucket holding one
+        of them is reduced and at the end of every backward pass."""
+        self._mg_flush_queued = False
+        if not self._pending_mg:
+            return
+        pend, self._pending_mg = self._pending_mg, []
+        from ..multi_tensor_apply import get_plan
+
+        by_dtype = {}
+        for mg, g in pend:
+            by_dtype.setdefault(g.dtype, []).append((mg, g))
+        for items in by_dtype.values():
+            mgs = [mg for mg, _ in items]
+            gs = [g for _, g in items]
+            get_plan([mgs, gs, mgs]).axpby(1.0, 1.0, -1, None)
+
     def _ensure_view(self, idx, p):
         if self.fp32_main_grad:
             return  # main_grad is the bucket view; p.grad is never used
@@ -515,6 +546,7 @@ class DistributedDataParallel(Module):
         and copies an fp32 staging buffer back, so every step of the bucket is ordered on the
         reduction stream and the compute stream only joins it at the end of backward. On the
         CPU (gloo) the wait is a host wait, so it is deferred to the end of backward."""
+        self._flush_main_grad()
         b.lane = lane
         stream = self._streams[lane]
         if stream is None:
@@ -578,6 +610,7 @@ class DistributedDataParallel(Module):
 
     def _end_of_backward(self):
         _TARGETS_GIVEN.clear()
+        self._flush_main_grad()
         ev0 = None
         if self.comm_timing and self._cuda:
             ev0 = torch.cuda.Event(enable_timing=True)

@@ -1168,6 +1168,30 @@ Tensor k_gemm_tt(Tensor a, Tensor b, int64_t splits, at::ScalarType out_dtype) {
   return k_splitk_reduce(slabs, out_dtype, c10::nullopt);
 }
 
+// out[P, Q] += a^T b in fp32 (a [R, P], b [R, Q] 16-bit, out fp32 contiguous): the weight gradient
+// accumulated straight into an fp32 main_grad by the transposed-read MFMA kernel's
+// read-modify-write epilogue — one launch, no slab, no 16-bit rounding of the micro-batch dW
+void k_gemm_tt_acc(Tensor a, Tensor b, Tensor out) {
+  TORCH_CHECK(k_gemm_tt_supported(a, b, 1), "gemm_tt_acc: unsupported operands");
+  const int64_t P = a.size(1), Q = b.size(1);
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.is_contiguous() && out.dim() == 2 &&
+                  out.size(0) == P && out.size(1) == Q && reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0,
+              "gemm_tt_acc: out must be a contiguous fp32 [P, Q] tensor");
+  apex::GemmArgs g{};
+  g.A = a.data_ptr();
+  g.B = b.data_ptr();
+  g.M = (int)P;
+  g.N = (int)Q;
+  g.K = (int)a.size(0);
+  g.lda = P;
+  g.ldb = Q;
+  g.ldc = Q;
+  g.splits = 1;
+  g.part = out.data_ptr<float>();
+  g.epi = apex::EPI_F32_ACC;
+  check(apex::gemm_tt(g, dt_code(a.scalar_type()), cur_stream()), "gemm_tt_acc");
+}
+
 // sum the rows of an fp32 [P, N] partials tensor -> [N] in out_dtype
 Tensor k_partial_colsum(Tensor part, at::ScalarType out_dtype, const c10::optional<Tensor>& out_opt) {
   TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.dim() == 2 && part.is_contiguous(),
@@ -1279,6 +1303,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("transpose", &k_transpose);
   m.def("gemm_tt_supported", &k_gemm_tt_supported);
   m.def("gemm_tt", &k_gemm_tt);
+  m.def("gemm_tt_acc", &k_gemm_tt_acc);
   m.attr("EPI_NONE") = (int)apex::EPI_NONE;
   m.attr("EPI_BIAS") = (int)apex::EPI_BIAS;
   m.attr("EPI_BIAS_GELU") = (int)apex::EPI_BIAS_GELU;

@@ -695,6 +695,33 @@ __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(const TI* __restrict
     }
     return;
   }
+  if constexpr (EPI == EPI_F32_ACC) {
+    // part[m, n] += acc in fp32 (one K slice: gemm_tt_acc's main_grad accumulation), in two halves
+    // of 16 fragments whose 16-byte loads are all issued before the first add
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      f32x4 prev[2][8];
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int n = n0 + wc * 64 + (2 * hf + jj) * 16 + 4 * lk;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int m = m0 + wr * 128 + i * 16 + lr;
+          prev[jj][i] = m < M && n < N ? *reinterpret_cast<const f32x4*>(part + (int64_t)m * ldc + n) : f32x4{};
+        }
+      }
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int n = n0 + wc * 64 + (2 * hf + jj) * 16 + 4 * lk;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int m = m0 + wr * 128 + i * 16 + lr;
+          if (m < M && n < N) *reinterpret_cast<f32x4*>(part + (int64_t)m * ldc + n) = prev[jj][i] + acc[2 * hf + jj][i];
+        }
+      }
+    }
+    return;
+  }
 
   if (__builtin_expect((ctl >> 16) == 2, 0) || (DBG & 512)) {  // keep the accumulators live, store nothing
     float t = 0.f;
@@ -1371,14 +1398,17 @@ bool gemm_tt_supported(int P, int Q, int R, int splits, int64_t lda, int64_t ldb
 
 int gemm_tt(const GemmArgs& g, int dt, hipStream_t s) {
   // C[P=M, Q=N] (+)= sum_r A[r, p] B[r, q]; g.K = contraction rows per split; g.part = fp32 slabs
-  // [splits, M, N] when g.epi == EPI_F32, else g.C in the operand dtype (splits must be 1)
+  // [splits, M, N] when g.epi == EPI_F32, the fp32 [M, N] accumulator (+=) when EPI_F32_ACC, else g.C
+  // in the operand dtype (splits must be 1 except for EPI_F32)
   if (!gemm_tt_supported(g.M, g.N, g.K * g.splits, g.splits, g.lda, g.ldb)) return -2;
-  if (g.epi != EPI_F32 && (g.epi != EPI_NONE || g.splits != 1)) return -3;
+  if (g.epi != EPI_F32 && ((g.epi != EPI_NONE && g.epi != EPI_F32_ACC) || g.splits != 1)) return -3;
   if (dt == kBF16Code) {
     if (g.epi == EPI_F32) launch_gemm<bf16, EPI_F32, true>(g, s);
+    else if (g.epi == EPI_F32_ACC) launch_gemm<bf16, EPI_F32_ACC, true>(g, s);
     else launch_gemm<bf16, EPI_NONE, true>(g, s);
   } else if (dt == kF16Code) {
     if (g.epi == EPI_F32) launch_gemm<f16, EPI_F32, true>(g, s);
+    else if (g.epi == EPI_F32_ACC) launch_gemm<f16, EPI_F32_ACC, true>(g, s);
     else launch_gemm<f16, EPI_NONE, true>(g, s);
   } else {
     return -1;

@@ -202,7 +202,10 @@ int xentropy_bwd(const void* dloss, int64_t dloss_stride, int dloss_dt, const vo
 enum GemmEpi : int { EPI_NONE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_DGELU = 3, EPI_RESID = 4, EPI_F32 = 5,
                      EPI_BIAS_GELU_TANH = 6, EPI_DGELU_TANH = 7,
                      // forward GELU that stores gelu'(h) instead of h, and its backward: C = acc * aux
-                     EPI_BIAS_GELU_D = 8, EPI_BIAS_GELU_TANH_D = 9, EPI_MUL = 10 };
+                     EPI_BIAS_GELU_D = 8, EPI_BIAS_GELU_TANH_D = 9, EPI_MUL = 10,
+                     // fp32 read-modify-write: part[m, n] += acc (the weight gradient accumulated
+                     // straight into an fp32 main_grad, one K slice)
+                     EPI_F32_ACC = 11 };
 struct GemmArgs {
   const void* A;  // [M, K] row-major, lda
   const void* B;  // [N, K] row-major, ldb

@@ -39,10 +39,13 @@ class _Dense(torch.nn.Module):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("path", ["lib", "tt"])  # hipBLASLt / split-K slabs vs gemm_tt_acc's epilogue
 @pytest.mark.parametrize("M", [2048, 16384])  # 16384 tokens: the split-K (several slabs) path
-def test_main_grad_accumulates_in_fp32(rccl_one_rank, M):
+def test_main_grad_accumulates_in_fp32(rccl_one_rank, M, path, monkeypatch):
+    from apex.ops import fused
     from apex.parallel import DistributedDataParallel as DDP
 
+    monkeypatch.setattr(fused, "_MAIN_GRAD_GEMM", path)
     torch.manual_seed(0)
     N, K, mbs = 256, 512, 8
     net = _Dense(N, K)
@@ -67,3 +70,20 @@ def test_main_grad_accumulates_in_fp32(rccl_one_rank, M):
     err16 = float((acc16.float() - ref).abs().max()) / scale
     assert err32 < 1e-5, err32
     assert err16 > 20 * err32, (err16, err32)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R,P,Q", [(2048, 256, 512), (8192, 768, 1024), (1024, 2560, 512)])
+def test_gemm_tt_acc_matches_fp32(R, P, Q):
+    """out[P, Q] += a^T b by the transposed-read MFMA kernel's fp32 read-modify-write epilogue."""
+    from apex import _ext
+
+    C = _ext.require()
+    torch.manual_seed(1)
+    a = torch.randn(R, P, device="cuda", dtype=torch.bfloat16)
+    b = torch.randn(R, Q, device="cuda", dtype=torch.bfloat16)
+    out = torch.randn(P, Q, device="cuda", dtype=torch.float32) * 10
+    ref = out + a.float().t() @ b.float()
+    C.gemm_tt_acc(a, b, out)
+    err = float((out - ref).abs().max() / ref.abs().max())
+    assert err < 1e-5, err

@@ -1,6 +1,8 @@
 """A/B of the fp32 main_grad accumulation paths on the Megatron GPT shapes (GPU box):
 split-K fp32 slabs + splitk_reduce(accumulate) vs one addmm with out_dtype=fp32 and beta=1
-accumulating straight into main_grad (hipBLASLt C = D = fp32), vs the bf16 dW baseline.
+accumulating straight into main_grad (hipBLASLt C = D = fp32) vs the transposed-read MFMA kernel
+with the fp32 read-modify-write epilogue (C.gemm_tt_acc), vs the bf16 dW baseline (TunableOp
+selections loaded as in the benches) alone and followed by the fp32 add into main_grad.
 
   python tools/main_grad_ab.py [tokens=8192] [hidden=2560]
 """
@@ -10,6 +12,9 @@ import sys
 import torch
 
 sys.path.insert(0, ".")
+from apex.utils import gemm_tuning  # noqa: E402
+
+gemm_tuning.enable_tuned_gemms()
 from apex import _ext  # noqa: E402
 from apex.ops import fused as F  # noqa: E402
 
@@ -48,8 +53,15 @@ def main():
         def bf16():
             torch.mm(dy.t(), x)
 
+        def bf16_add():
+            mg.add_(torch.mm(dy.t(), x))
+
+        def tt_acc():
+            C.gemm_tt_acc(dy, x, mg)
+
         row = {"M": M, "N": N, "K": K}
-        for name, fn in (("slabs_reduce", slabs), ("addmm_fp32_beta1", addmm), ("bf16_dW", bf16)):
+        for name, fn in (("slabs_reduce", slabs), ("addmm_fp32_beta1", addmm), ("tt_acc", tt_acc),
+                         ("bf16_dW", bf16), ("bf16_dW_add", bf16_add)):
             try:
                 mg.zero_()
                 fn()
