@@ -35,6 +35,17 @@ from .fused import ACT_GELU, _2d, _gt, _seed, _wgrad
 # APEX_MLP_STORE=h keeps the pre-activation and re-evaluates erf/exp in the backward epilogue
 _STORE_DERIV = os.environ.get("APEX_MLP_STORE", "deriv") != "h"
 
+# Memory-efficient post-LN: the bias+dropout+residual+LN forward does not store its LN input s; the
+# backward rebuilds x-hat = (y - beta) / gamma from the LN output y, which is saved anyway as the next
+# sublayer's GEMM input — one [tokens, hidden] write less per sublayer (and that much less activation
+# memory). As with any output-based LayerNorm backward, a gamma entry of exactly 0 makes its column's
+# x-hat unrecoverable. APEX_LN_MEM=0 stores s.
+_LN_MEM = os.environ.get("APEX_LN_MEM", "1") != "0"
+
+
+def _ln_mem(C, cols):
+    return _LN_MEM and C.bdaln_supported(cols)
+
 class _AttnSublayer(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, wqkv, bqkv, wo, bo, gamma, beta, heads, p_attn, p_hidden, eps, causal, k_lens):
@@ -51,8 +62,11 @@ class _AttnSublayer(torch.autograd.Function):
         o2 = o.view(B * S, E)
         t = G.linear(o2, wo, f8=f8)
         sh, oh = _seed(x.device) if p_hidden > 0 else (0, 0)
-        y, s, mean, rstd = C.bdaln_fwd(t, bo, x2.contiguous(), gamma, beta, float(eps), float(p_hidden), sh, oh)
-        ctx.save_for_backward(x2, wqkv, qkv, o, lse, k_lens, dmask, wo, s, gamma, mean, rstd)
+        mem = _ln_mem(C, E)
+        y, s, mean, rstd = C.bdaln_fwd(t, bo, x2.contiguous(), gamma, beta, float(eps), float(p_hidden), sh, oh,
+                                       store_s=not mem)
+        ctx.save_for_backward(x2, wqkv, qkv, o, lse, k_lens, dmask, wo, y if mem else s, gamma, mean, rstd)
+        ctx.ln_beta = beta if mem else None
         ctx.f8 = f8
         ctx.params = (wqkv, bqkv, wo, bo, gamma, beta)
         ctx.cfg = (B, S, E, heads, d, scale, causal, p_attn, sa, oa, p_hidden, sh, oh, bqkv is not None,
@@ -67,7 +81,7 @@ class _AttnSublayer(torch.autograd.Function):
         pqkv, pbqkv, pwo, pbo, pg, pb = ctx.params
         dres, dt, dgamma, dbeta, dbo = C.bdaln_bwd(_2d(dy), s, gamma, mean, rstd, float(p_hidden), sh, oh, has_bo,
                                                    dgamma_out=_gt(pg), dbeta_out=_gt(pb),
-                                                   dbias_out=_gt(pbo) if has_bo else None)
+                                                   dbias_out=_gt(pbo) if has_bo else None, beta=ctx.ln_beta)
         f8 = ctx.f8
         dctx = G.dgrad(dt, wo, f8=f8).view(B, S, heads, d)
         dwo = _wgrad(dt, o.view(B * S, E), param=pwo)
@@ -103,8 +117,11 @@ class _FFNSublayer(torch.autograd.Function):
             hb = b1
         t = G.linear(g, w2, f8=f8)
         seed, off = _seed(x.device) if p > 0 else (0, 0)
-        y, s, mean, rstd = C.bdaln_fwd(t, b2, x2.contiguous(), gamma, beta, float(eps), float(p), seed, off)
-        ctx.save_for_backward(x2, w1, hb, h, g, w2, s, gamma, mean, rstd)
+        mem = _ln_mem(C, x2.shape[1])
+        y, s, mean, rstd = C.bdaln_fwd(t, b2, x2.contiguous(), gamma, beta, float(eps), float(p), seed, off,
+                                       store_s=not mem)
+        ctx.save_for_backward(x2, w1, hb, h, g, w2, y if mem else s, gamma, mean, rstd)
+        ctx.ln_beta = beta if mem else None
         ctx.cfg = (p, seed, off, act, b2 is not None, b1.dtype if b1 is not None else None)
         ctx.params = (w1, b1, w2, b2, gamma, beta)
         return y.view_as(x)
@@ -118,7 +135,7 @@ class _FFNSublayer(torch.autograd.Function):
         pw1, pb1, pw2, pb2, pg, pb = ctx.params
         dres, dt, dgamma, dbeta, db2 = C.bdaln_bwd(_2d(dy), s, gamma, mean, rstd, float(p), seed, off, has_b2,
                                                    dgamma_out=_gt(pg), dbeta_out=_gt(pb),
-                                                   dbias_out=_gt(pb2) if has_b2 else None)
+                                                   dbias_out=_gt(pb2) if has_b2 else None, beta=ctx.ln_beta)
         if hb is None and act == ACT_GELU and b1dt is not None:
             tb1 = _gt(pb1)
             if _STORE_DERIV:

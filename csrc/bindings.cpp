@@ -536,16 +536,18 @@ Tensor k_splitk_reduce(Tensor slabs, at::ScalarType out_dtype, const c10::option
 bool k_bdaln_supported(int64_t cols) { return apex::bdaln_supported((int)cols) != 0; }
 bool k_bdaln_wide_supported(int64_t cols) { return apex::bdaln_wide_supported((int)cols) != 0; }
 
+// store_s = false (post-LN memory-efficient mode): the LN input s is not written (an empty tensor is
+// returned); the backward rebuilds x-hat from y (k_bdaln_bwd with beta)
 std::vector<Tensor> k_bdaln_fwd(Tensor x, const c10::optional<Tensor>& b, Tensor res, Tensor gamma,
-                                Tensor beta, double eps, double p, int64_t seed, int64_t offset) {
+                                Tensor beta, double eps, double p, int64_t seed, int64_t offset, bool store_s) {
   TORCH_CHECK(x.is_contiguous() && res.is_contiguous() && x.sizes() == res.sizes(), "bdaln: shapes");
   const int64_t cols = cols_of(x), rows = x.numel() / std::max<int64_t>(cols, 1);
-  Tensor y = at::empty_like(x), s = at::empty_like(x);
+  Tensor y = at::empty_like(x), s = store_s ? at::empty_like(x) : at::empty({0}, x.options());
   auto fo = x.options().dtype(at::kFloat);
   Tensor mean = at::empty({rows}, fo), rstd = at::empty({rows}, fo);
   auto dp = drop_params(p);
   check(apex::bdaln_fwd(x.data_ptr(), opt_vptr(b), res.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
-                        y.data_ptr(), s.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(), rows,
+                        y.data_ptr(), store_s ? s.data_ptr() : nullptr, mean.data_ptr<float>(), rstd.data_ptr<float>(), rows,
                         (int)cols, (float)eps, (uint64_t)seed, (uint64_t)offset, dp.first, dp.second,
                         dt_code(x.scalar_type()), dt_code(gamma.scalar_type()), cur_stream()),
         "bdaln_fwd");
@@ -555,8 +557,14 @@ std::vector<Tensor> k_bdaln_fwd(Tensor x, const c10::optional<Tensor>& b, Tensor
 std::vector<Tensor> k_bdaln_bwd(Tensor dy, Tensor s, Tensor gamma, Tensor mean, Tensor rstd, double p,
                                 int64_t seed, int64_t offset, bool has_bias, const c10::optional<Tensor>& dgamma_out,
                                 const c10::optional<Tensor>& dbeta_out, const c10::optional<Tensor>& dbias_out,
-                                const c10::optional<Tensor>& ds_extra) {
+                                const c10::optional<Tensor>& ds_extra, const c10::optional<Tensor>& beta) {
+  // beta given: `s` is the LN output y of a store_s = false forward (x-hat = (y - beta) / gamma)
   Tensor dyc = dy.contiguous();
+  const bool from_y = beta.has_value() && beta->defined();
+  if (from_y)
+    TORCH_CHECK(beta->is_contiguous() && beta->sizes() == gamma.sizes() && beta->scalar_type() == gamma.scalar_type() &&
+                    s.is_contiguous(),
+                "bdaln_bwd: beta like gamma, y contiguous");
   const int64_t cols = cols_of(s), rows = s.numel() / std::max<int64_t>(cols, 1);
   Tensor dse;
   if (ds_extra.has_value() && ds_extra->defined()) {
@@ -569,7 +577,8 @@ std::vector<Tensor> k_bdaln_bwd(Tensor dy, Tensor s, Tensor gamma, Tensor mean, 
   Tensor dbias = has_bias ? out_or_empty(dbias_out, gamma.sizes(), gamma.options(), "bdaln_bwd dbias") : Tensor();
   Tensor ws = at::empty({apex::bdaln_ws_floats(rows, (int)cols)}, s.options().dtype(at::kFloat));
   auto dp = drop_params(p);
-  check(apex::bdaln_bwd(dyc.data_ptr(), s.data_ptr(), gamma.data_ptr(), mean.data_ptr<float>(),
+  check(apex::bdaln_bwd(dyc.data_ptr(), s.data_ptr(), gamma.data_ptr(), from_y ? beta->data_ptr() : nullptr,
+                        mean.data_ptr<float>(),
                         rstd.data_ptr<float>(), dse.defined() ? dse.data_ptr() : nullptr, dres.data_ptr(),
                         dx.data_ptr(), dgamma.data_ptr(),
                         dbeta.data_ptr(), has_bias ? dbias.data_ptr() : nullptr, ws.data_ptr<float>(), rows,
@@ -1285,7 +1294,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("accumulate") = false);
   m.def("bdaln_supported", &k_bdaln_supported);
   m.def("bdaln_wide_supported", &k_bdaln_wide_supported);
-  m.def("bdaln_fwd", &k_bdaln_fwd);
+  m.def("bdaln_fwd", &k_bdaln_fwd, py::arg("x"), py::arg("b"), py::arg("res"), py::arg("gamma"), py::arg("beta"),
+        py::arg("eps"), py::arg("p"), py::arg("seed"), py::arg("offset"), py::arg("store_s") = true);
   m.def("embed_ln_fwd", &k_embed_ln_fwd);
   m.def("embed_ln_bwd", &k_embed_ln_bwd, py::arg("dy"), py::arg("s"), py::arg("gamma"), py::arg("mean"),
         py::arg("rstd"), py::arg("tids"), py::arg("tvocab"), py::arg("npos"), py::arg("p"), py::arg("seed"),
@@ -1295,7 +1305,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out") = py::none());
   m.def("bdaln_bwd", &k_bdaln_bwd, py::arg("dy"), py::arg("s"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"),
         py::arg("p"), py::arg("seed"), py::arg("offset"), py::arg("has_bias"), py::arg("dgamma_out") = py::none(),
-        py::arg("dbeta_out") = py::none(), py::arg("dbias_out") = py::none(), py::arg("ds_extra") = py::none());
+        py::arg("dbeta_out") = py::none(), py::arg("dbias_out") = py::none(), py::arg("ds_extra") = py::none(),
+        py::arg("beta") = py::none());
   m.def("input_normalize", &k_input_normalize);
   m.def("gemm_supported", &k_gemm_supported);
   m.def("gemm", &k_gemm, py::arg("a"), py::arg("b"), py::arg("epi") = 0, py::arg("bias") = py::none(),

@@ -226,8 +226,9 @@ __global__ void __launch_bounds__(kEwBlock) bdaln_fwd_kernel(const T* __restrict
         v[j][k] = rv[k] + t;
       }
       // the LN input is stored at the activation precision and normalised from that value,
-      // so backward (which reads s_out) sees exactly what forward normalised
-      store_f<T, 8>(s_out + e, v[j]);
+      // so backward (which reads s_out) sees exactly what forward normalised; s_out == nullptr:
+      // not stored (post-LN memory-efficient mode: the backward rebuilds x-hat from y)
+      if (s_out) store_f<T, 8>(s_out + e, v[j]);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         v[j][k] = to_f(from_f<T>(v[j][k]));
@@ -277,9 +278,13 @@ __global__ void __launch_bounds__(kEwBlock) bdaln_fwd_kernel(const T* __restrict
 // ~4.2 TB/s (rocprofv3 FETCH/WRITE_SIZE, profiles/r2_pmc_bw_kernels.json).
 // EXTRA (pre-LN residual streams, GPT): s also feeds the next residual add, so its gradient is
 // LN_bwd(dy) + dse — dse is added here instead of by a separate autograd accumulate pass.
-template <typename T, typename W, int VPT, bool DROP, bool EXTRA = false>
-__global__ void __launch_bounds__(kEwBlock) bdaln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ s,
+// FROMY (post-LN, memory-efficient): `s` points at the LN OUTPUT y and x-hat = (y - beta) / gamma,
+// so the forward need not store s at all (one [rows, cols] write less per sublayer; y is saved
+// anyway as the next GEMM's input). dgamma accumulates dy * (y - beta) and is divided by gamma once.
+template <typename T, typename W, int VPT, bool DROP, bool EXTRA = false, bool FROMY = false>
+__global__ void __launch_bounds__(kEwBlock) __attribute__((amdgpu_waves_per_eu(FROMY ? 3 : 1))) bdaln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ s,
                                                             const W* __restrict__ gamma,
+                                                            const W* __restrict__ beta,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ rstd,
                                                             const T* __restrict__ dse,
@@ -329,19 +334,34 @@ __global__ void __launch_bounds__(kEwBlock) bdaln_bwd_kernel(const T* __restrict
         if constexpr (EXTRA) ev[j][k] = to_f(ne[j].v[k]);
       }
     if (rr + 1 < rows_per_wave) fetch(row + 4);
-    const float mu = mean[row], rs = rstd[row];
+    const float mu = FROMY ? 0.f : mean[row], rs = rstd[row];
     float s1 = 0.f, s2 = 0.f;
+    // FROMY: beta and 1/gamma are re-read / re-derived per row (L1-resident beta, v_rcp) instead of
+    // held in registers across the row loop, which took the kernel from 3 to 2 waves per SIMD; the
+    // empty asm keeps the compiler from hoisting them back out
+    if constexpr (FROMY) asm volatile("" ::: "memory");
 #pragma unroll
     for (int j = 0; j < VPT; ++j) {
       const int vi = j * 64 + lane;
       if (vi < nvec) {
+        float bt[8];
+        if constexpr (FROMY) load_f<W, 8>(beta + vi * 8, bt);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          xh[j][k] = (xh[j][k] - mu) * rs;
           const float dyg = dv[j][k] * g[j][k];
           s1 += dyg;
-          s2 += dyg * xh[j][k];
-          dg[j][k] += dv[j][k] * xh[j][k];
+          if constexpr (FROMY) {
+            const float yc = xh[j][k] - bt[k];  // = x-hat * gamma
+            s2 += dv[j][k] * yc;
+            dg[j][k] += dv[j][k] * yc;  // / gamma at the end
+            float gk = g[j][k];
+            asm volatile("" : "+v"(gk));
+            xh[j][k] = yc * __builtin_amdgcn_rcpf(gk);
+          } else {
+            xh[j][k] = (xh[j][k] - mu) * rs;
+            s2 += dyg * xh[j][k];
+            dg[j][k] += dv[j][k] * xh[j][k];
+          }
           dbt[j][k] += dv[j][k];
         }
       }
@@ -378,7 +398,7 @@ __global__ void __launch_bounds__(kEwBlock) bdaln_bwd_kernel(const T* __restrict
     if (vi < nvec) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        mine[vi * 8 + k] = dg[j][k];
+        mine[vi * 8 + k] = FROMY ? dg[j][k] / g[j][k] : dg[j][k];
         mine[cols + vi * 8 + k] = dbt[j][k];
         mine[2 * cols + vi * 8 + k] = dbi[j][k];
       }
@@ -968,14 +988,15 @@ int64_t bdaln_ws_floats(int64_t rows, int cols) {
   return (int64_t)kBdalnMaxParts * 3 * (int64_t)cols;
 }
 
-int bdaln_bwd(const void* dy, const void* s_in, const void* gamma, const float* mean, const float* rstd,
-              const void* dse, void* dres, void* dx, void* dgamma, void* dbeta, void* dbias, float* ws,
-              int64_t rows, int cols, uint64_t seed, uint64_t offset, uint32_t thresh, float scale, int xdt,
-              int wdt, hipStream_t s) {
+int bdaln_bwd(const void* dy, const void* s_in, const void* gamma, const void* beta, const float* mean,
+              const float* rstd, const void* dse, void* dres, void* dx, void* dgamma, void* dbeta, void* dbias,
+              float* ws, int64_t rows, int cols, uint64_t seed, uint64_t offset, uint32_t thresh, float scale,
+              int xdt, int wdt, hipStream_t s) {
   if (rows == 0) return 0;
   const int vpt = bdaln_vpt(cols);
   const int rpw = bdaln_rpw(rows);
   const int parts = (int)((rows + 4 * rpw - 1) / (4 * rpw));
+  if (beta && (!vpt || dse)) return -3;  // FROMY: post-LN (no ds_extra), narrow rows only
   if (!vpt) {
     const int wv = bdaln_wide_vpt(cols);
     const size_t wlds = (size_t)4 * cols * sizeof(float);
@@ -1001,10 +1022,20 @@ int bdaln_bwd(const void* dy, const void* s_in, const void* gamma, const float* 
   EW_DISPATCH(xdt, T, EW_DISPATCH(wdt, W, EW_VPT(vpt, VPT, {
     auto launch = [&](auto drop_tag, auto extra_tag) {
       hipLaunchKernelGGL((bdaln_bwd_kernel<T, W, VPT, decltype(drop_tag)::value, decltype(extra_tag)::value>),
-                         dim3(parts), dim3(kEwBlock), lds, s, (const T*)dy, (const T*)s_in, (const W*)gamma, mean,
-                         rstd, (const T*)dse, (T*)dres, (T*)dx, ws, rows, cols, rpw, seed, offset, thresh, scale);
+                         dim3(parts), dim3(kEwBlock), lds, s, (const T*)dy, (const T*)s_in, (const W*)gamma,
+                         (const W*)nullptr, mean, rstd, (const T*)dse, (T*)dres, (T*)dx, ws, rows, cols, rpw, seed,
+                         offset, thresh, scale);
     };
-    if (thresh) {
+    if (beta) {
+      auto launch_y = [&](auto drop_tag) {
+        hipLaunchKernelGGL((bdaln_bwd_kernel<T, W, VPT, decltype(drop_tag)::value, false, true>), dim3(parts),
+                           dim3(kEwBlock), lds, s, (const T*)dy, (const T*)s_in, (const W*)gamma, (const W*)beta,
+                           mean, rstd, (const T*)nullptr, (T*)dres, (T*)dx, ws, rows, cols, rpw, seed, offset,
+                           thresh, scale);
+      };
+      if (thresh) launch_y(std::true_type{});
+      else launch_y(std::false_type{});
+    } else if (thresh) {
       if (dse) launch(std::true_type{}, std::true_type{});
       else launch(std::true_type{}, std::false_type{});
     } else {

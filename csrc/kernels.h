@@ -152,10 +152,10 @@ int embed_segsum(const void* ds, const int* sorted, const int64_t* perm, void* d
                  hipStream_t s);
 int64_t bdaln_ws_floats(int64_t rows, int cols);
 // dse (nullable): extra gradient of s from its other consumers (pre-LN residual stream), added to ds
-int bdaln_bwd(const void* dy, const void* s_in, const void* gamma, const float* mean, const float* rstd,
-              const void* dse, void* dres, void* dx, void* dgamma, void* dbeta, void* dbias, float* ws,
-              int64_t rows, int cols, uint64_t seed, uint64_t offset, uint32_t thresh, float scale, int xdt,
-              int wdt, hipStream_t s);
+int bdaln_bwd(const void* dy, const void* s_in, const void* gamma, const void* beta, const float* mean,
+              const float* rstd, const void* dse, void* dres, void* dx, void* dgamma, void* dbeta, void* dbias,
+              float* ws, int64_t rows, int cols, uint64_t seed, uint64_t offset, uint32_t thresh, float scale,
+              int xdt, int wdt, hipStream_t s);  // beta != nullptr: s_in is the LN output y (post-LN, narrow)
 
 // ----------------------------- weight norm / RNN cells / SyncBN ------------
 int weight_norm_fwd(const void* v, const void* g, void* w, float* norms, int64_t R, int64_t C, int row_mode,

@@ -195,3 +195,37 @@ def test_bert_sublayer_fusion_matches_op_by_op(p):
     torch.testing.assert_close(dx1, dx2, rtol=3e-2, atol=3e-2)
     for n in g1:  # bias grads are 256-row sums of bf16 values: tolerance relative to their scale
         torch.testing.assert_close(g1[n], g2[n], rtol=5e-2, atol=5e-2 * max(1.0, float(g2[n].abs().max())), msg=n)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("cols,p", [(1024, 0.0), (1024, 0.1), (768, 0.1), (512, 0.0)])
+def test_bdaln_bwd_from_output_matches_stored_input(dt, cols, p):
+    """Memory-efficient post-LN (store_s=False forward, backward from y and beta) vs the stored-s
+    backward of the same forward: identical outputs, gradients within the 16-bit storage error, and
+    both against the fp32 autograd reference."""
+    C = _C()
+    torch.manual_seed(cols)
+    rows = 999
+    t = torch.randn(rows, cols, device=DEV).to(dt)
+    b = torch.randn(cols, device=DEV).to(dt)
+    res = torch.randn(rows, cols, device=DEV).to(dt)
+    g = (1 + 0.2 * torch.randn(cols, device=DEV)).to(dt)
+    be = (0.3 * torch.randn(cols, device=DEV)).to(dt)
+    dy = torch.randn(rows, cols, device=DEV).to(dt)
+    y, s, mean, rstd = C.bdaln_fwd(t, b, res, g, be, 1e-12, p, 11, 3)
+    y2, s2, mean2, rstd2 = C.bdaln_fwd(t, b, res, g, be, 1e-12, p, 11, 3, store_s=False)
+    assert s2.numel() == 0 and torch.equal(y, y2) and torch.equal(rstd, rstd2)
+    ref = C.bdaln_bwd(dy, s, g, mean, rstd, p, 11, 3, True)
+    got = C.bdaln_bwd(dy, y2, g, mean2, rstd2, p, 11, 3, True, beta=be)
+    for a, r, name in zip(got, ref, ("dres", "dx", "dgamma", "dbeta", "dbias")):
+        scale = r.float().abs().max().item() + 1e-6
+        err = (a.float() - r.float()).abs().max().item() / scale
+        assert err < (2e-2 if dt == torch.bfloat16 else 4e-3), (name, err)
+    if p == 0.0:  # against fp32 autograd of LN(res + t + b)
+        leaves = [x.float().requires_grad_(True) for x in (t, b, res, g, be)]
+        tr, br, rr, gr, ber = leaves
+        F.layer_norm(rr + tr + br, (cols,), gr, ber, 1e-12).backward(dy.float())
+        tol = 3e-2 if dt == torch.bfloat16 else 5e-3
+        for a, r, name in ((got[0], rr.grad, "dres"), (got[2], gr.grad, "dgamma"), (got[3], ber.grad, "dbeta")):
+            err = (a.float() - r).abs().max().item() / (r.abs().max().item() + 1e-6)
+            assert err < 4 * tol, (name, err)
