@@ -282,7 +282,7 @@ __global__ void __launch_bounds__(kEwBlock) bdaln_fwd_kernel(const T* __restrict
 // so the forward need not store s at all (one [rows, cols] write less per sublayer; y is saved
 // anyway as the next GEMM's input). dgamma accumulates dy * (y - beta) and is divided by gamma once.
 template <typename T, typename W, int VPT, bool DROP, bool EXTRA = false, bool FROMY = false>
-__global__ void __launch_bounds__(kEwBlock) __attribute__((amdgpu_waves_per_eu(FROMY ? 3 : 1))) bdaln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ s,
+__global__ void __launch_bounds__(kEwBlock) bdaln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ s,
                                                             const W* __restrict__ gamma,
                                                             const W* __restrict__ beta,
                                                             const float* __restrict__ mean,
@@ -321,6 +321,16 @@ __global__ void __launch_bounds__(kEwBlock) __attribute__((amdgpu_waves_per_eu(F
     }
   };
   fetch(r0 + wid);
+  if constexpr (FROMY) {
+    // beta and 1/gamma (fp32) staged once in the head of the partial-combine LDS buffer (free until
+    // the row loop ends): per row they come back as 16-byte LDS reads — a register copy took the
+    // kernel from 3 to 2 waves per SIMD, per-row global reads put an L2 round trip on every row
+    for (int c = threadIdx.x; c < cols; c += kEwBlock) {
+      lds[c] = to_f(beta[c]);
+      lds[cols + c] = 1.f / to_f(gamma[c]);
+    }
+    __syncthreads();
+  }
   for (int rr = 0; rr < rows_per_wave; ++rr) {
     const int64_t row = r0 + (int64_t)rr * 4 + wid;
     if (row >= rows) break;
@@ -336,16 +346,17 @@ __global__ void __launch_bounds__(kEwBlock) __attribute__((amdgpu_waves_per_eu(F
     if (rr + 1 < rows_per_wave) fetch(row + 4);
     const float mu = FROMY ? 0.f : mean[row], rs = rstd[row];
     float s1 = 0.f, s2 = 0.f;
-    // FROMY: beta and 1/gamma are re-read / re-derived per row (L1-resident beta, v_rcp) instead of
-    // held in registers across the row loop, which took the kernel from 3 to 2 waves per SIMD; the
-    // empty asm keeps the compiler from hoisting them back out
-    if constexpr (FROMY) asm volatile("" ::: "memory");
 #pragma unroll
     for (int j = 0; j < VPT; ++j) {
       const int vi = j * 64 + lane;
       if (vi < nvec) {
-        float bt[8];
-        if constexpr (FROMY) load_f<W, 8>(beta + vi * 8, bt);
+        float bt[8], ig[8];
+        if constexpr (FROMY) {
+          *reinterpret_cast<float4*>(bt) = *reinterpret_cast<const float4*>(lds + vi * 8);
+          *reinterpret_cast<float4*>(bt + 4) = *reinterpret_cast<const float4*>(lds + vi * 8 + 4);
+          *reinterpret_cast<float4*>(ig) = *reinterpret_cast<const float4*>(lds + cols + vi * 8);
+          *reinterpret_cast<float4*>(ig + 4) = *reinterpret_cast<const float4*>(lds + cols + vi * 8 + 4);
+        }
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const float dyg = dv[j][k] * g[j][k];
@@ -354,9 +365,7 @@ __global__ void __launch_bounds__(kEwBlock) __attribute__((amdgpu_waves_per_eu(F
             const float yc = xh[j][k] - bt[k];  // = x-hat * gamma
             s2 += dv[j][k] * yc;
             dg[j][k] += dv[j][k] * yc;  // / gamma at the end
-            float gk = g[j][k];
-            asm volatile("" : "+v"(gk));
-            xh[j][k] = yc * __builtin_amdgcn_rcpf(gk);
+            xh[j][k] = yc * ig[k];
           } else {
             xh[j][k] = (xh[j][k] - mu) * rs;
             s2 += dyg * xh[j][k];
@@ -391,6 +400,7 @@ __global__ void __launch_bounds__(kEwBlock) __attribute__((amdgpu_waves_per_eu(F
       }
     }
   }
+  if constexpr (FROMY) __syncthreads();  // every wave is done with the staged beta / 1/gamma
   float* mine = lds + wid * 3 * cols;
 #pragma unroll
   for (int j = 0; j < VPT; ++j) {
