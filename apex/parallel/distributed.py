@@ -44,6 +44,8 @@ from torch.nn.modules import Module
 from .. import _ext
 from ..utils import prof
 
+_ALIGN_SLOTS = os.environ.get("APEX_DDP_ALIGN", "1") != "0"  # 16-byte gradient slots (A/B knob)
+
 # ----------------------------------------------------------------------------
 # flat collective helpers (R-17)
 # ----------------------------------------------------------------------------
@@ -702,7 +704,14 @@ class DistributedDataParallel(Module):
         self._buckets = []
         self._param_bucket = {}
         for dt, idxs in by_dtype.items():
-            total = sum(self._params[i].numel() for i in idxs)
+            # every slot starts on a 16-byte boundary: one odd-sized parameter (BERT's 30522-entry
+            # MLM bias) otherwise shifts every later gradient view off alignment, and the fused
+            # multi-tensor kernels (grad norm, LAMB / Adam) drop to their scalar path for the
+            # whole parameter list (the plan's `aligned` flag is all-or-nothing)
+            al = max(1, 16 // torch.empty((), dtype=dt).element_size()) if _ALIGN_SLOTS else 1
+            total = 0
+            for i in idxs:
+                total = -(-total // al) * al + self._params[i].numel()
             dev = self._params[idxs[0]].device
             flat = torch.zeros(total, dtype=dt, device=dev)
             flat._apex_nparams = len(idxs)  # lets fused optimizers zero the grads with one fill
@@ -712,6 +721,7 @@ class DistributedDataParallel(Module):
             for i in idxs:
                 p = self._params[i]
                 n = p.numel()
+                off = -(-off // al) * al
                 if p.is_contiguous() or not _dense_non_overlapping(p):
                     v = flat[off:off + n].view(p.shape)
                 else:  # e.g. channels_last conv weight: the grad view keeps the param's strides

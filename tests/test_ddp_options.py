@@ -207,11 +207,13 @@ def test_bucket_layout_world8(fake_world8):
     model().backward()
     # grad-ready order is reverse of use: params 5,4,3,2,1,0 (sizes 400,20,700,50,300,100)
     got = [(b.numel, [sizes[i] for i in b.params]) for b in model._buckets]
-    # first bucket cut at >=150 elements, then every >=500
-    assert got == [(400, [400]), (720, [20, 700]), (450, [50, 300, 100])], got
+    # first bucket cut at >=150 elements, then every >=500; every slot starts on a 16-byte
+    # boundary (fp32: 4 elements), so the 50-element grad is followed by 2 padding elements
+    assert got == [(400, [400]), (720, [20, 700]), (452, [50, 300, 100])], got
     # grads are views of one flat buffer laid out in bucket order
     flat = model.allreduce_buffers[0]
-    assert flat.numel() == sum(sizes)
+    assert flat.numel() == sum(sizes) + 2
+    assert all(p.grad.data_ptr() % 16 == 0 for p in params)
     for i, p in enumerate(params):
         assert p.grad.data_ptr() >= flat.data_ptr()
         # the fake collective sums nothing, so the average leaves grad / world
@@ -222,7 +224,7 @@ def test_bucket_layout_world8(fake_world8):
     assert model._next_bucket == len(model._buckets)
     st = model.comm_stats()
     assert st["world_size"] == 8 and st["num_buckets"] == 3
-    assert st["bucket_bytes"] == [400 * 4, 720 * 4, 450 * 4]
+    assert st["bucket_bytes"] == [400 * 4, 720 * 4, 452 * 4]
 
 
 def test_broadcast_layout_from_rank0_world8(fake_world8, monkeypatch):
