@@ -43,7 +43,16 @@ int attn_fwd(const AttnArgs& a, int dt, hipStream_t s) {
   }
 }
 
-bool attn_bwd_needs_dq_acc(const AttnArgs& a) { return a.Sk > kBwdBK; }
+// Two-kernel backward (key-stationary dK/dV + query-stationary dQ, delta pre-pass) for key ranges
+// longer than one 128-key block; APEX_ATTN_BWD_SPLIT=1 also selects it for short ones (A/B knob)
+bool attn_bwd_split() {
+  static const bool on = [] {
+    const char* e = getenv("APEX_ATTN_BWD_SPLIT");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+bool attn_bwd_needs_dq_acc(const AttnArgs& a) { return a.Sk > kBwdBK || attn_bwd_split(); }
 
 int attn_bwd(const AttnArgs& a, const void* dout, float* delta_ws, void* dk, void* dv, int dt,
              hipStream_t s) {

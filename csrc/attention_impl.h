@@ -1184,7 +1184,7 @@ template <int D>
 int attn_bwd_impl(const AttnArgs& a, const void* dout, float* delta_ws, void* dk, void* dv, int dt,
                   hipStream_t s) {
   const bool drop = a.drop_thresh > 0;
-  const bool multi = a.Sk > kBwdBK;
+  const bool multi = attn_bwd_needs_dq_acc(a);
   if (multi && !delta_ws) return -4;
   if (a.bias && a.dsum) return -5;  // (not instantiated: the packed-QKV bias-grad fusion runs without a score bias)
   // (B*H, blocks) grids, heaviest blocks first under a causal mask (see attn_fwd_impl)

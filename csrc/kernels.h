@@ -109,6 +109,7 @@ inline uint32_t attn_drop_thresh(double p) {  // 8-bit keep threshold in [1, 255
 }
 int attn_fwd(const AttnArgs& a, int dt, hipStream_t s);
 bool attn_bwd_needs_dq_acc(const AttnArgs& a);
+bool attn_bwd_split();
 // delta_ws: [B*H*Sq] fp32 workspace when attn_bwd_needs_dq_acc (two-kernel backward)
 int attn_bwd(const AttnArgs& a, const void* dout, float* delta_ws, void* dk, void* dv, int dt,
              hipStream_t s);
