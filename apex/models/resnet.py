@@ -4,13 +4,26 @@ FusedSGD + SyncBatchNorm") and the model of the reference's ImageNet examples
 
 Convolutions run on MIOpen through PyTorch (library GEMM-class work); BatchNorm can be
 swapped for apex.parallel.SyncBatchNorm with ``convert_syncbn_model`` (HIP Welford
-kernels + one RCCL all-gather per layer). ``channels_last`` keeps activations NHWC,
+kernels + one RCCL all-gather per layer); ``fuse_bn_relu`` then folds the ReLUs and each block's
+residual add into the SyncBatchNorm kernels. ``channels_last`` keeps activations NHWC,
 the layout MIOpen's fastest bf16 kernels use.
 """
 from __future__ import annotations
 
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
+
+
+def _bn_relu(bn, x, z=None):
+    """relu(bn(x) (+ z)) — one fused HIP kernel each way when ``bn`` is an apex SyncBatchNorm with
+    ``fuse_relu`` set (``fuse_bn_relu``), else BatchNorm, add and ReLU as separate ops."""
+    if getattr(bn, "fuse_relu", False):
+        return bn(x, z) if z is not None else bn(x)
+    y = bn(x)
+    if z is not None:
+        y = y + z
+    return F.relu(y, inplace=True)
 
 
 def conv3x3(i, o, stride=1, groups=1, dilation=1):
@@ -35,9 +48,8 @@ class BasicBlock(nn.Module):
 
     def forward(self, x):
         idt = x if self.downsample is None else self.downsample(x)
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.bn2(self.conv2(out))
-        return self.relu(out + idt)
+        out = _bn_relu(self.bn1, self.conv1(x))
+        return _bn_relu(self.bn2, self.conv2(out), idt)
 
 
 class Bottleneck(nn.Module):
@@ -56,10 +68,9 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         idt = x if self.downsample is None else self.downsample(x)
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.relu(self.bn2(self.conv2(out)))
-        out = self.bn3(self.conv3(out))
-        return self.relu(out + idt)
+        out = _bn_relu(self.bn1, self.conv1(x))
+        out = _bn_relu(self.bn2, self.conv2(out))
+        return _bn_relu(self.bn3, self.conv3(out), idt)
 
 
 class ResNet(nn.Module):
@@ -100,9 +111,25 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.maxpool(_bn_relu(self.bn1, self.conv1(x)))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         return self.fc(torch.flatten(self.avgpool(x), 1))
+
+
+def fuse_bn_relu(model):
+    """Set ``fuse_relu`` on every apex SyncBatchNorm that a ReLU follows (the stem, each block's
+    inner norms and its output norm, whose residual add is fused too — not the downsample norms):
+    BN + add + ReLU become one HIP kernel each way. Run after ``convert_syncbn_model``."""
+    from ..parallel.sync_batchnorm import SyncBatchNorm
+
+    bns = [model.bn1] if hasattr(model, "bn1") else []
+    for m in model.modules():
+        if isinstance(m, (BasicBlock, Bottleneck)):
+            bns += [m.bn1, m.bn2] + ([m.bn3] if isinstance(m, Bottleneck) else [])
+    for bn in bns:
+        if isinstance(bn, SyncBatchNorm):
+            bn.fuse_relu = True
+    return model
 
 
 def resnet18(**kw):

@@ -51,9 +51,14 @@ def _bshape(x, channel_last):
 
 
 class SyncBatchnormFunction(torch.autograd.Function):
+    """y = BN(input) (+ z) (+ ReLU). The residual ``z`` and the ReLU are fused into the HIP
+    elementwise kernel; backward masks the gradient with the saved output inside the reduce /
+    elementwise kernels (no separate mask pass) and returns the residual's gradient from the same
+    pass (the ResNet bottleneck tail relu(bn3(conv3) + identity) as one kernel each way)."""
+
     @staticmethod
     def forward(ctx, input, weight, bias, running_mean, running_var, eps, momentum, group, channel_last,
-                fuse_relu):
+                fuse_relu, z=None):
         native = _ext.use_native(input)
         x = input.contiguous()  # channel_last: logical [N, ..., C] layout (apex convention)
         C = _ext.require() if native else None
@@ -76,8 +81,10 @@ class SyncBatchnormFunction(torch.autograd.Function):
                 running_mean.mul_(1 - momentum).add_(mean.to(running_mean.dtype), alpha=momentum)
                 running_var.mul_(1 - momentum).add_(unbiased.to(running_var.dtype), alpha=momentum)
         invstd = torch.rsqrt(var + eps)
+        has_z = z is not None
         if native:
-            y = C.bn_elemt(x, mean, invstd, weight, bias, channel_last, fuse_relu)
+            y = C.bn_elemt(x, mean, invstd, weight, bias, channel_last, fuse_relu,
+                           z=z.contiguous() if has_z else None)
         else:
             sh = _bshape(x, channel_last)
             y = (x.float() - mean.view(sh)) * invstd.view(sh)
@@ -85,25 +92,28 @@ class SyncBatchnormFunction(torch.autograd.Function):
                 y = y * weight.float().view(sh)
             if bias is not None:
                 y = y + bias.float().view(sh)
+            if has_z:
+                y = y + z.float()
             if fuse_relu:
                 y = torch.relu(y)
             y = y.to(x.dtype)
         # the global count stays on the device (a float(count) here was one host round trip per
         # BatchNorm layer per forward)
         ctx.save_for_backward(x, weight, mean, invstd, y if fuse_relu else None, count)
-        ctx.cfg = (group, channel_last, fuse_relu, native, bias is not None)
+        ctx.cfg = (group, channel_last, fuse_relu, native, bias is not None, has_z)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, weight, mean, invstd, y, count = ctx.saved_tensors
-        group, channel_last, fuse_relu, native, has_bias = ctx.cfg
+        group, channel_last, fuse_relu, native, has_bias, has_z = ctx.cfg
         dy = dy.contiguous()
-        if fuse_relu:
+        if fuse_relu and not native:
             dy = dy * (y > 0).to(dy.dtype)
+        ym = y if (fuse_relu and native) else None  # the kernels mask with the saved output
         if native:
             C = _ext.require()
-            sums = C.bn_bwd_reduce(dy, x, mean, channel_last)
+            sums = C.bn_bwd_reduce(dy, x, mean, channel_last, ym=ym)
         else:
             sh = _bshape(x, channel_last)
             dims = [d for d in range(x.dim()) if d != (x.dim() - 1 if channel_last else 1)]
@@ -113,8 +123,12 @@ class SyncBatchnormFunction(torch.autograd.Function):
             dist.all_reduce(sums, group=group)
         dw = (sums[1] * invstd).to(weight.dtype) if weight is not None and ctx.needs_input_grad[1] else None
         db = sums[0].to(weight.dtype) if has_bias and ctx.needs_input_grad[2] else None
+        dz = None
         if native:
-            dx = C.bn_bwd_elemt(dy, x, mean, invstd, weight, sums, count.contiguous(), channel_last)
+            dx, dz = C.bn_bwd_elemt(dy, x, mean, invstd, weight, sums, count.contiguous(), channel_last, ym=ym,
+                                    with_dz=has_z and ym is not None)
+            if has_z and ym is None:
+                dz = dy  # no ReLU: the residual's gradient is dy itself
         else:
             sh = _bshape(x, channel_last)
             total = count.clamp(min=1)
@@ -125,7 +139,8 @@ class SyncBatchnormFunction(torch.autograd.Function):
             if weight is not None:
                 dx = dx * weight.float().view(sh)
             dx = dx.to(x.dtype)
-        return dx, dw, db, None, None, None, None, None, None, None
+            dz = dy if has_z else None
+        return dx, dw, db, None, None, None, None, None, None, None, (dz if has_z else None)
 
 
 class SyncBatchNorm(_BatchNorm):
@@ -150,16 +165,18 @@ class SyncBatchNorm(_BatchNorm):
         self.channel_last = channel_last
 
     def forward(self, input, z=None):
+        """BN(input), plus ``z`` (a residual of input's shape, added after the affine transform) and
+        the ReLU when ``fuse_relu`` — relu(BN(input) + z), NVIDIA Apex's fused SyncBatchNorm
+        semantics — in one HIP kernel each way."""
         self._check_input_dim(input)
-        if z is not None:
-            input = input + z
         if (not self.channel_last and input.dim() == 4 and input.shape[1] > 1
                 and input.is_contiguous(memory_format=torch.channels_last) and not input.is_contiguous()):
             # torch channels_last (NCHW shape, NHWC storage): run the NHWC kernels on the
             # zero-copy [N, H, W, C] view instead of transposing to NCHW and back
             self.channel_last = True
             try:
-                return self.forward(input.permute(0, 2, 3, 1)).permute(0, 3, 1, 2)
+                zz = z.permute(0, 2, 3, 1) if z is not None else None
+                return self.forward(input.permute(0, 2, 3, 1), zz).permute(0, 3, 1, 2)
             finally:
                 self.channel_last = False
         if self.training and self.track_running_stats:
@@ -170,12 +187,15 @@ class SyncBatchNorm(_BatchNorm):
             invstd = torch.rsqrt(self.running_var.float() + self.eps)
             if _ext.use_native(input):
                 y = _ext.require().bn_elemt(input.contiguous(), mean, invstd, self.weight, self.bias,
-                                            self.channel_last, self.fuse_relu)
+                                            self.channel_last, self.fuse_relu,
+                                            z=z.contiguous() if z is not None else None)
                 return y
             sh = _bshape(input, self.channel_last)
             y = (input.float() - mean.view(sh)) * invstd.view(sh)
             if self.weight is not None:
                 y = y * self.weight.float().view(sh) + self.bias.float().view(sh)
+            if z is not None:
+                y = y + z.float()
             y = torch.relu(y) if self.fuse_relu else y
             return y.to(input.dtype)
         momentum = self.momentum if self.momentum is not None else 0.0
@@ -183,7 +203,7 @@ class SyncBatchNorm(_BatchNorm):
                                            self.running_mean if self.track_running_stats else None,
                                            self.running_var if self.track_running_stats else None,
                                            self.eps, momentum, self.process_group, self.channel_last,
-                                           self.fuse_relu)
+                                           self.fuse_relu, z)
 
 
 def convert_syncbn_model(module, process_group=None, channel_last=False):

@@ -4,7 +4,7 @@ N>1), img/s. Synthetic normalised images (NHWC/channels_last, MIOpen's fast bf16
 random-init weights. Throughput = world x batch / step time (the reference's definition,
 examples/imagenet/main.py:348,354).
 
-  python benchmarks/resnet50.py [--batch 256] [--steps 20] [--warmup 5] [--no-syncbn] [--fp32]
+  python benchmarks/resnet50.py [--batch 256] [--steps 20] [--warmup 5] [--no-syncbn] [--no-fuse-bn] [--fp32]
   torchrun --nproc-per-node N benchmarks/resnet50.py ...
 """
 import argparse
@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-syncbn", action="store_true")
+    ap.add_argument("--no-fuse-bn", action="store_true", help="BN, residual add and ReLU as separate ops")
     ap.add_argument("--nchw", action="store_true", help="keep NCHW activations")
     ap.add_argument("--fp32", action="store_true")
     ap.add_argument("--conv-search", action="store_true",
@@ -38,7 +39,7 @@ def main():
     env = init_distributed(single_rank_group=True)  # apex DDP at every N (hooks + buckets timed at N=1 too)
     import apex
     from apex import amp
-    from apex.models.resnet import resnet50, synthetic_batch
+    from apex.models.resnet import fuse_bn_relu, resnet50, synthetic_batch
     from apex.optimizers import FusedSGD
     from apex.parallel import DistributedDataParallel as DDP
     from apex.parallel import convert_syncbn_model
@@ -48,6 +49,8 @@ def main():
     model = resnet50()
     if not args.no_syncbn:
         model = convert_syncbn_model(model)  # channels_last inputs take the NHWC kernels
+        if not args.no_fuse_bn:
+            fuse_bn_relu(model)  # BN + residual add + ReLU as one HIP kernel each way
     cl = not args.nchw
     model = model.to(env.device, memory_format=torch.channels_last if cl else torch.contiguous_format)
     opt = FusedSGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)

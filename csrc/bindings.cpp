@@ -790,50 +790,73 @@ std::vector<Tensor> k_bn_combine(Tensor gathered) {
   return {mean, var, cnt};
 }
 
+// z: optional residual added after the affine, before the ReLU (same shape / layout as x)
 Tensor k_bn_elemt(Tensor x, Tensor mean, Tensor invstd, const c10::optional<Tensor>& w,
-                  const c10::optional<Tensor>& b, bool nhwc, bool relu) {
+                  const c10::optional<Tensor>& b, bool nhwc, bool relu, const c10::optional<Tensor>& z) {
   auto d = bn_dims(x, nhwc);
+  Tensor zc;
+  if (z.has_value() && z->defined()) {
+    zc = z->contiguous();
+    TORCH_CHECK(zc.sizes() == x.sizes() && zc.scalar_type() == x.scalar_type(), "bn_elemt: z like x");
+  }
   Tensor y = at::empty_like(x);
   const int wdt = w.has_value() && w->defined() ? dt_code(w->scalar_type()) : apex::kF32Code;
   Tensor coef = at::empty({2 * d[1] + 4}, x.options().dtype(at::kFloat));
   check(apex::bn_elemt(x.data_ptr(), mean.data_ptr<float>(), invstd.data_ptr<float>(), opt_vptr(w), opt_vptr(b),
-                       y.data_ptr(), d[0], d[1], d[2], nhwc, relu, dt_code(x.scalar_type()), wdt,
+                       zc.defined() ? zc.data_ptr() : nullptr, y.data_ptr(), d[0], d[1], d[2], nhwc, relu, dt_code(x.scalar_type()), wdt,
                        coef.data_ptr<float>(), cur_stream()),
         "bn_elemt");
   return y;
 }
 
 // local (sum_dy, sum_dy_xmu) -> [2, C]
-Tensor k_bn_bwd_reduce(Tensor dy, Tensor x, Tensor mean, bool nhwc) {
+// ym: optional forward output of a fused-ReLU bn_elemt (the gradient counts only where ym > 0)
+Tensor k_bn_bwd_reduce(Tensor dy, Tensor x, Tensor mean, bool nhwc, const c10::optional<Tensor>& ym) {
   auto d = bn_dims(x, nhwc);
   Tensor dyc = dy.contiguous();
+  Tensor yc;
+  if (ym.has_value() && ym->defined()) {
+    yc = ym->contiguous();
+    TORCH_CHECK(yc.sizes() == x.sizes() && yc.scalar_type() == x.scalar_type(), "bn_bwd_reduce: ym like x");
+  }
   const int sp = apex::bn_splits_for(d[0], d[1], d[2], nhwc, dt_code(x.scalar_type()));
   auto fo = x.options().dtype(at::kFloat);
   Tensor part = at::empty({d[1] * sp * 2}, fo);
   Tensor out = at::empty({2, d[1]}, fo);
-  check(apex::bn_bwd_reduce(dyc.data_ptr(), x.data_ptr(), mean.data_ptr<float>(), part.data_ptr<float>(),
+  check(apex::bn_bwd_reduce(dyc.data_ptr(), x.data_ptr(), yc.defined() ? yc.data_ptr() : nullptr,
+                            mean.data_ptr<float>(), part.data_ptr<float>(),
                             out.data_ptr<float>(), out.data_ptr<float>() + d[1], d[0], d[1], d[2], nhwc,
                             dt_code(x.scalar_type()), cur_stream()),
         "bn_bwd_reduce");
   return out;
 }
 
-Tensor k_bn_bwd_elemt(Tensor dy, Tensor x, Tensor mean, Tensor invstd, const c10::optional<Tensor>& w,
-                      Tensor sums, Tensor count, bool nhwc) {
+// ym: as k_bn_bwd_reduce; with_dz: also return the masked gradient (the fused residual's gradient)
+std::vector<Tensor> k_bn_bwd_elemt(Tensor dy, Tensor x, Tensor mean, Tensor invstd, const c10::optional<Tensor>& w,
+                                   Tensor sums, Tensor count, bool nhwc, const c10::optional<Tensor>& ym,
+                                   bool with_dz) {
   auto d = bn_dims(x, nhwc);
   TORCH_CHECK(count.is_cuda() && count.scalar_type() == at::kFloat && count.numel() == d[1] && count.is_contiguous(),
               "bn_bwd_elemt: count must be the fp32 [C] device tensor from bn_combine");
   Tensor dyc = dy.contiguous();
   Tensor dx = at::empty_like(x);
   Tensor sc = sums.contiguous();
+  Tensor yc, dz;
+  if (ym.has_value() && ym->defined()) {
+    yc = ym->contiguous();
+    TORCH_CHECK(yc.sizes() == x.sizes() && yc.scalar_type() == x.scalar_type(), "bn_bwd_elemt: ym like x");
+  }
+  TORCH_CHECK(!with_dz || yc.defined(), "bn_bwd_elemt: with_dz needs ym");
+  if (with_dz) dz = at::empty_like(x);
   Tensor coef = at::empty({3 * d[1] + 4}, x.options().dtype(at::kFloat));
   const int wdt = w.has_value() && w->defined() ? dt_code(w->scalar_type()) : apex::kF32Code;
   check(apex::bn_bwd_elemt(dyc.data_ptr(), x.data_ptr(), mean.data_ptr<float>(), invstd.data_ptr<float>(),
                            opt_vptr(w), sc.data_ptr<float>(), sc.data_ptr<float>() + d[1],
-                           count.data_ptr<float>(), dx.data_ptr(), d[0], d[1], d[2], nhwc,
+                           count.data_ptr<float>(), yc.defined() ? yc.data_ptr() : nullptr,
+                           with_dz ? dz.data_ptr() : nullptr, dx.data_ptr(), d[0], d[1], d[2], nhwc,
                            dt_code(x.scalar_type()), wdt, coef.data_ptr<float>(), cur_stream()),
         "bn_bwd_elemt");
-  return dx;
+  return {dx, dz};
 }
 
 // --------------------------------------------------------------------------
@@ -1278,9 +1301,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gru_cell_bwd", &k_gru_bwd);
   m.def("bn_local_stats", &k_bn_local_stats);
   m.def("bn_combine", &k_bn_combine);
-  m.def("bn_elemt", &k_bn_elemt);
-  m.def("bn_bwd_reduce", &k_bn_bwd_reduce);
-  m.def("bn_bwd_elemt", &k_bn_bwd_elemt);
+  m.def("bn_elemt", &k_bn_elemt, py::arg("x"), py::arg("mean"), py::arg("invstd"), py::arg("w"), py::arg("b"),
+        py::arg("nhwc"), py::arg("relu"), py::arg("z") = py::none());
+  m.def("bn_bwd_reduce", &k_bn_bwd_reduce, py::arg("dy"), py::arg("x"), py::arg("mean"), py::arg("nhwc"),
+        py::arg("ym") = py::none());
+  m.def("bn_bwd_elemt", &k_bn_bwd_elemt, py::arg("dy"), py::arg("x"), py::arg("mean"), py::arg("invstd"),
+        py::arg("w"), py::arg("sums"), py::arg("count"), py::arg("nhwc"), py::arg("ym") = py::none(),
+        py::arg("with_dz") = false);
   m.def("scaled_softmax_supported", &k_smx_supported);
   m.def("scaled_masked_softmax_fwd", &k_smx_fwd);
   m.def("scaled_masked_softmax_bwd", &k_smx_bwd);

@@ -176,13 +176,17 @@ int bn_stats(const void* x, float* part, int64_t N, int64_t C, int64_t S, int nh
              hipStream_t s);
 int bn_combine(const float* in, int groups, int64_t C, int gmajor, float* mean, float* var, float* count,
                hipStream_t s);
-int bn_elemt(const void* x, const float* mean, const float* invstd, const void* w, const void* b, void* y,
-             int64_t N, int64_t C, int64_t S, int nhwc, int relu, int dt, int wdt, float* coef, hipStream_t s);
-int bn_bwd_reduce(const void* dy, const void* x, const float* mean, float* part, float* sum_dy,
+// Fused residual + ReLU (ResNet blocks): bn_elemt adds z (nullable, x's layout) after the affine
+// and before the ReLU; the backward kernels take the forward output ym (nullable) and pass the
+// gradient only where ym > 0; bn_bwd_elemt also writes that masked gradient to dz (z's gradient).
+int bn_elemt(const void* x, const float* mean, const float* invstd, const void* w, const void* b, const void* z,
+             void* y, int64_t N, int64_t C, int64_t S, int nhwc, int relu, int dt, int wdt, float* coef,
+             hipStream_t s);
+int bn_bwd_reduce(const void* dy, const void* x, const void* ym, const float* mean, float* part, float* sum_dy,
                   float* sum_dy_xmu, int64_t N, int64_t C, int64_t S, int nhwc, int dt, hipStream_t s);
 int bn_bwd_elemt(const void* dy, const void* x, const float* mean, const float* invstd, const void* w,
-                 const float* sum_dy, const float* sum_dy_xmu, const float* count, void* dx, int64_t N, int64_t C,
-                 int64_t S, int nhwc, int dt, int wdt, float* coef, hipStream_t s);
+                 const float* sum_dy, const float* sum_dy_xmu, const float* count, const void* ym, void* dz,
+                 void* dx, int64_t N, int64_t C, int64_t S, int nhwc, int dt, int wdt, float* coef, hipStream_t s);
 
 // ----------------------------- fused scale-mask softmax --------------------
 // mode 0: scale only, 1: byte mask [B, mask_heads, sq, cols] (nonzero masked), 2: causal

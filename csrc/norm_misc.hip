@@ -347,14 +347,16 @@ __global__ void bn_combine_kernel(const float* __restrict__ in, int groups, int6
 template <typename T, typename W>
 __global__ void __launch_bounds__(256) bn_elemt_kernel(const T* __restrict__ x, const float* __restrict__ mean,
                                                       const float* __restrict__ invstd, const W* __restrict__ w,
-                                                      const W* __restrict__ b, T* __restrict__ y, int64_t N,
-                                                      int64_t C, int64_t S, int nhwc, int relu) {
+                                                      const W* __restrict__ b, const T* __restrict__ z,
+                                                      T* __restrict__ y, int64_t N, int64_t C, int64_t S, int nhwc,
+                                                      int relu) {
   const int64_t total = N * C * S;
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
     const int64_t c = nhwc ? e % C : (e / S) % C;
     float v = (to_f(x[e]) - mean[c]) * invstd[c];
     if (w) v *= to_f(w[c]);
     if (b) v += to_f(b[c]);
+    if (z) v += to_f(z[e]);
     if (relu) v = fmaxf(v, 0.f);
     y[e] = from_f<T>(v);
   }
@@ -363,7 +365,7 @@ __global__ void __launch_bounds__(256) bn_elemt_kernel(const T* __restrict__ x, 
 // partial sums per channel: sum(dy), sum(dy * (x - mean)) ; grid (C, splits)
 template <typename T>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ x,
-                                                           const float* __restrict__ mean,
+                                                           const T* __restrict__ ym, const float* __restrict__ mean,
                                                            float* __restrict__ part, int64_t N, int64_t C,
                                                            int64_t S, int nhwc) {
   __shared__ float red[4];
@@ -376,7 +378,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const T* __restrict_
   for (int64_t e = e0 + threadIdx.x; e < e1; e += 256) {
     const int64_t n = e / S, s3 = e % S;
     const int64_t off = nhwc ? e * C + c : (n * C + c) * S + s3;
-    const float d = to_f(dy[off]);
+    const float d = ym && !(to_f(ym[off]) > 0.f) ? 0.f : to_f(dy[off]);
     s1 += d;
     s2 += d * (to_f(x[off]) - mu);
   }
@@ -410,6 +412,7 @@ __global__ void __launch_bounds__(256) bn_bwd_elemt_kernel(const T* __restrict__
                                                           const W* __restrict__ w, const float* __restrict__ sum_dy,
                                                           const float* __restrict__ sum_dy_xmu,
                                                           const float* __restrict__ count,
+                                                          const T* __restrict__ ym, T* __restrict__ dz,
                                                           T* __restrict__ dx, int64_t N, int64_t C, int64_t S,
                                                           int nhwc) {
   const int64_t total = N * C * S;
@@ -419,7 +422,9 @@ __global__ void __launch_bounds__(256) bn_bwd_elemt_kernel(const T* __restrict__
     const float inv_count = 1.f / fmaxf(count[c], 1.f);
     const float mdy = sum_dy[c] * inv_count, mdx = sum_dy_xmu[c] * inv_count;
     const float xm = to_f(x[e]) - mean[c];
-    float v = (to_f(dy[e]) - mdy - xm * is * is * mdx) * is;
+    const float g = ym && !(to_f(ym[e]) > 0.f) ? 0.f : to_f(dy[e]);
+    if (dz) dz[e] = from_f<T>(g);
+    float v = (g - mdy - xm * is * is * mdx) * is;
     if (w) v *= to_f(w[c]);
     dx[e] = from_f<T>(v);
   }
@@ -621,12 +626,15 @@ __device__ __forceinline__ void load_coef(const float* __restrict__ k, int c0, f
 // nvec < 2^31 (checked by the launcher): 32-bit index math
 template <typename T>
 __global__ void __launch_bounds__(256) bn_elemt_vec(const T* __restrict__ x, const float* __restrict__ k,
-                                                   T* __restrict__ y, int nvec, int C, int S, int nhwc, int relu) {
+                                                   const T* __restrict__ z, T* __restrict__ y, int nvec, int C, int S,
+                                                   int nhwc, int relu) {
   constexpr int V = BnVec<T>::V;
   typedef typename BnVec<T>::P P;
   const int SV = S / V, CV = C / V;
   for (int e = blockIdx.x * 256 + threadIdx.x; e < nvec; e += gridDim.x * 256) {
     const P pk = *reinterpret_cast<const P*>(x + (int64_t)e * V);
+    P zk;
+    if (z) zk = *reinterpret_cast<const P*>(z + (int64_t)e * V);
     P o;
     if (nhwc) {
       const int c0 = (e % CV) * V;
@@ -636,6 +644,7 @@ __global__ void __launch_bounds__(256) bn_elemt_vec(const T* __restrict__ x, con
 #pragma unroll
       for (int i = 0; i < V; ++i) {
         float v = to_f(pk.v[i]) * k0[i] + k1[i];
+        if (z) v += to_f(zk.v[i]);
         if (relu) v = fmaxf(v, 0.f);
         o.v[i] = from_f<T>(v);
       }
@@ -645,6 +654,7 @@ __global__ void __launch_bounds__(256) bn_elemt_vec(const T* __restrict__ x, con
 #pragma unroll
       for (int i = 0; i < V; ++i) {
         float v = to_f(pk.v[i]) * k0 + k1;
+        if (z) v += to_f(zk.v[i]);
         if (relu) v = fmaxf(v, 0.f);
         o.v[i] = from_f<T>(v);
       }
@@ -655,7 +665,7 @@ __global__ void __launch_bounds__(256) bn_elemt_vec(const T* __restrict__ x, con
 
 template <typename T>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_nchw_vec(const T* __restrict__ dy, const T* __restrict__ x,
-                                                             const float* __restrict__ mean,
+                                                             const T* __restrict__ ym, const float* __restrict__ mean,
                                                              float* __restrict__ part, int N, int C, int S) {
   constexpr int V = BnVec<T>::V;
   typedef typename BnVec<T>::P P;
@@ -672,9 +682,11 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_nchw_vec(const T* __restric
     const int64_t off = ((int64_t)n * C + c) * S + (int64_t)sv * V;
     const P d = *reinterpret_cast<const P*>(dy + off);
     const P xv = *reinterpret_cast<const P*>(x + off);
+    P yv;
+    if (ym) yv = *reinterpret_cast<const P*>(ym + off);
 #pragma unroll
     for (int k = 0; k < V; ++k) {
-      const float g = to_f(d.v[k]);
+      const float g = ym && !(to_f(yv.v[k]) > 0.f) ? 0.f : to_f(d.v[k]);
       s1 += g;
       s2 += g * (to_f(xv.v[k]) - mu);
     }
@@ -689,7 +701,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_nchw_vec(const T* __restric
 
 template <typename T>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_nhwc_vec(const T* __restrict__ dy, const T* __restrict__ x,
-                                                             const float* __restrict__ mean,
+                                                             const T* __restrict__ ym, const float* __restrict__ mean,
                                                              float* __restrict__ part, int64_t R, int C, int cvb,
                                                              int rpb) {
   constexpr int V = BnVec<T>::V;
@@ -708,9 +720,11 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_nhwc_vec(const T* __restric
     for (int64_t r = (int64_t)blockIdx.y * rpb + tr; r < R; r += step) {
       const P d = *reinterpret_cast<const P*>(dy + r * C + (int64_t)cv * V);
       const P xv = *reinterpret_cast<const P*>(x + r * C + (int64_t)cv * V);
+      P yv;
+      if (ym) yv = *reinterpret_cast<const P*>(ym + r * C + (int64_t)cv * V);
 #pragma unroll
       for (int k = 0; k < V; ++k) {
-        const float g = to_f(d.v[k]);
+        const float g = ym && !(to_f(yv.v[k]) > 0.f) ? 0.f : to_f(d.v[k]);
         s1[k] += g;
         s2[k] += g * (to_f(xv.v[k]) - mu[k]);
       }
@@ -740,14 +754,22 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_nhwc_vec(const T* __restric
 
 template <typename T>
 __global__ void __launch_bounds__(256) bn_bwd_elemt_vec(const T* __restrict__ dy, const T* __restrict__ x,
-                                                       const float* __restrict__ k, T* __restrict__ dx, int nvec,
-                                                       int C, int S, int nhwc) {
+                                                       const float* __restrict__ k, const T* __restrict__ ym,
+                                                       T* __restrict__ dz, T* __restrict__ dx, int nvec, int C, int S,
+                                                       int nhwc) {
   constexpr int V = BnVec<T>::V;
   typedef typename BnVec<T>::P P;
   const int SV = S / V, CV = C / V;
   for (int e = blockIdx.x * 256 + threadIdx.x; e < nvec; e += gridDim.x * 256) {
-    const P d = *reinterpret_cast<const P*>(dy + (int64_t)e * V);
+    P d = *reinterpret_cast<const P*>(dy + (int64_t)e * V);
     const P xv = *reinterpret_cast<const P*>(x + (int64_t)e * V);
+    if (ym) {  // fused ReLU: the gradient passes where the forward output was positive
+      const P yv = *reinterpret_cast<const P*>(ym + (int64_t)e * V);
+#pragma unroll
+      for (int i = 0; i < V; ++i)
+        if (!(to_f(yv.v[i]) > 0.f)) d.v[i] = from_f<T>(0.f);
+      if (dz) *reinterpret_cast<P*>(dz + (int64_t)e * V) = d;  // the residual input's gradient
+    }
     P o;
     if (nhwc) {
       const int c0 = (e % CV) * V;
@@ -897,51 +919,53 @@ int bn_combine(const float* in, int groups, int64_t C, int gmajor, float* mean, 
   return (int)hipGetLastError();
 }
 
-int bn_elemt(const void* x, const float* mean, const float* invstd, const void* w, const void* b, void* y,
-             int64_t N, int64_t C, int64_t S, int nhwc, int relu, int dt, int wdt, float* coef, hipStream_t s) {
+int bn_elemt(const void* x, const float* mean, const float* invstd, const void* w, const void* b, const void* z,
+             void* y, int64_t N, int64_t C, int64_t S, int nhwc, int relu, int dt, int wdt, float* coef,
+             hipStream_t s) {
   const int64_t total = N * C * S;
   if (total == 0) return 0;
   if (!w && !b) wdt = kF32;
   const int V = bn_vec(dt);
-  if (coef && bn_vec_ok(x, N, C, S, nhwc, V) && ((uintptr_t)y & 15) == 0 && ((uintptr_t)coef & 15) == 0) {
+  if (coef && bn_vec_ok(x, N, C, S, nhwc, V) && ((uintptr_t)y & 15) == 0 && ((uintptr_t)coef & 15) == 0 &&
+      ((uintptr_t)z & 15) == 0) {
     NM_DISPATCH(wdt, W,
         hipLaunchKernelGGL((bn_coef_fwd_kernel<W>), dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, mean, invstd,
                            (const W*)w, (const W*)b, coef, (int)C));
     const int64_t nvec = total / V;
     const int64_t grid = min((nvec + 255) / 256, (int64_t)4096);
     NM_DISPATCH(dt, T,
-        hipLaunchKernelGGL((bn_elemt_vec<T>), dim3((unsigned)grid), dim3(256), 0, s, (const T*)x, coef, (T*)y,
-                           (int)nvec, (int)C, (int)S, nhwc, relu));
+        hipLaunchKernelGGL((bn_elemt_vec<T>), dim3((unsigned)grid), dim3(256), 0, s, (const T*)x, coef, (const T*)z,
+                           (T*)y, (int)nvec, (int)C, (int)S, nhwc, relu));
     return (int)hipGetLastError();
   }
   const int64_t grid = min((total + 255) / 256, (int64_t)8192);
   NM_DISPATCH(dt, T, NM_DISPATCH(wdt, W,
       hipLaunchKernelGGL((bn_elemt_kernel<T, W>), dim3((unsigned)grid), dim3(256), 0, s, (const T*)x, mean,
-                         invstd, (const W*)w, (const W*)b, (T*)y, N, C, S, nhwc, relu)));
+                         invstd, (const W*)w, (const W*)b, (const T*)z, (T*)y, N, C, S, nhwc, relu)));
   return (int)hipGetLastError();
 }
 
-int bn_bwd_reduce(const void* dy, const void* x, const float* mean, float* part, float* sum_dy,
+int bn_bwd_reduce(const void* dy, const void* x, const void* ym, const float* mean, float* part, float* sum_dy,
                   float* sum_dy_xmu, int64_t N, int64_t C, int64_t S, int nhwc, int dt, hipStream_t s) {
   if (C == 0) return 0;
   const int V = bn_vec(dt);
   const int sp = bn_splits(N, S, C, nhwc, V);
-  if (bn_vec_ok(x, N, C, S, nhwc, V) && ((uintptr_t)dy & 15) == 0) {
+  if (bn_vec_ok(x, N, C, S, nhwc, V) && ((uintptr_t)dy & 15) == 0 && ((uintptr_t)ym & 15) == 0) {
     if (nhwc) {
       int cvb, rpb, gx;
       bn_nhwc_geom(C, V, cvb, rpb, gx);
       NM_DISPATCH(dt, T,
           hipLaunchKernelGGL((bn_bwd_reduce_nhwc_vec<T>), dim3(gx, sp), dim3(256), 0, s, (const T*)dy,
-                             (const T*)x, mean, part, N * S, (int)C, cvb, rpb));
+                             (const T*)x, (const T*)ym, mean, part, N * S, (int)C, cvb, rpb));
     } else {
       NM_DISPATCH(dt, T,
           hipLaunchKernelGGL((bn_bwd_reduce_nchw_vec<T>), dim3((unsigned)C, sp), dim3(256), 0, s, (const T*)dy,
-                             (const T*)x, mean, part, (int)N, (int)C, (int)S));
+                             (const T*)x, (const T*)ym, mean, part, (int)N, (int)C, (int)S));
     }
   } else {
     NM_DISPATCH(dt, T,
         hipLaunchKernelGGL((bn_bwd_reduce_kernel<T>), dim3((unsigned)C, sp), dim3(256), 0, s, (const T*)dy,
-                           (const T*)x, mean, part, N, C, S, nhwc));
+                           (const T*)x, (const T*)ym, mean, part, N, C, S, nhwc));
   }
   if (sp >= 64)
     hipLaunchKernelGGL(bn_bwd_finalize_par_kernel, dim3((unsigned)C), dim3(256), 0, s, part, sp, sum_dy, sum_dy_xmu);
@@ -952,14 +976,14 @@ int bn_bwd_reduce(const void* dy, const void* x, const float* mean, float* part,
 }
 
 int bn_bwd_elemt(const void* dy, const void* x, const float* mean, const float* invstd, const void* w,
-                 const float* sum_dy, const float* sum_dy_xmu, const float* count, void* dx, int64_t N, int64_t C,
-                 int64_t S, int nhwc, int dt, int wdt, float* coef, hipStream_t s) {
+                 const float* sum_dy, const float* sum_dy_xmu, const float* count, const void* ym, void* dz,
+                 void* dx, int64_t N, int64_t C, int64_t S, int nhwc, int dt, int wdt, float* coef, hipStream_t s) {
   const int64_t total = N * C * S;
   if (total == 0) return 0;
   if (!w) wdt = kF32;
   const int V = bn_vec(dt);
   if (coef && bn_vec_ok(x, N, C, S, nhwc, V) && ((uintptr_t)dy & 15) == 0 && ((uintptr_t)dx & 15) == 0 &&
-      ((uintptr_t)coef & 15) == 0) {
+      ((uintptr_t)coef & 15) == 0 && ((uintptr_t)ym & 15) == 0 && ((uintptr_t)dz & 15) == 0) {
     NM_DISPATCH(wdt, W,
         hipLaunchKernelGGL((bn_coef_bwd_kernel<W>), dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, mean, invstd,
                            (const W*)w, sum_dy, sum_dy_xmu, count, coef, (int)C));
@@ -967,14 +991,14 @@ int bn_bwd_elemt(const void* dy, const void* x, const float* mean, const float* 
     const int64_t grid = min((nvec + 255) / 256, (int64_t)4096);
     NM_DISPATCH(dt, T,
         hipLaunchKernelGGL((bn_bwd_elemt_vec<T>), dim3((unsigned)grid), dim3(256), 0, s, (const T*)dy, (const T*)x,
-                           coef, (T*)dx, (int)nvec, (int)C, (int)S, nhwc));
+                           coef, (const T*)ym, (T*)dz, (T*)dx, (int)nvec, (int)C, (int)S, nhwc));
     return (int)hipGetLastError();
   }
   const int64_t grid = min((total + 255) / 256, (int64_t)8192);
   NM_DISPATCH(dt, T, NM_DISPATCH(wdt, W,
       hipLaunchKernelGGL((bn_bwd_elemt_kernel<T, W>), dim3((unsigned)grid), dim3(256), 0, s, (const T*)dy,
-                         (const T*)x, mean, invstd, (const W*)w, sum_dy, sum_dy_xmu, count, (T*)dx, N, C,
-                         S, nhwc)));
+                         (const T*)x, mean, invstd, (const W*)w, sum_dy, sum_dy_xmu, count, (const T*)ym,
+                         (T*)dz, (T*)dx, N, C, S, nhwc)));
   return (int)hipGetLastError();
 }
 

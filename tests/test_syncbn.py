@@ -138,3 +138,73 @@ def test_syncbn_channels_last_memory_format_and_large_mean(dt):
     torch.testing.assert_close(y.float(), yr.float(), rtol=tol, atol=tol)
     torch.testing.assert_close(x.grad.float(), xr.grad.float(), rtol=2 * tol, atol=2 * tol)
     torch.testing.assert_close(m.running_var, ref.running_var.float(), rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("channels_last", [False, True])
+def test_syncbn_fused_residual_relu_cpu(channels_last):
+    """relu(BN(x) + z) through SyncBatchNorm(fuse_relu=True)(x, z): output and gradients of x, z,
+    weight, bias against the separate-op composition (CPU reference path)."""
+    from apex.parallel import SyncBatchNorm
+
+    torch.manual_seed(3)
+    x = torch.randn(4, 16, 5, 6, dtype=torch.float32)
+    z = torch.randn(4, 16, 5, 6, dtype=torch.float32)
+    if channels_last:
+        x, z = x.to(memory_format=torch.channels_last), z.to(memory_format=torch.channels_last)
+    bn = SyncBatchNorm(16, fuse_relu=True)
+    ref = torch.nn.BatchNorm2d(16)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+        ref.weight.copy_(bn.weight)
+        ref.bias.copy_(bn.bias)
+    x1, z1, x2, z2 = (t.clone().requires_grad_() for t in (x, z, x, z))
+    y = bn(x1, z1)
+    yr = torch.relu(ref(x2) + z2)
+    dy = torch.randn_like(yr)
+    y.backward(dy)
+    yr.backward(dy)
+    torch.testing.assert_close(y, yr, atol=1e-5, rtol=1e-4)  # the reference path computes in fp32
+    for a, b in ((x1.grad, x2.grad), (z1.grad, z2.grad), (bn.weight.grad, ref.weight.grad),
+                 (bn.bias.grad, ref.bias.grad)):
+        torch.testing.assert_close(a, b, atol=1e-5, rtol=1e-4)
+    torch.testing.assert_close(bn.running_mean, ref.running_mean)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("shape,mem", [((8, 64, 14, 14), "cl"), ((4, 32, 16, 8), "nchw"), ((6, 5, 7, 7), "nchw"),
+                                       ((4, 24, 9, 9), "cl")])
+@pytest.mark.parametrize("with_z", [True, False])
+def test_syncbn_fused_residual_relu_gpu(dt, shape, mem, with_z):
+    """relu(BN(x) + z) in the HIP kernels (vectorised NHWC / NCHW and the scalar fallback for odd
+    channel / plane counts): output and the x, z, weight, bias gradients vs the fp32 composition."""
+    from apex.parallel import SyncBatchNorm
+
+    torch.manual_seed(4)
+    C = shape[1]
+    fmt = torch.channels_last if mem == "cl" else torch.contiguous_format
+    x = (torch.randn(shape, device="cuda") * 2 + 0.3).to(dt).contiguous(memory_format=fmt).requires_grad_(True)
+    z = torch.randn(shape, device="cuda").to(dt).contiguous(memory_format=fmt).requires_grad_(True)
+    m = SyncBatchNorm(C, fuse_relu=True).cuda()
+    with torch.no_grad():
+        m.weight.uniform_(0.5, 1.5)
+        m.bias.uniform_(-0.5, 0.5)
+    y = m(x, z) if with_z else m(x)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr, zr = (t.detach().float().requires_grad_(True) for t in (x, z))
+    ref = nn.BatchNorm2d(C).cuda()
+    ref.load_state_dict({k: v for k, v in m.state_dict().items() if k != "num_batches_tracked"}, strict=False)
+    with torch.no_grad():
+        ref.running_mean.zero_()
+        ref.running_var.fill_(1)
+    yr = torch.relu(ref(xr) + zr) if with_z else torch.relu(ref(xr))
+    yr.backward(dy.float())
+    tol = 3e-2 if dt == torch.bfloat16 else 1e-4
+    torch.testing.assert_close(y.float(), yr, rtol=tol, atol=tol)
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=2 * tol, atol=2 * tol)
+    if with_z:
+        torch.testing.assert_close(z.grad.float(), zr.grad, rtol=tol, atol=tol)
+    torch.testing.assert_close(m.weight.grad.float(), ref.weight.grad, rtol=tol * 4, atol=tol * 20)
+    torch.testing.assert_close(m.bias.grad.float(), ref.bias.grad, rtol=tol * 4, atol=tol * 20)
