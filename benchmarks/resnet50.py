@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-syncbn", action="store_true")
     ap.add_argument("--no-fuse-bn", action="store_true", help="BN, residual add and ReLU as separate ops")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the training step as a HIP graph (one process per GPU, N = 1 path)")
     ap.add_argument("--nchw", action="store_true", help="keep NCHW activations")
     ap.add_argument("--fp32", action="store_true")
     ap.add_argument("--conv-search", action="store_true",
@@ -58,7 +60,8 @@ def main():
         model, opt = amp.initialize(model, opt, opt_level="O0", verbosity=0)
     else:
         model, opt = amp.initialize(model, opt, opt_level="O2", cast_model_type=torch.bfloat16, verbosity=0)
-    model = DDP(model, message_size=int(os.environ.get("APEX_DDP_MESSAGE_SIZE", 25_000_000)), comm_timing=True)
+    model = DDP(model, message_size=int(os.environ.get("APEX_DDP_MESSAGE_SIZE", 25_000_000)),
+                comm_timing=not args.graph)  # (timing events are not recorded inside a captured graph)
     g = torch.Generator(device=env.device).manual_seed(1 + env.rank)
     dt = torch.float32 if args.fp32 else torch.bfloat16
     batches = [synthetic_batch(args.batch, args.image_size, device=env.device, dtype=dt, channels_last=cl,
@@ -73,7 +76,40 @@ def main():
         opt.zero_grad()
         return loss
 
-    elapsed, loss, extra = instrumented_steps(env, step, args.steps, args.warmup, ddp=model)
+    run, graphed = step, False
+    if args.graph:
+        # the whole training step (forward, backward, loss scaling, FusedSGD) as one HIP graph per
+        # input buffer, replayed each step: at ~2000 dispatches per step the eager loop leaves the
+        # GPU idle ~13 % of the time between launches (profiles/r3_resnet50_step_kernels.txt).
+        # Captured after eager warmup steps (MIOpen algorithm selection, the DDP bucket layout and
+        # the optimizer state exist by then); any capture failure falls back to the eager step.
+        try:
+            for i in range(3):
+                step(i)
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                for i in range(2):
+                    step(i)
+            torch.cuda.current_stream().wait_stream(side)
+            torch.cuda.synchronize()
+            graphs, outs = [], []
+            for k in range(2):
+                gr = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gr):
+                    outs.append(step(k))
+                graphs.append(gr)
+
+            def run(i):
+                graphs[i % 2].replay()
+                return outs[i % 2]
+
+            graphed = True
+        except Exception as e:  # noqa: BLE001
+            print(f"graph capture failed, eager steps: {e!r}"[:300], file=sys.stderr)
+            torch.cuda.synchronize()
+    elapsed, loss, extra = instrumented_steps(env, run, args.steps, args.warmup, ddp=model)
+    extra["hip_graph"] = graphed
     emit(env, metric="img/s ResNet-50 amp-O2 bf16 + FusedSGD + SyncBatchNorm", items_per_step=args.batch * env.world,
          unit="img/s", steps=args.steps, warmup=args.warmup, elapsed=elapsed,
          dtype="fp32" if args.fp32 else "bf16", data="synthetic normalised images; random-init weights",
