@@ -58,29 +58,42 @@ class SyncBatchnormFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, input, weight, bias, running_mean, running_var, eps, momentum, group, channel_last,
-                fuse_relu, z=None):
+                fuse_relu, z=None, num_batches_tracked=None):
         native = _ext.use_native(input)
         x = input.contiguous()  # channel_last: logical [N, ..., C] layout (apex convention)
         C = _ext.require() if native else None
-        local = C.bn_local_stats(x, channel_last) if native else _local_stats_ref(x, channel_last)
         world = _world(group)
-        if world > 1:
-            gathered = torch.empty((world * local.shape[0], 3), dtype=local.dtype, device=local.device)
-            dist.all_gather_into_tensor(gathered, local, group=group)
-            gathered = gathered.view(world, -1, 3)
+        # the combine kernel also writes invstd and updates fp32 running statistics in place (and,
+        # single-process, bumps num_batches_tracked): one launch instead of ~10 small torch ops
+        fused_running = native and (running_mean is None or (
+            running_mean.dtype == torch.float32 and running_var.dtype == torch.float32
+            and running_mean.is_contiguous() and running_var.is_contiguous()))
+        rm, rv = (running_mean, running_var) if fused_running else (None, None)
+        if fused_running and world == 1:
+            mean, var, count, invstd = C.bn_stats(x, channel_last, eps, rm, rv, momentum, num_batches_tracked)
+            num_batches_tracked = None
         else:
-            gathered = local.unsqueeze(0)
-        if native:
-            mean, var, count = C.bn_combine(gathered)
-        else:
-            mean, var, count = _combine_ref(gathered)
-        if running_mean is not None:
+            local = C.bn_local_stats(x, channel_last) if native else _local_stats_ref(x, channel_last)
+            if world > 1:
+                gathered = torch.empty((world * local.shape[0], 3), dtype=local.dtype, device=local.device)
+                dist.all_gather_into_tensor(gathered, local, group=group)
+                gathered = gathered.view(world, -1, 3)
+            else:
+                gathered = local.unsqueeze(0)
+            if native:
+                mean, var, count, invstd = C.bn_combine(gathered, eps, rm, rv, momentum)
+            else:
+                mean, var, count = _combine_ref(gathered)
+                invstd = torch.rsqrt(var + eps)
+            if running_mean is not None and not fused_running:
+                with torch.no_grad():
+                    n = count[0] if count.numel() else torch.tensor(1.0)
+                    unbiased = var * n / (n - 1).clamp(min=1)
+                    running_mean.mul_(1 - momentum).add_(mean.to(running_mean.dtype), alpha=momentum)
+                    running_var.mul_(1 - momentum).add_(unbiased.to(running_var.dtype), alpha=momentum)
+        if num_batches_tracked is not None:
             with torch.no_grad():
-                n = count[0] if count.numel() else torch.tensor(1.0)
-                unbiased = var * n / (n - 1).clamp(min=1)
-                running_mean.mul_(1 - momentum).add_(mean.to(running_mean.dtype), alpha=momentum)
-                running_var.mul_(1 - momentum).add_(unbiased.to(running_var.dtype), alpha=momentum)
-        invstd = torch.rsqrt(var + eps)
+                num_batches_tracked.add_(1)
         has_z = z is not None
         if native:
             y = C.bn_elemt(x, mean, invstd, weight, bias, channel_last, fuse_relu,
@@ -140,7 +153,7 @@ class SyncBatchnormFunction(torch.autograd.Function):
                 dx = dx * weight.float().view(sh)
             dx = dx.to(x.dtype)
             dz = dy if has_z else None
-        return dx, dw, db, None, None, None, None, None, None, None, (dz if has_z else None)
+        return dx, dw, db, None, None, None, None, None, None, None, (dz if has_z else None), None
 
 
 class SyncBatchNorm(_BatchNorm):
@@ -179,8 +192,6 @@ class SyncBatchNorm(_BatchNorm):
                 return self.forward(input.permute(0, 2, 3, 1), zz).permute(0, 3, 1, 2)
             finally:
                 self.channel_last = False
-        if self.training and self.track_running_stats:
-            self.num_batches_tracked += 1
         use_batch_stats = self.training or not self.track_running_stats
         if not use_batch_stats:
             mean = self.running_mean.float()
@@ -198,12 +209,19 @@ class SyncBatchNorm(_BatchNorm):
                 y = y + z.float()
             y = torch.relu(y) if self.fuse_relu else y
             return y.to(input.dtype)
-        momentum = self.momentum if self.momentum is not None else 0.0
+        track = self.training and self.track_running_stats
+        if self.momentum is not None:
+            momentum = self.momentum
+        elif track:  # cumulative moving average (torch semantics); one host read, this mode only
+            momentum = 1.0 / float(self.num_batches_tracked + 1)
+        else:
+            momentum = 0.0
+        # num_batches_tracked is incremented by the function (inside the combine kernel when it can)
         return SyncBatchnormFunction.apply(input, self.weight, self.bias,
                                            self.running_mean if self.track_running_stats else None,
                                            self.running_var if self.track_running_stats else None,
                                            self.eps, momentum, self.process_group, self.channel_last,
-                                           self.fuse_relu, z)
+                                           self.fuse_relu, z, self.num_batches_tracked if track else None)
 
 
 def convert_syncbn_model(module, process_group=None, channel_last=False):

@@ -757,37 +757,82 @@ std::vector<int64_t> bn_dims(const Tensor& x, bool nhwc) {
   return {N, C, S};
 }
 
-// local per-channel (mean, m2, count) triples [C, 3]
-Tensor k_bn_local_stats(Tensor x, bool nhwc) {
+static Tensor bn_partials(const Tensor& x, bool nhwc, int* spo) {
   TORCH_CHECK(x.is_contiguous(), "syncbn: input must be contiguous in its layout");
   auto d = bn_dims(x, nhwc);
   const int sp = apex::bn_splits_for(d[0], d[1], d[2], nhwc, dt_code(x.scalar_type()));
-  auto fo = x.options().dtype(at::kFloat);
-  Tensor part = at::empty({d[1] * sp * 3}, fo);
-  int spo = 0;
+  Tensor part = at::empty({d[1] * sp * 3}, x.options().dtype(at::kFloat));
   check(apex::bn_stats(x.data_ptr(), part.data_ptr<float>(), d[0], d[1], d[2], nhwc, dt_code(x.scalar_type()),
-                       &spo, cur_stream()),
+                       spo, cur_stream()),
         "bn_stats");
-  Tensor out = at::empty({d[1], 3}, fo);
-  Tensor mean = at::empty({d[1]}, fo), var = at::empty({d[1]}, fo), cnt = at::empty({d[1]}, fo);
-  check(apex::bn_combine(part.data_ptr<float>(), spo, d[1], 0, mean.data_ptr<float>(), var.data_ptr<float>(),
-                         cnt.data_ptr<float>(), cur_stream()),
+  return part;
+}
+
+static void check_running(const c10::optional<Tensor>& rm, const c10::optional<Tensor>& rv, int64_t C) {
+  TORCH_CHECK(rv.has_value() && rv->defined() && rm->scalar_type() == at::kFloat && rv->scalar_type() == at::kFloat &&
+                  rm->is_contiguous() && rv->is_contiguous() && rm->numel() == C && rv->numel() == C,
+              "syncbn: fp32 contiguous [C] running statistics");
+}
+
+// local per-channel (mean, m2, count) triples [C, 3], written by the combine kernel itself
+Tensor k_bn_local_stats(Tensor x, bool nhwc) {
+  int spo = 0;
+  Tensor part = bn_partials(x, nhwc, &spo);
+  const int64_t C = bn_dims(x, nhwc)[1];
+  Tensor out = at::empty({C, 3}, x.options().dtype(at::kFloat));
+  check(apex::bn_combine(part.data_ptr<float>(), spo, C, 0, nullptr, nullptr, nullptr, cur_stream(), nullptr, 0.f,
+                         nullptr, nullptr, 0.f, out.data_ptr<float>()),
         "bn_combine");
-  // triple = (mean, m2 = var*count, count)
-  return at::stack({mean, var * cnt, cnt}, 1).contiguous();
+  return out;
+}
+
+// Single-process statistics in two launches: partial Welford reduce, then one combine that writes
+// mean / biased var / count / invstd, updates the fp32 running statistics (unbiased variance) and
+// bumps num_batches_tracked — the whole forward prologue of a BatchNorm layer.
+std::vector<Tensor> k_bn_stats(Tensor x, bool nhwc, double eps, const c10::optional<Tensor>& running_mean,
+                               const c10::optional<Tensor>& running_var, double momentum,
+                               const c10::optional<Tensor>& num_batches_tracked) {
+  int spo = 0;
+  Tensor part = bn_partials(x, nhwc, &spo);
+  const int64_t C = bn_dims(x, nhwc)[1];
+  auto fo = x.options().dtype(at::kFloat);
+  Tensor mean = at::empty({C}, fo), var = at::empty({C}, fo), cnt = at::empty({C}, fo), inv = at::empty({C}, fo);
+  const bool upd = running_mean.has_value() && running_mean->defined();
+  if (upd) check_running(running_mean, running_var, C);
+  int64_t* nt = nullptr;
+  if (num_batches_tracked.has_value() && num_batches_tracked->defined()) {
+    TORCH_CHECK(num_batches_tracked->scalar_type() == at::kLong && num_batches_tracked->numel() == 1 &&
+                    num_batches_tracked->device() == x.device(),
+                "syncbn: num_batches_tracked must be a one-element int64 tensor on the input's device");
+    nt = num_batches_tracked->data_ptr<int64_t>();
+  }
+  check(apex::bn_combine(part.data_ptr<float>(), spo, C, 0, mean.data_ptr<float>(), var.data_ptr<float>(),
+                         cnt.data_ptr<float>(), cur_stream(), inv.data_ptr<float>(), (float)eps,
+                         upd ? running_mean->data_ptr<float>() : nullptr,
+                         upd ? running_var->data_ptr<float>() : nullptr, (float)momentum, nullptr, nt),
+        "bn_combine");
+  return {mean, var, cnt, inv};
 }
 
 // gathered [G, C, 3] -> (mean, biased var, count)
-std::vector<Tensor> k_bn_combine(Tensor gathered) {
+// eps >= 0: also return invstd; running_mean / running_var (fp32, contiguous): updated in place with
+// `momentum` by the same kernel (one launch for the whole post-combine tail of a BatchNorm layer)
+std::vector<Tensor> k_bn_combine(Tensor gathered, double eps, const c10::optional<Tensor>& running_mean,
+                                 const c10::optional<Tensor>& running_var, double momentum) {
   Tensor g = gathered.contiguous();
   const int groups = (int)g.size(0);
   const int64_t C = g.size(1);
   auto fo = g.options().dtype(at::kFloat);
   Tensor mean = at::empty({C}, fo), var = at::empty({C}, fo), cnt = at::empty({C}, fo);
+  Tensor invstd = eps >= 0.0 ? at::empty({C}, fo) : Tensor();
+  const bool upd = running_mean.has_value() && running_mean->defined();
+  if (upd) check_running(running_mean, running_var, C);
   check(apex::bn_combine(g.data_ptr<float>(), groups, C, 1, mean.data_ptr<float>(), var.data_ptr<float>(),
-                         cnt.data_ptr<float>(), cur_stream()),
+                         cnt.data_ptr<float>(), cur_stream(), invstd.defined() ? invstd.data_ptr<float>() : nullptr,
+                         (float)std::max(eps, 0.0), upd ? running_mean->data_ptr<float>() : nullptr,
+                         upd ? running_var->data_ptr<float>() : nullptr, (float)momentum),
         "bn_combine");
-  return {mean, var, cnt};
+  return {mean, var, cnt, invstd};
 }
 
 // z: optional residual added after the affine, before the ReLU (same shape / layout as x)
@@ -1300,7 +1345,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gru_cell_fwd", &k_gru_fwd);
   m.def("gru_cell_bwd", &k_gru_bwd);
   m.def("bn_local_stats", &k_bn_local_stats);
-  m.def("bn_combine", &k_bn_combine);
+  m.def("bn_stats", &k_bn_stats, py::arg("x"), py::arg("nhwc"), py::arg("eps"), py::arg("running_mean") = py::none(),
+        py::arg("running_var") = py::none(), py::arg("momentum") = 0.0, py::arg("num_batches_tracked") = py::none());
+  m.def("bn_combine", &k_bn_combine, py::arg("gathered"), py::arg("eps") = -1.0, py::arg("running_mean") = py::none(),
+        py::arg("running_var") = py::none(), py::arg("momentum") = 0.0);
   m.def("bn_elemt", &k_bn_elemt, py::arg("x"), py::arg("mean"), py::arg("invstd"), py::arg("w"), py::arg("b"),
         py::arg("nhwc"), py::arg("relu"), py::arg("z") = py::none());
   m.def("bn_bwd_reduce", &k_bn_bwd_reduce, py::arg("dy"), py::arg("x"), py::arg("mean"), py::arg("nhwc"),

@@ -174,8 +174,11 @@ int gru_cell_bwd(const void* dhy, const void* hx, const float* ws, void* dig, vo
 int bn_splits_for(int64_t N, int64_t C, int64_t S, int nhwc, int dt);
 int bn_stats(const void* x, float* part, int64_t N, int64_t C, int64_t S, int nhwc, int dt, int* splits_out,
              hipStream_t s);
+// invstd (nullable): rsqrt(var + eps); rmean / rvar (nullable, fp32): running-statistics momentum update
 int bn_combine(const float* in, int groups, int64_t C, int gmajor, float* mean, float* var, float* count,
-               hipStream_t s);
+               hipStream_t s, float* invstd = nullptr, float eps = 0.f, float* rmean = nullptr,
+               float* rvar = nullptr, float momentum = 0.f, float* triple = nullptr,
+               int64_t* ntrack = nullptr);
 // Fused residual + ReLU (ResNet blocks): bn_elemt adds z (nullable, x's layout) after the affine
 // and before the ReLU; the backward kernels take the forward output ym (nullable) and pass the
 // gradient only where ym > 0; bn_bwd_elemt also writes that masked gradient to dz (z's gradient).

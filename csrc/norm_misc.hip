@@ -330,8 +330,40 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(const T* __restrict__ x, 
 
 // combine `groups` Welford triples per channel: in[(g*C + c)*3 ...] (g-major, e.g. all-gathered)
 // or in[(c*groups + g)*3] (c-major, local splits). Writes mean, biased var, count per channel.
+// The combine's tail for one channel: the global mean / biased variance / count, and optionally
+// invstd = rsqrt(var + eps) and the momentum update of the fp32 running statistics (unbiased
+// variance) — the 8-10 small torch launches per BatchNorm layer that otherwise follow the combine.
+struct BnFinish {
+  float* invstd;
+  float* rmean;
+  float* rvar;
+  float* triple;    // [C, 3] (mean, m2, count): the per-rank record all-gathered by SyncBatchNorm
+  int64_t* ntrack;  // num_batches_tracked += 1 (channel 0)
+  float eps, momentum;
+};
+__device__ __forceinline__ void bn_finish(const Welford& r, int64_t c, float* mean, float* var, float* count,
+                                          const BnFinish& f) {
+  const float v = r.n > 0.f ? r.m2 / r.n : 0.f;
+  if (mean) mean[c] = r.mean;
+  if (var) var[c] = v;
+  if (count) count[c] = r.n;
+  if (f.triple) {
+    f.triple[c * 3] = r.mean;
+    f.triple[c * 3 + 1] = r.m2;
+    f.triple[c * 3 + 2] = r.n;
+  }
+  if (f.ntrack && c == 0) f.ntrack[0] += 1;
+  if (f.invstd) f.invstd[c] = rsqrtf(v + f.eps);
+  if (f.rmean) {
+    const float m = f.momentum;
+    f.rmean[c] = (1.f - m) * f.rmean[c] + m * r.mean;
+    f.rvar[c] = (1.f - m) * f.rvar[c] + m * (v * r.n / fmaxf(r.n - 1.f, 1.f));
+  }
+}
+
 __global__ void bn_combine_kernel(const float* __restrict__ in, int groups, int64_t C, int gmajor,
-                                  float* __restrict__ mean, float* __restrict__ var, float* __restrict__ count) {
+                                  float* __restrict__ mean, float* __restrict__ var, float* __restrict__ count,
+                                  BnFinish fin) {
   const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (c >= C) return;
   Welford t{0.f, 0.f, 0.f};
@@ -339,9 +371,7 @@ __global__ void bn_combine_kernel(const float* __restrict__ in, int groups, int6
     const float* p = in + (gmajor ? ((int64_t)g * C + c) : (c * groups + g)) * 3;
     t = wf_merge(t, Welford{p[0], p[1], p[2]});
   }
-  mean[c] = t.mean;
-  var[c] = t.n > 0.f ? t.m2 / t.n : 0.f;
-  if (count) count[c] = t.n;
+  bn_finish(t, c, mean, var, count, fin);
 }
 
 template <typename T, typename W>
@@ -811,7 +841,7 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_par_kernel(const float* _
 // parallel combine of c-major local partials (groups >= 64): one block per channel
 __global__ void __launch_bounds__(256) bn_combine_par_kernel(const float* __restrict__ in, int groups,
                                                             float* __restrict__ mean, float* __restrict__ var,
-                                                            float* __restrict__ count) {
+                                                            float* __restrict__ count, BnFinish fin) {
   __shared__ float sm[3][4];
   const int64_t c = blockIdx.x;
   Welford t{0.f, 0.f, 0.f};
@@ -834,9 +864,7 @@ __global__ void __launch_bounds__(256) bn_combine_par_kernel(const float* __rest
   if (threadIdx.x == 0) {
     Welford r{sm[0][0], sm[1][0], sm[2][0]};
     for (int k = 1; k < 4; ++k) r = wf_merge(r, Welford{sm[0][k], sm[1][k], sm[2][k]});
-    mean[c] = r.mean;
-    var[c] = r.n > 0.f ? r.m2 / r.n : 0.f;
-    if (count) count[c] = r.n;
+    bn_finish(r, c, mean, var, count, fin);
   }
 }
 
@@ -908,13 +936,15 @@ int bn_stats(const void* x, float* part, int64_t N, int64_t C, int64_t S, int nh
 }
 
 int bn_combine(const float* in, int groups, int64_t C, int gmajor, float* mean, float* var, float* count,
-               hipStream_t s) {
+               hipStream_t s, float* invstd, float eps, float* rmean, float* rvar, float momentum,
+               float* triple, int64_t* ntrack) {
   if (C == 0) return 0;
+  const BnFinish fin{invstd, rmean, rvar, triple, ntrack, eps, momentum};
   if (!gmajor && groups >= 64) {
-    hipLaunchKernelGGL(bn_combine_par_kernel, dim3((unsigned)C), dim3(256), 0, s, in, groups, mean, var, count);
+    hipLaunchKernelGGL(bn_combine_par_kernel, dim3((unsigned)C), dim3(256), 0, s, in, groups, mean, var, count, fin);
   } else {
     hipLaunchKernelGGL(bn_combine_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, in, groups, C,
-                       gmajor, mean, var, count);
+                       gmajor, mean, var, count, fin);
   }
   return (int)hipGetLastError();
 }

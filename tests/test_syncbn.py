@@ -208,3 +208,42 @@ def test_syncbn_fused_residual_relu_gpu(dt, shape, mem, with_z):
         torch.testing.assert_close(z.grad.float(), zr.grad, rtol=tol, atol=tol)
     torch.testing.assert_close(m.weight.grad.float(), ref.weight.grad, rtol=tol * 4, atol=tol * 20)
     torch.testing.assert_close(m.bias.grad.float(), ref.bias.grad, rtol=tol * 4, atol=tol * 20)
+
+
+def _running_stats_case(device, dt, momentum, channel_last_mem):
+    from apex.parallel import SyncBatchNorm
+
+    torch.manual_seed(5)
+    C = 24
+    m = SyncBatchNorm(C, momentum=momentum).to(device)
+    ref = nn.BatchNorm2d(C, momentum=momentum).to(device)
+    fmt = torch.channels_last if channel_last_mem else torch.contiguous_format
+    for step in range(3):
+        x = (torch.randn(6, C, 5, 7, device=device) * (step + 1) + step).to(dt).contiguous(memory_format=fmt)
+        m(x)
+        ref(x.float())
+    assert int(m.num_batches_tracked) == 3
+    torch.testing.assert_close(m.running_mean, ref.running_mean, rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(m.running_var, ref.running_var, rtol=1e-3, atol=1e-3)
+    m.eval()
+    ref.eval()
+    x = torch.randn(2, C, 5, 7, device=device).to(dt)
+    tol = 3e-2 if dt == torch.bfloat16 else 1e-4
+    torch.testing.assert_close(m(x).float(), ref(x.float()), rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("momentum", [0.1, None])
+def test_syncbn_running_stats_cpu(momentum):
+    """Running mean / unbiased running variance / num_batches_tracked over several steps vs
+    torch BatchNorm, incl. momentum=None (cumulative average)."""
+    _running_stats_case("cpu", torch.float32, momentum, False)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("momentum", [0.1, None])
+@pytest.mark.parametrize("cl", [False, True])
+def test_syncbn_running_stats_gpu(dt, momentum, cl):
+    """The fused combine kernel (invstd + in-place fp32 running-statistics update +
+    num_batches_tracked in the same launch) against torch BatchNorm over several steps."""
+    _running_stats_case("cuda", dt, momentum, cl)
