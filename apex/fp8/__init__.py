@@ -21,6 +21,14 @@ Scaling
     small RCCL call per step). A tensor's first quantisation uses current scaling.
   Nothing here synchronises with the host.
 
+Producer-side quantisation
+  The post-LN blocks (apex.ops.blocks) have their bias+dropout+residual+LayerNorm kernels write
+  the fp8 codes of their output next to the bf16 value: the LN output (e4m3, the next sublayer's
+  GEMM operand; slot keyed by the LN's gamma, role "y") and, in backward, dt (e5m2 under the
+  consuming GEMM's own "dy" slot). ``produce()`` hands the kernel its scale / amax and an output
+  buffer; ``register()`` files the codes under the bf16 tensor; the consuming ``forward_gemm`` /
+  ``backward_gemm`` takes them instead of running a standalone quantise pass over that tensor.
+
 Use
   amp:       ``amp.initialize(model, opt, opt_level="O2", fp8=True)`` (or an ``Fp8Recipe``) — the
              patched ``optimizer.step()`` calls ``apex.fp8.step()``;
@@ -95,6 +103,8 @@ class Fp8State:
         self._wcache: dict = {}
         self._fwd = self.recipe.fmt("fwd")
         self._bwd = self.recipe.fmt("bwd")
+        self._pre: dict = {}  # (data_ptr, numel) -> (tensor, version, codes, slot): producer-made codes
+        self.prequant_hits = 0
         self._grow(128)
 
     # ------------------------------------------------------------------ slots
@@ -131,7 +141,7 @@ class Fp8State:
         st = ref()
         if st is None:
             return
-        for role in ("w", "x", "dy"):
+        for role in ("w", "x", "dy", "y"):
             s = st.slots.pop((key, role), None)
             if s is not None:
                 st._fresh.discard(s)
@@ -208,6 +218,48 @@ class Fp8State:
             e[4] = _C().fp8_quantize_t(w.detach().contiguous(), self._fwd, self._view("scale", e[2]))
         return e[4], self._view("scale_inv", e[2])
 
+    # ------------------------------------------------------------------ producer-side codes
+    _PRE_MAX = 64  # pending entries kept at most (an unconsumed output is dropped oldest first)
+
+    def produce(self, key, fmt, like):
+        """Arguments for a producer kernel that writes fp8 codes of its own output ``like``:
+        ``(codes_out, scale, amax, fmt, slot)`` — or None on the slot's first use, when there is
+        no amax history to scale with yet (the caller then runs without the side output and
+        ``quantize_output`` measures the tensor with current scaling)."""
+        if not (like.is_cuda and like.dtype in (torch.bfloat16, torch.float16)):
+            return None
+        s = self.slot(key, fmt)
+        if s in self._fresh:
+            return None
+        codes = torch.empty(like.shape, dtype=torch.uint8, device=like.device)
+        return codes, self._view("scale", s), self._view("amax", s), fmt, s
+
+    def register(self, t, codes, slot, fmt):
+        """File producer-made codes of ``t`` (format ``fmt``, scaled by ``slot``) for the GEMM that
+        consumes ``t`` next."""
+        if len(self._pre) >= self._PRE_MAX:
+            self._pre.pop(next(iter(self._pre)))
+        self._pre[(t.data_ptr(), t.numel())] = (t, t._version, codes, slot, fmt)
+
+    def quantize_output(self, t, key, fmt):
+        """First use of a producer slot: standalone current-scaled quantisation of ``t`` (records
+        the amax the slot's later fused passes scale with), filed like a producer's codes."""
+        if not (t.is_cuda and t.dtype in (torch.bfloat16, torch.float16) and t.is_contiguous()):
+            return
+        s = self.slot(key, fmt)
+        codes, _ = self.quantize(t, key, fmt)
+        self.register(t, codes, s, fmt)
+
+    def _take(self, a, fmt):
+        e = self._pre.pop((a.data_ptr(), a.numel()), None)
+        if e is None:
+            return None
+        t, ver, codes, s, cfmt = e
+        if a._version != ver or a.dtype != t.dtype or not a.is_contiguous() or cfmt != fmt:
+            return None
+        self.prequant_hits += 1
+        return codes.view(a.shape), self._view("scale_inv", s)
+
     # ------------------------------------------------------------------ GEMMs
     @staticmethod
     def _fits(a, w, bias, aux, contraction, width):
@@ -225,7 +277,8 @@ class Fp8State:
         """a [M, K] @ w[N, K]^T with epilogue ``epi`` on the fp8 kernel -> (out, extra) or None."""
         if not self._fits(a, w, bias, aux, w.shape[1], w.shape[0]):
             return None
-        a8, ia = self.quantize(a, (self.key_of(w), "x"), self._fwd)
+        pre = self._take(a, self._fwd) if self._pre else None
+        a8, ia = pre if pre is not None else self.quantize(a, (self.key_of(w), "x"), self._fwd)
         w8, iw = self.weight(w)
         return _C().gemm_f8(a8, w8, ia, iw, self._fwd, epi, bias, aux, None, a.dtype)
 
@@ -233,7 +286,8 @@ class Fp8State:
         """dy [M, N] @ w[N, K] with epilogue ``epi`` (dy e5m2 x W^T e4m3) -> (out, extra) or None."""
         if not self._fits(dy, w, None, aux, w.shape[0], w.shape[1]):
             return None
-        d8, id_ = self.quantize(dy, (self.key_of(w), "dy"), self._bwd)
+        pre = self._take(dy, self._bwd) if self._pre else None
+        d8, id_ = pre if pre is not None else self.quantize(dy, (self.key_of(w), "dy"), self._bwd)
         wt8, iw = self.weight_t(w)
         return _C().gemm_f8(d8, wt8, id_, iw, self._bwd, epi, None, aux, bias_grad_dtype, dy.dtype)
 
@@ -245,6 +299,7 @@ class Fp8State:
         self.gen += 1
         self.steps += 1
         self._wcache.clear()
+        self._pre.clear()
         if self.n == 0:
             return
         r = self.recipe

@@ -46,6 +46,33 @@ _LN_MEM = os.environ.get("APEX_LN_MEM", "1") != "0"
 def _ln_mem(C, cols):
     return _LN_MEM and C.bdaln_supported(cols)
 
+
+# fp8 codes written by the bias+dropout+residual+LayerNorm kernels themselves (apex.fp8 "producer-side
+# quantisation"): the LN output for the next sublayer's GEMM (e4m3), dt for this sublayer's
+# output-gradient GEMM (e5m2) — instead of standalone quantise passes re-reading them from HBM.
+# APEX_FP8_PRODUCER=0 turns it off (A/B).
+_FP8_PRODUCER = os.environ.get("APEX_FP8_PRODUCER", "1") != "0"
+
+
+def _q8(f8, key, fmt, like):
+    """(codes, scale, amax, fmt, slot) for a producer kernel, or None (no fp8 / first use)."""
+    if f8 is None or not _FP8_PRODUCER:
+        return None
+    return f8.produce(key, fmt, like)
+
+
+def _q8_kw(q8):
+    return {} if q8 is None else dict(q8_out=q8[0], q8_scale=q8[1], q8_amax=q8[2], q8_fmt=q8[3])
+
+
+def _q8_file(f8, t, q8, key, fmt):
+    if f8 is None or not _FP8_PRODUCER:
+        return
+    if q8 is not None:
+        f8.register(t, q8[0], q8[4], q8[3])
+    else:
+        f8.quantize_output(t, key, fmt)  # first use: measure with current scaling
+
 class _AttnSublayer(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, wqkv, bqkv, wo, bo, gamma, beta, heads, p_attn, p_hidden, eps, causal, k_lens):
@@ -63,8 +90,12 @@ class _AttnSublayer(torch.autograd.Function):
         t = G.linear(o2, wo, f8=f8)
         sh, oh = _seed(x.device) if p_hidden > 0 else (0, 0)
         mem = _ln_mem(C, E)
+        ykey = (f8.key_of(gamma), "y") if f8 is not None else None
+        q8 = _q8(f8, ykey, f8._fwd, t) if f8 is not None else None
         y, s, mean, rstd = C.bdaln_fwd(t, bo, x2.contiguous(), gamma, beta, float(eps), float(p_hidden), sh, oh,
-                                       store_s=not mem)
+                                       store_s=not mem, **_q8_kw(q8))
+        if f8 is not None:
+            _q8_file(f8, y, q8, ykey, f8._fwd)
         ctx.save_for_backward(x2, wqkv, qkv, o, lse, k_lens, dmask, wo, y if mem else s, gamma, mean, rstd)
         ctx.ln_beta = beta if mem else None
         ctx.f8 = f8
@@ -79,10 +110,15 @@ class _AttnSublayer(torch.autograd.Function):
         x2, wqkv, qkv, o, lse, k_lens, dmask, wo, s, gamma, mean, rstd = ctx.saved_tensors
         B, S, E, heads, d, scale, causal, p_attn, sa, oa, p_hidden, sh, oh, has_bqkv, has_bo, bdt = ctx.cfg
         pqkv, pbqkv, pwo, pbo, pg, pb = ctx.params
+        f8 = ctx.f8
+        dkey = (f8.key_of(wo), "dy") if f8 is not None else None
+        q8 = _q8(f8, dkey, f8._bwd, s) if f8 is not None else None
         dres, dt, dgamma, dbeta, dbo = C.bdaln_bwd(_2d(dy), s, gamma, mean, rstd, float(p_hidden), sh, oh, has_bo,
                                                    dgamma_out=_gt(pg), dbeta_out=_gt(pb),
-                                                   dbias_out=_gt(pbo) if has_bo else None, beta=ctx.ln_beta)
-        f8 = ctx.f8
+                                                   dbias_out=_gt(pbo) if has_bo else None, beta=ctx.ln_beta,
+                                                   **_q8_kw(q8))
+        if q8 is not None:
+            f8.register(dt, q8[0], q8[4], q8[3])
         dctx = G.dgrad(dt, wo, f8=f8).view(B, S, heads, d)
         dwo = _wgrad(dt, o.view(B * S, E), param=pwo)
         q, k, v = qkv.view(B, S, 3, heads, d).unbind(2)
@@ -118,8 +154,12 @@ class _FFNSublayer(torch.autograd.Function):
         t = G.linear(g, w2, f8=f8)
         seed, off = _seed(x.device) if p > 0 else (0, 0)
         mem = _ln_mem(C, x2.shape[1])
+        ykey = (f8.key_of(gamma), "y") if f8 is not None else None
+        q8 = _q8(f8, ykey, f8._fwd, t) if f8 is not None else None
         y, s, mean, rstd = C.bdaln_fwd(t, b2, x2.contiguous(), gamma, beta, float(eps), float(p), seed, off,
-                                       store_s=not mem)
+                                       store_s=not mem, **_q8_kw(q8))
+        if f8 is not None:
+            _q8_file(f8, y, q8, ykey, f8._fwd)
         ctx.save_for_backward(x2, w1, hb, h, g, w2, y if mem else s, gamma, mean, rstd)
         ctx.ln_beta = beta if mem else None
         ctx.cfg = (p, seed, off, act, b2 is not None, b1.dtype if b1 is not None else None)
@@ -133,9 +173,14 @@ class _FFNSublayer(torch.autograd.Function):
         p, seed, off, act, has_b2, b1dt = ctx.cfg
         f8 = ctx.f8
         pw1, pb1, pw2, pb2, pg, pb = ctx.params
+        dkey = (f8.key_of(w2), "dy") if f8 is not None else None
+        q8 = _q8(f8, dkey, f8._bwd, s) if f8 is not None else None
         dres, dt, dgamma, dbeta, db2 = C.bdaln_bwd(_2d(dy), s, gamma, mean, rstd, float(p), seed, off, has_b2,
                                                    dgamma_out=_gt(pg), dbeta_out=_gt(pb),
-                                                   dbias_out=_gt(pb2) if has_b2 else None, beta=ctx.ln_beta)
+                                                   dbias_out=_gt(pb2) if has_b2 else None, beta=ctx.ln_beta,
+                                                   **_q8_kw(q8))
+        if q8 is not None:
+            f8.register(dt, q8[0], q8[4], q8[3])
         if hb is None and act == ACT_GELU and b1dt is not None:
             tb1 = _gt(pb1)
             if _STORE_DERIV:

@@ -534,12 +534,34 @@ Tensor k_splitk_reduce(Tensor slabs, at::ScalarType out_dtype, const c10::option
 }
 
 bool k_bdaln_supported(int64_t cols) { return apex::bdaln_supported((int)cols) != 0; }
+
+// fp8 side output of a producer: codes uint8 like `like`, fp32 one-element scale / amax (device)
+static apex::Q8Out q8_args(const c10::optional<Tensor>& out, const c10::optional<Tensor>& scale,
+                           const c10::optional<Tensor>& amax, int64_t fmt, const Tensor& like, const char* what) {
+  apex::Q8Out q;
+  if (!out.has_value() || !out->defined()) return q;
+  TORCH_CHECK(out->scalar_type() == at::kByte && out->is_contiguous() && out->numel() == like.numel() &&
+                  out->device() == like.device(),
+              what, ": q8_out must be a contiguous uint8 tensor like the output");
+  TORCH_CHECK(scale.has_value() && amax.has_value() && scale->scalar_type() == at::kFloat &&
+                  amax->scalar_type() == at::kFloat && scale->numel() >= 1 && amax->numel() >= 1 &&
+                  scale->device() == like.device() && amax->device() == like.device(),
+              what, ": q8_scale / q8_amax fp32 device tensors");
+  TORCH_CHECK(fmt == 0 || fmt == 1, what, ": q8_fmt 0 (e4m3) or 1 (e5m2)");
+  q.y = out->data_ptr<uint8_t>();
+  q.scale = scale->data_ptr<float>();
+  q.amax = amax->data_ptr<float>();
+  q.fmt = (int)fmt;
+  return q;
+}
 bool k_bdaln_wide_supported(int64_t cols) { return apex::bdaln_wide_supported((int)cols) != 0; }
 
 // store_s = false (post-LN memory-efficient mode): the LN input s is not written (an empty tensor is
 // returned); the backward rebuilds x-hat from y (k_bdaln_bwd with beta)
 std::vector<Tensor> k_bdaln_fwd(Tensor x, const c10::optional<Tensor>& b, Tensor res, Tensor gamma,
-                                Tensor beta, double eps, double p, int64_t seed, int64_t offset, bool store_s) {
+                                Tensor beta, double eps, double p, int64_t seed, int64_t offset, bool store_s,
+                                const c10::optional<Tensor>& q8_out, const c10::optional<Tensor>& q8_scale,
+                                const c10::optional<Tensor>& q8_amax, int64_t q8_fmt) {
   TORCH_CHECK(x.is_contiguous() && res.is_contiguous() && x.sizes() == res.sizes(), "bdaln: shapes");
   const int64_t cols = cols_of(x), rows = x.numel() / std::max<int64_t>(cols, 1);
   Tensor y = at::empty_like(x), s = store_s ? at::empty_like(x) : at::empty({0}, x.options());
@@ -549,7 +571,8 @@ std::vector<Tensor> k_bdaln_fwd(Tensor x, const c10::optional<Tensor>& b, Tensor
   check(apex::bdaln_fwd(x.data_ptr(), opt_vptr(b), res.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
                         y.data_ptr(), store_s ? s.data_ptr() : nullptr, mean.data_ptr<float>(), rstd.data_ptr<float>(), rows,
                         (int)cols, (float)eps, (uint64_t)seed, (uint64_t)offset, dp.first, dp.second,
-                        dt_code(x.scalar_type()), dt_code(gamma.scalar_type()), cur_stream()),
+                        dt_code(x.scalar_type()), dt_code(gamma.scalar_type()), cur_stream(),
+                        q8_args(q8_out, q8_scale, q8_amax, q8_fmt, y, "bdaln_fwd")),
         "bdaln_fwd");
   return {y, s, mean, rstd};
 }
@@ -557,7 +580,9 @@ std::vector<Tensor> k_bdaln_fwd(Tensor x, const c10::optional<Tensor>& b, Tensor
 std::vector<Tensor> k_bdaln_bwd(Tensor dy, Tensor s, Tensor gamma, Tensor mean, Tensor rstd, double p,
                                 int64_t seed, int64_t offset, bool has_bias, const c10::optional<Tensor>& dgamma_out,
                                 const c10::optional<Tensor>& dbeta_out, const c10::optional<Tensor>& dbias_out,
-                                const c10::optional<Tensor>& ds_extra, const c10::optional<Tensor>& beta) {
+                                const c10::optional<Tensor>& ds_extra, const c10::optional<Tensor>& beta,
+                                const c10::optional<Tensor>& q8_out, const c10::optional<Tensor>& q8_scale,
+                                const c10::optional<Tensor>& q8_amax, int64_t q8_fmt) {
   // beta given: `s` is the LN output y of a store_s = false forward (x-hat = (y - beta) / gamma)
   Tensor dyc = dy.contiguous();
   const bool from_y = beta.has_value() && beta->defined();
@@ -583,7 +608,8 @@ std::vector<Tensor> k_bdaln_bwd(Tensor dy, Tensor s, Tensor gamma, Tensor mean, 
                         dx.data_ptr(), dgamma.data_ptr(),
                         dbeta.data_ptr(), has_bias ? dbias.data_ptr() : nullptr, ws.data_ptr<float>(), rows,
                         (int)cols, (uint64_t)seed, (uint64_t)offset, dp.first, dp.second,
-                        dt_code(s.scalar_type()), dt_code(gamma.scalar_type()), cur_stream()),
+                        dt_code(s.scalar_type()), dt_code(gamma.scalar_type()), cur_stream(),
+                        q8_args(q8_out, q8_scale, q8_amax, q8_fmt, dx, "bdaln_bwd")),
         "bdaln_bwd");
   return {dres, dx, dgamma, dbeta, dbias};
 }
@@ -1370,7 +1396,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bdaln_supported", &k_bdaln_supported);
   m.def("bdaln_wide_supported", &k_bdaln_wide_supported);
   m.def("bdaln_fwd", &k_bdaln_fwd, py::arg("x"), py::arg("b"), py::arg("res"), py::arg("gamma"), py::arg("beta"),
-        py::arg("eps"), py::arg("p"), py::arg("seed"), py::arg("offset"), py::arg("store_s") = true);
+        py::arg("eps"), py::arg("p"), py::arg("seed"), py::arg("offset"), py::arg("store_s") = true, py::arg("q8_out") = py::none(), py::arg("q8_scale") = py::none(),
+        py::arg("q8_amax") = py::none(), py::arg("q8_fmt") = 0);
   m.def("embed_ln_fwd", &k_embed_ln_fwd);
   m.def("embed_ln_bwd", &k_embed_ln_bwd, py::arg("dy"), py::arg("s"), py::arg("gamma"), py::arg("mean"),
         py::arg("rstd"), py::arg("tids"), py::arg("tvocab"), py::arg("npos"), py::arg("p"), py::arg("seed"),
@@ -1381,7 +1408,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bdaln_bwd", &k_bdaln_bwd, py::arg("dy"), py::arg("s"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"),
         py::arg("p"), py::arg("seed"), py::arg("offset"), py::arg("has_bias"), py::arg("dgamma_out") = py::none(),
         py::arg("dbeta_out") = py::none(), py::arg("dbias_out") = py::none(), py::arg("ds_extra") = py::none(),
-        py::arg("beta") = py::none());
+        py::arg("beta") = py::none(), py::arg("q8_out") = py::none(), py::arg("q8_scale") = py::none(),
+        py::arg("q8_amax") = py::none(), py::arg("q8_fmt") = 0);
   m.def("input_normalize", &k_input_normalize);
   m.def("gemm_supported", &k_gemm_supported);
   m.def("gemm", &k_gemm, py::arg("a"), py::arg("b"), py::arg("epi") = 0, py::arg("bias") = py::none(),

@@ -13,57 +13,19 @@
 // is clamped to the format's finite range first (e4m3fn has no infinity).
 #include "common.h"
 #include "kernels.h"
+#include "fp8_pack.h"
 
 namespace apex {
 
 namespace {
 
-constexpr float kE4M3Max = 448.f;
-constexpr float kE5M2Max = 57344.f;
-
-// non-negative floats order like their bit patterns: max via integer atomics
-__device__ __forceinline__ void atomic_max_pos(float* p, float v) {
-  atomicMax(reinterpret_cast<unsigned int*>(p), __float_as_uint(v));
-}
-
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
-}
-
-// block max -> ONE atomic per 256-thread block (thousands of same-address atomics serialise in
-// L2: one per wave made the quantiser atomic-bound at ~0.19 ms regardless of size). The plain
-// pre-read is only a filter: amax only grows, so a stale value costs an extra atomic, never a
-// missed one.
-__device__ __forceinline__ void block_amax(float mx, float* amax) {
-  __shared__ float red[4];
-  mx = wave_max(mx);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const float m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-    if (m > 0.f && m > *(volatile float*)amax) atomic_max_pos(amax, m);
-  }
-}
-
 template <int FMT>
 __device__ __forceinline__ uint32_t pack4(float a, float b, float c, float d) {
-  const float m = FMT == 0 ? kE4M3Max : kE5M2Max;
-  a = fminf(fmaxf(a, -m), m);
-  b = fminf(fmaxf(b, -m), m);
-  c = fminf(fmaxf(c, -m), m);
-  d = fminf(fmaxf(d, -m), m);
-  int w = 0;
-  if constexpr (FMT == 0) {
-    w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, w, false);
-    w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
-  } else {
-    w = __builtin_amdgcn_cvt_pk_bf8_f32(a, b, w, false);
-    w = __builtin_amdgcn_cvt_pk_bf8_f32(c, d, w, true);
-  }
-  return (uint32_t)w;
+  return f8_pack4<FMT>(a, b, c, d);
 }
+
+__device__ __forceinline__ float wave_max(float v) { return f8_wave_max(v); }
+__device__ __forceinline__ void block_amax(float mx, float* amax) { f8_block_amax(mx, amax); }
 
 // Scale source of one quantisation. Delayed: s = scale[0] (from the history), the input's amax
 // is folded into amax[0] for the next update. Current (cur != null, amax already measured by

@@ -11,6 +11,7 @@
 // row block, written as fp32 partial rows and reduced by colsum_reduce (deterministic).
 #include "common.h"
 #include "kernels.h"
+#include "fp8_pack.h"
 
 #include <type_traits>
 
@@ -197,10 +198,13 @@ __global__ void __launch_bounds__(kEwBlock) bdaln_fwd_kernel(const T* __restrict
                                                             T* __restrict__ s_out, float* __restrict__ mean,
                                                             float* __restrict__ rstd, int64_t rows, int cols,
                                                             float eps, uint64_t seed, uint64_t offset,
-                                                            uint32_t thresh, float scale) {
+                                                            uint32_t thresh, float scale, Q8Out q8) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
+  if (row >= rows) {
+    if (q8.y) f8_block_amax(0.f, q8.amax);  // the block reduction needs every wave
+    return;
+  }
   const int nvec = cols >> 3;
   float v[VPT][8];
   float sum = 0.f;
@@ -257,6 +261,8 @@ __global__ void __launch_bounds__(kEwBlock) bdaln_fwd_kernel(const T* __restrict
     mean[row] = mu;
     rstd[row] = rs;
   }
+  float qs = 0.f, mx = 0.f;
+  if (q8.y) qs = q8.scale[0];
 #pragma unroll
   for (int j = 0; j < VPT; ++j) {
     const int vi = j * 64 + lane;
@@ -267,8 +273,19 @@ __global__ void __launch_bounds__(kEwBlock) bdaln_fwd_kernel(const T* __restrict
 #pragma unroll
       for (int k = 0; k < 8; ++k) o[k] = (v[j][k] - mu) * rs * gv[k] + bb[k];
       store_f<T, 8>(y + row * cols + vi * 8, o);
+      if (q8.y) {
+        // fp8 codes of the output as stored (rounded to T first): the next GEMM's operand without
+        // a standalone quantise pass re-reading y from HBM
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          o[k] = to_f(from_f<T>(o[k]));
+          mx = fmaxf(mx, fabsf(o[k]));
+        }
+        f8_store8(q8.y + row * cols + vi * 8, o, qs, q8.fmt);
+      }
     }
   }
+  if (q8.y) f8_block_amax(mx, q8.amax);
 }
 
 // part rows: [dgamma | dbeta | dbias] (3*cols floats) per block.
@@ -281,7 +298,9 @@ __global__ void __launch_bounds__(kEwBlock) bdaln_fwd_kernel(const T* __restrict
 // FROMY (post-LN, memory-efficient): `s` points at the LN OUTPUT y and x-hat = (y - beta) / gamma,
 // so the forward need not store s at all (one [rows, cols] write less per sublayer; y is saved
 // anyway as the next GEMM's input). dgamma accumulates dy * (y - beta) and is divided by gamma once.
-template <typename T, typename W, int VPT, bool DROP, bool EXTRA = false, bool FROMY = false>
+// Q8: also write fp8 codes of dx (template flag: the runtime branch cost the plain kernel its third
+// wave per SIMD, 168 -> 170 VGPRs)
+template <typename T, typename W, int VPT, bool DROP, bool EXTRA = false, bool FROMY = false, bool Q8 = false>
 __global__ void __launch_bounds__(kEwBlock) bdaln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ s,
                                                             const W* __restrict__ gamma,
                                                             const W* __restrict__ beta,
@@ -291,7 +310,8 @@ __global__ void __launch_bounds__(kEwBlock) bdaln_bwd_kernel(const T* __restrict
                                                             T* __restrict__ dres, T* __restrict__ dx,
                                                             float* __restrict__ part, int64_t rows, int cols,
                                                             int rows_per_wave, uint64_t seed,
-                                                            uint64_t offset, uint32_t thresh, float scale) {
+                                                            uint64_t offset, uint32_t thresh, float scale,
+                                                            Q8Out q8) {
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [4][3*cols]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int nvec = cols >> 3;
@@ -307,6 +327,8 @@ __global__ void __launch_bounds__(kEwBlock) bdaln_bwd_kernel(const T* __restrict
     if (j * 64 + lane < nvec) load_f<W, 8>(gamma + (j * 64 + lane) * 8, g[j]);
   }
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_wave * 4;
+  float qs = 0.f, mx = 0.f;
+  if constexpr (Q8) qs = q8.scale[0];
   typedef Pack<T, 8> P8;
   P8 ns[VPT], nd[VPT], ne[EXTRA ? VPT : 1];
   auto fetch = [&](int64_t row) {
@@ -397,9 +419,18 @@ __global__ void __launch_bounds__(kEwBlock) bdaln_bwd_kernel(const T* __restrict
           dbi[j][k] += ds[k];
         }
         store_f<T, 8>(dx + e, ds);
+        if constexpr (Q8) {  // fp8 codes of dx as stored: the output-gradient GEMM's operand
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            ds[k] = to_f(from_f<T>(ds[k]));
+            mx = fmaxf(mx, fabsf(ds[k]));
+          }
+          f8_store8(q8.y + e, ds, qs, q8.fmt);
+        }
       }
     }
   }
+  if constexpr (Q8) f8_block_amax(mx, q8.amax);
   if constexpr (FROMY) __syncthreads();  // every wave is done with the staged beta / 1/gamma
   float* mine = lds + wid * 3 * cols;
 #pragma unroll
@@ -954,7 +985,7 @@ int bdaln_wide_supported(int cols) { return bdaln_wide_vpt(cols) > 0; }
 
 int bdaln_fwd(const void* x, const void* b, const void* res, const void* gamma, const void* beta, void* y,
               void* s_out, float* mean, float* rstd, int64_t rows, int cols, float eps, uint64_t seed,
-              uint64_t offset, uint32_t thresh, float scale, int xdt, int wdt, hipStream_t s) {
+              uint64_t offset, uint32_t thresh, float scale, int xdt, int wdt, hipStream_t s, Q8Out q8) {
   if (rows == 0) return 0;
   const int vpt = bdaln_vpt(cols);
   const dim3 grid((unsigned)((rows + 3) / 4));
@@ -964,11 +995,11 @@ int bdaln_fwd(const void* x, const void* b, const void* res, const void* gamma, 
       if (thresh)
         hipLaunchKernelGGL((bdaln_fwd_kernel<T, W, VPT, true>), grid, dim3(kEwBlock), 0, s, (const T*)x,
                            (const W*)b, (const T*)res, (const W*)gamma, (const W*)beta, (T*)y, (T*)s_out,
-                           mean, rstd, rows, cols, eps, seed, offset, thresh, scale);
+                           mean, rstd, rows, cols, eps, seed, offset, thresh, scale, q8);
       else
         hipLaunchKernelGGL((bdaln_fwd_kernel<T, W, VPT, false>), grid, dim3(kEwBlock), 0, s, (const T*)x,
                            (const W*)b, (const T*)res, (const W*)gamma, (const W*)beta, (T*)y, (T*)s_out,
-                           mean, rstd, rows, cols, eps, seed, offset, thresh, scale);
+                           mean, rstd, rows, cols, eps, seed, offset, thresh, scale, q8);
     })));
     return (int)hipGetLastError();
   }
@@ -976,11 +1007,11 @@ int bdaln_fwd(const void* x, const void* b, const void* res, const void* gamma, 
     if (thresh)
       hipLaunchKernelGGL((bdaln_fwd_kernel<T, W, VPT, true>), grid, dim3(kEwBlock), 0, s, (const T*)x,
                          (const W*)b, (const T*)res, (const W*)gamma, (const W*)beta, (T*)y, (T*)s_out,
-                         mean, rstd, rows, cols, eps, seed, offset, thresh, scale);
+                         mean, rstd, rows, cols, eps, seed, offset, thresh, scale, q8);
     else
       hipLaunchKernelGGL((bdaln_fwd_kernel<T, W, VPT, false>), grid, dim3(kEwBlock), 0, s, (const T*)x,
                          (const W*)b, (const T*)res, (const W*)gamma, (const W*)beta, (T*)y, (T*)s_out,
-                         mean, rstd, rows, cols, eps, seed, offset, thresh, scale);
+                         mean, rstd, rows, cols, eps, seed, offset, thresh, scale, q8);
   })));
   return (int)hipGetLastError();
 }
@@ -1001,12 +1032,13 @@ int64_t bdaln_ws_floats(int64_t rows, int cols) {
 int bdaln_bwd(const void* dy, const void* s_in, const void* gamma, const void* beta, const float* mean,
               const float* rstd, const void* dse, void* dres, void* dx, void* dgamma, void* dbeta, void* dbias,
               float* ws, int64_t rows, int cols, uint64_t seed, uint64_t offset, uint32_t thresh, float scale,
-              int xdt, int wdt, hipStream_t s) {
+              int xdt, int wdt, hipStream_t s, Q8Out q8) {
   if (rows == 0) return 0;
   const int vpt = bdaln_vpt(cols);
   const int rpw = bdaln_rpw(rows);
   const int parts = (int)((rows + 4 * rpw - 1) / (4 * rpw));
   if (beta && (!vpt || dse)) return -3;  // FROMY: post-LN (no ds_extra), narrow rows only
+  if (q8.y && (!vpt || dse)) return -3;  // fp8 side output: narrow rows, no ds_extra
   if (!vpt) {
     const int wv = bdaln_wide_vpt(cols);
     const size_t wlds = (size_t)4 * cols * sizeof(float);
@@ -1031,17 +1063,29 @@ int bdaln_bwd(const void* dy, const void* s_in, const void* gamma, const void* b
   const size_t lds = (size_t)4 * 3 * cols * sizeof(float);
   EW_DISPATCH(xdt, T, EW_DISPATCH(wdt, W, EW_VPT(vpt, VPT, {
     auto launch = [&](auto drop_tag, auto extra_tag) {
-      hipLaunchKernelGGL((bdaln_bwd_kernel<T, W, VPT, decltype(drop_tag)::value, decltype(extra_tag)::value>),
-                         dim3(parts), dim3(kEwBlock), lds, s, (const T*)dy, (const T*)s_in, (const W*)gamma,
-                         (const W*)nullptr, mean, rstd, (const T*)dse, (T*)dres, (T*)dx, ws, rows, cols, rpw, seed,
-                         offset, thresh, scale);
+      constexpr bool D = decltype(drop_tag)::value, E = decltype(extra_tag)::value;
+      if (q8.y && !E)
+        hipLaunchKernelGGL((bdaln_bwd_kernel<T, W, VPT, D, false, false, true>), dim3(parts), dim3(kEwBlock), lds, s,
+                           (const T*)dy, (const T*)s_in, (const W*)gamma, (const W*)nullptr, mean, rstd,
+                           (const T*)dse, (T*)dres, (T*)dx, ws, rows, cols, rpw, seed, offset, thresh, scale, q8);
+      else
+        hipLaunchKernelGGL((bdaln_bwd_kernel<T, W, VPT, D, E>), dim3(parts), dim3(kEwBlock), lds, s, (const T*)dy,
+                           (const T*)s_in, (const W*)gamma, (const W*)nullptr, mean, rstd, (const T*)dse, (T*)dres,
+                           (T*)dx, ws, rows, cols, rpw, seed, offset, thresh, scale, q8);
     };
     if (beta) {
       auto launch_y = [&](auto drop_tag) {
-        hipLaunchKernelGGL((bdaln_bwd_kernel<T, W, VPT, decltype(drop_tag)::value, false, true>), dim3(parts),
-                           dim3(kEwBlock), lds, s, (const T*)dy, (const T*)s_in, (const W*)gamma, (const W*)beta,
-                           mean, rstd, (const T*)nullptr, (T*)dres, (T*)dx, ws, rows, cols, rpw, seed, offset,
-                           thresh, scale);
+        constexpr bool D = decltype(drop_tag)::value;
+        if (q8.y)
+          hipLaunchKernelGGL((bdaln_bwd_kernel<T, W, VPT, D, false, true, true>), dim3(parts), dim3(kEwBlock), lds,
+                             s, (const T*)dy, (const T*)s_in, (const W*)gamma, (const W*)beta, mean, rstd,
+                             (const T*)nullptr, (T*)dres, (T*)dx, ws, rows, cols, rpw, seed, offset, thresh, scale,
+                             q8);
+        else
+          hipLaunchKernelGGL((bdaln_bwd_kernel<T, W, VPT, D, false, true>), dim3(parts), dim3(kEwBlock), lds, s,
+                             (const T*)dy, (const T*)s_in, (const W*)gamma, (const W*)beta, mean, rstd,
+                             (const T*)nullptr, (T*)dres, (T*)dx, ws, rows, cols, rpw, seed, offset, thresh, scale,
+                             q8);
       };
       if (thresh) launch_y(std::true_type{});
       else launch_y(std::false_type{});

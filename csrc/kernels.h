@@ -133,11 +133,20 @@ int colsum(const void* x, void* out, float* ws, int64_t rows, int cols, int xdt,
 int splitk_reduce(const float* slabs, void* out, int64_t n, int nsplit, int odt, hipStream_t s,
                   int accumulate = 0);
 int64_t colsum_parts(int64_t rows);
+// fp8 side output of a producer kernel (delayed scaling: codes = sat(v * scale[0]), max|v| folded
+// into amax[0] for the next scale update; fmt 0 = e4m3, 1 = e5m2). y == nullptr: none.
+struct Q8Out {
+  uint8_t* y = nullptr;
+  const float* scale = nullptr;
+  float* amax = nullptr;
+  int fmt = 0;
+};
 int bdaln_supported(int cols);
 int bdaln_wide_supported(int cols);  // 2056..4096 columns (bdaln fwd/bwd only, not the embedding block)
 int bdaln_fwd(const void* x, const void* b, const void* res, const void* gamma, const void* beta, void* y,
               void* s_out, float* mean, float* rstd, int64_t rows, int cols, float eps, uint64_t seed,
-              uint64_t offset, uint32_t thresh, float scale, int xdt, int wdt, hipStream_t s);
+              uint64_t offset, uint32_t thresh, float scale, int xdt, int wdt, hipStream_t s,
+              Q8Out q8 = Q8Out{});  // q8: fp8 codes of y (narrow rows only)
 // BERT embeddings: s = Ww[id] + Wp[row % S] + Wt[type]; y = dropout(LN(s)); backward -> ds, dWp, dWt
 // (type vocab <= 2), dgamma, dbeta; embed_segsum: word rows from the id-sorted token list
 int embed_ln_fwd(const int* ids, const int* tids, const void* Ww, const void* Wp, const void* Wt, const void* gamma,
@@ -156,7 +165,8 @@ int64_t bdaln_ws_floats(int64_t rows, int cols);
 int bdaln_bwd(const void* dy, const void* s_in, const void* gamma, const void* beta, const float* mean,
               const float* rstd, const void* dse, void* dres, void* dx, void* dgamma, void* dbeta, void* dbias,
               float* ws, int64_t rows, int cols, uint64_t seed, uint64_t offset, uint32_t thresh, float scale,
-              int xdt, int wdt, hipStream_t s);  // beta != nullptr: s_in is the LN output y (post-LN, narrow)
+              int xdt, int wdt, hipStream_t s,  // beta != nullptr: s_in is the LN output y (post-LN, narrow)
+              Q8Out q8 = Q8Out{});  // q8: fp8 codes of dx (narrow rows only)
 
 // ----------------------------- weight norm / RNN cells / SyncBN ------------
 int weight_norm_fwd(const void* v, const void* g, void* w, float* norms, int64_t R, int64_t C, int row_mode,

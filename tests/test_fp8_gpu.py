@@ -359,3 +359,94 @@ def test_state_dict_roundtrip(fp8_off):
     st.load_state_dict(sd, lin)
     s = st.slots[(st.key_of(lin.weight), "x")]
     assert float(st.scale[s]) == scale_x and s not in st._fresh
+
+
+# ------------------------------------------------------------------ producer-side quantisation
+@pytest.mark.parametrize("fmt", [0, 1])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_bdaln_q8_side_output_matches_standalone_quantize(fmt, p):
+    """The LayerNorm forward's fp8 side output (codes of y) and the backward's (codes of dx), for the
+    stored-input and the from-output backward: bit-identical to the standalone quantiser run on
+    the bf16 tensor with the same scale, and the same amax recorded."""
+    C = _C()
+    torch.manual_seed(11)
+    rows, cols = 1000, 1024
+    dt = torch.bfloat16
+    t = torch.randn(rows, cols, device=DEV, dtype=dt)
+    res = torch.randn(rows, cols, device=DEV, dtype=dt)
+    b = torch.randn(cols, device=DEV, dtype=dt) * 0.1
+    g = (torch.rand(cols, device=DEV) + 0.5).to(dt)
+    be = (torch.randn(cols, device=DEV) * 0.1).to(dt)
+    scale = torch.tensor([5.5], device=DEV)
+    amax = torch.zeros(1, device=DEV)
+    codes = torch.empty(rows, cols, device=DEV, dtype=torch.uint8)
+    y, s, mean, rstd = C.bdaln_fwd(t, b, res, g, be, 1e-12, p, 11, 3, q8_out=codes, q8_scale=scale, q8_amax=amax,
+                                   q8_fmt=fmt)
+    amax_ref = torch.zeros(1, device=DEV)
+    ref = C.fp8_quantize(y, fmt, scale, amax_ref)
+    assert torch.equal(codes, ref)
+    assert float(amax) == float(amax_ref) == float(y.float().abs().max())
+    dy = torch.randn(rows, cols, device=DEV, dtype=dt)
+    for from_y in (False, True):
+        dcodes = torch.empty_like(codes)
+        damax = torch.zeros(1, device=DEV)
+        sin = y if from_y else s
+        dres, dx, _, _, _ = C.bdaln_bwd(dy, sin, g, mean, rstd, p, 11, 3, True, beta=be if from_y else None,
+                                        q8_out=dcodes, q8_scale=scale, q8_amax=damax, q8_fmt=1 - fmt)
+        plain = C.bdaln_bwd(dy, sin, g, mean, rstd, p, 11, 3, True, beta=be if from_y else None)
+        assert torch.equal(dx, plain[1]) and torch.equal(dres, plain[0])  # the side output changes nothing
+        damax_ref = torch.zeros(1, device=DEV)
+        dref = C.fp8_quantize(dx, 1 - fmt, scale, damax_ref)
+        assert torch.equal(dcodes, dref), from_y
+        assert float(damax) == float(damax_ref)
+
+
+def test_blocks_fp8_producer_codes_match_standalone_path(fp8_off, monkeypatch):
+    """BERT sublayers under fp8 for three optimizer steps with the LN kernels writing the fp8 codes
+    (APEX_FP8_PRODUCER default) vs the standalone quantise passes: identical outputs and gradients
+    (same amax histories, same scales, same codes), and the producer codes are actually consumed."""
+    from apex.ops import blocks
+
+    fp8 = fp8_off
+    torch.manual_seed(0)
+    B, S, E, H, F = 4, 128, 256, 4, 1024
+    dt = torch.bfloat16
+    x = torch.randn(B, S, E, device=DEV, dtype=dt)
+    mk = lambda *s, sc=0.05: (torch.randn(*s, device=DEV) * sc).to(dt).requires_grad_(True)
+    params = [mk(3 * E, E), mk(3 * E), mk(E, E), mk(E), mk(F, E), mk(F), mk(E, F), mk(E)]
+    params += [(torch.rand(E, device=DEV) + 0.5).to(dt).requires_grad_(True), mk(E),
+               (torch.rand(E, device=DEV) + 0.5).to(dt).requires_grad_(True), mk(E)]
+    # a second attention layer with its own weights (shared weights would share "x" slots)
+    params += [mk(3 * E, E), mk(3 * E), mk(E, E), mk(E), (torch.rand(E, device=DEV) + 0.5).to(dt).requires_grad_(True),
+               mk(E)]
+
+    def run_steps(producer):
+        monkeypatch.setattr(blocks, "_FP8_PRODUCER", producer)
+        fp8.disable()
+        outs = []
+        for step in range(3):
+            with fp8.fp8_autocast():
+                wqkv, bqkv, wo, bo, w1, b1, w2, b2, g1, be1, g2, be2, wq2, bq2, wo2, bo2, g3, be3 = params
+                xi = x.clone().requires_grad_(True)
+                h = blocks.attention_sublayer(xi, wqkv, bqkv, wo, bo, g1, be1, H)
+                y = blocks.ffn_sublayer(h, w1, b1, w2, b2, g2, be2)
+                # the second layer's QKV consumes the FFN LN output's producer codes
+                y2 = blocks.attention_sublayer(y, wq2, bq2, wo2, bo2, g3, be3, H)
+                dy = torch.randn(y2.shape, device=DEV, generator=torch.Generator(device=DEV).manual_seed(step)).to(dt)
+                grads = torch.autograd.grad(y2, [xi] + params, dy)
+            outs.append((y2.detach(), grads))
+            fp8.step()
+        hits = fp8.state().prequant_hits
+        fp8.disable()
+        return outs, hits
+
+    ref, hits_off = run_steps(False)
+    got, hits_on = run_steps(True)
+    assert hits_off == 0
+    # per step: 2 LN outputs consumed in forward + 3 dt in backward; step 0's backward slots are
+    # fresh (standalone current scaling), its forward producer slots file standalone codes
+    assert hits_on == 2 + 2 * 5, hits_on
+    for (ya, ga), (yb, gb) in zip(got, ref):
+        torch.testing.assert_close(ya, yb, rtol=0, atol=0)
+        for a, b in zip(ga, gb):
+            torch.testing.assert_close(a, b, rtol=0, atol=0)
