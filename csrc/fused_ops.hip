@@ -299,9 +299,10 @@ __global__ void __launch_bounds__(kEwBlock) bdaln_fwd_kernel(const T* __restrict
 // so the forward need not store s at all (one [rows, cols] write less per sublayer; y is saved
 // anyway as the next GEMM's input). dgamma accumulates dy * (y - beta) and is divided by gamma once.
 // Q8: also write fp8 codes of dx (template flag: the runtime branch cost the plain kernel its third
-// wave per SIMD, 168 -> 170 VGPRs)
+// wave per SIMD, 168 -> 170 VGPRs; the Q8 variant is held to 3 waves per SIMD explicitly — at 2 it
+// ran 210 vs 145 us at the BERT shape)
 template <typename T, typename W, int VPT, bool DROP, bool EXTRA = false, bool FROMY = false, bool Q8 = false>
-__global__ void __launch_bounds__(kEwBlock) bdaln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ s,
+__global__ void __launch_bounds__(kEwBlock) __attribute__((amdgpu_waves_per_eu(Q8 ? 3 : 1))) bdaln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ s,
                                                             const W* __restrict__ gamma,
                                                             const W* __restrict__ beta,
                                                             const float* __restrict__ mean,
