@@ -221,7 +221,7 @@ class Fp8State:
     # ------------------------------------------------------------------ producer-side codes
     _PRE_MAX = 64  # pending entries kept at most (an unconsumed output is dropped oldest first)
 
-    def produce(self, key, fmt, like):
+    def produce(self, key, fmt, like, shape=None):
         """Arguments for a producer kernel that writes fp8 codes of its own output ``like``:
         ``(codes_out, scale, amax, fmt, slot)`` — or None on the slot's first use, when there is
         no amax history to scale with yet (the caller then runs without the side output and
@@ -231,7 +231,7 @@ class Fp8State:
         s = self.slot(key, fmt)
         if s in self._fresh:
             return None
-        codes = torch.empty(like.shape, dtype=torch.uint8, device=like.device)
+        codes = torch.empty(like.shape if shape is None else shape, dtype=torch.uint8, device=like.device)
         return codes, self._view("scale", s), self._view("amax", s), fmt, s
 
     def register(self, t, codes, slot, fmt):
@@ -273,14 +273,26 @@ class Fp8State:
             return False
         return True
 
-    def forward_gemm(self, a, w, epi, bias=None, aux=None):
-        """a [M, K] @ w[N, K]^T with epilogue ``epi`` on the fp8 kernel -> (out, extra) or None."""
+    def forward_gemm(self, a, w, epi, bias=None, aux=None, q8=None):
+        """a [M, K] @ w[N, K]^T with epilogue ``epi`` on the fp8 kernel -> (out, extra) or None.
+        ``q8`` (from ``produce``; bias+GELU epilogues): the epilogue also writes the output's fp8
+        codes — ``q8_written(q8)`` tells the caller whether this call ran and wrote them."""
         if not self._fits(a, w, bias, aux, w.shape[1], w.shape[0]):
             return None
         pre = self._take(a, self._fwd) if self._pre else None
         a8, ia = pre if pre is not None else self.quantize(a, (self.key_of(w), "x"), self._fwd)
         w8, iw = self.weight(w)
-        return _C().gemm_f8(a8, w8, ia, iw, self._fwd, epi, bias, aux, None, a.dtype)
+        kw = {}
+        if q8 is not None:
+            kw = dict(q8_out=q8[0], q8_scale=q8[1], q8_amax=q8[2], q8_fmt=q8[3])
+            self._q8_last = q8[0]
+        return _C().gemm_f8(a8, w8, ia, iw, self._fwd, epi, bias, aux, None, a.dtype, **kw)
+
+    def q8_written(self, q8):
+        """True when the last ``forward_gemm`` given ``q8`` ran on the fp8 kernel (codes written)."""
+        ok = q8 is not None and getattr(self, "_q8_last", None) is q8[0]
+        self._q8_last = None
+        return ok
 
     def backward_gemm(self, dy, w, epi, aux=None, bias_grad_dtype=None):
         """dy [M, N] @ w[N, K] with epilogue ``epi`` (dy e5m2 x W^T e4m3) -> (out, extra) or None."""

@@ -54,11 +54,11 @@ def _ln_mem(C, cols):
 _FP8_PRODUCER = os.environ.get("APEX_FP8_PRODUCER", "1") != "0"
 
 
-def _q8(f8, key, fmt, like):
+def _q8(f8, key, fmt, like, shape=None):
     """(codes, scale, amax, fmt, slot) for a producer kernel, or None (no fp8 / first use)."""
     if f8 is None or not _FP8_PRODUCER:
         return None
-    return f8.produce(key, fmt, like)
+    return f8.produce(key, fmt, like, shape=shape)
 
 
 def _q8_kw(q8):
@@ -144,8 +144,14 @@ class _FFNSublayer(torch.autograd.Function):
         f8 = ctx.f8 = G.fp8_state()
         if act == ACT_GELU and b1 is not None:
             # g = gelu(h), h = x W1^T + b1; the backward keeps gelu'(h) (computed in this epilogue
-            # from the same exp/erf) rather than h
-            g, h = G.linear_gelu_d(x2, w1, b1, f8=f8) if _STORE_DERIV else G.linear_gelu(x2, w1, b1, f8=f8)
+            # from the same exp/erf) rather than h. fp8: the epilogue also writes g's e4m3 codes for
+            # the W2 GEMM (producer slot keyed by W1, role "y")
+            gkey = (f8.key_of(w1), "y") if f8 is not None else None
+            q8 = _q8(f8, gkey, f8._fwd, x2, shape=(x2.shape[0], w1.shape[0])) if f8 is not None else None
+            g, h = G.linear_gelu_d(x2, w1, b1, f8=f8, q8=q8) if _STORE_DERIV else \
+                G.linear_gelu(x2, w1, b1, f8=f8, q8=q8)
+            if f8 is not None:
+                _q8_file(f8, g, q8 if f8.q8_written(q8) else None, gkey, f8._fwd)
             hb = None
         else:
             h = torch.mm(x2, w1.t())

@@ -100,12 +100,13 @@ def linear(x, w, b=None, f8=None):
 ACT_GELU, ACT_GELU_TANH = 0, 1  # apex.ops.fused activation codes
 
 
-def linear_gelu(x, w, b, act=ACT_GELU, f8=None):
-    """(gelu(h), h) with h = x w^T + b (erf GELU, or tanh GELU for act=1); h kept for backward."""
+def linear_gelu(x, w, b, act=ACT_GELU, f8=None, q8=None):
+    """(gelu(h), h) with h = x w^T + b (erf GELU, or tanh GELU for act=1); h kept for backward.
+    ``q8``: fp8 side output of gelu(h) on the fp8 path (apex.fp8 producer-side codes)."""
     a = _2d(x)
     C = _C()
     shp = (*x.shape[:-1], w.shape[0])
-    r = f8.forward_gemm(a, w, C.EPI_BIAS_GELU_TANH if act == ACT_GELU_TANH else C.EPI_BIAS_GELU, b) \
+    r = f8.forward_gemm(a, w, C.EPI_BIAS_GELU_TANH if act == ACT_GELU_TANH else C.EPI_BIAS_GELU, b, q8=q8) \
         if f8 is not None and b is not None else None
     if r is not None:
         return r[0].view(shp), r[1].view(shp)
@@ -119,14 +120,14 @@ def linear_gelu(x, w, b, act=ACT_GELU, f8=None):
     return y.view(shp), h.view(shp)
 
 
-def linear_gelu_d(x, w, b, act=ACT_GELU, f8=None):
+def linear_gelu_d(x, w, b, act=ACT_GELU, f8=None, q8=None):
     """(gelu(h), gelu'(h)) with h = x w^T + b: the forward of an MLP whose backward multiplies by
     the stored derivative (dgrad_mul) instead of re-evaluating erf/exp from h. The derivative
     is taken at the rounded h, as the unfused composition's backward would."""
     a = _2d(x)
     C = _C()
     shp = (*x.shape[:-1], w.shape[0])
-    r = f8.forward_gemm(a, w, C.EPI_BIAS_GELU_TANH_D if act == ACT_GELU_TANH else C.EPI_BIAS_GELU_D, b) \
+    r = f8.forward_gemm(a, w, C.EPI_BIAS_GELU_TANH_D if act == ACT_GELU_TANH else C.EPI_BIAS_GELU_D, b, q8=q8) \
         if f8 is not None and b is not None else None
     if r is not None:
         return r[0].view(shp), r[1].view(shp)

@@ -1104,7 +1104,9 @@ bool k_gemm_f8_supported(Tensor a, Tensor b) {
 
 std::vector<Tensor> k_gemm_f8(Tensor a, Tensor b, Tensor alpha_a, Tensor alpha_b, int64_t fmt_a, int64_t epi,
                               const c10::optional<Tensor>& bias, const c10::optional<Tensor>& aux,
-                              c10::optional<at::ScalarType> bias_grad_dtype, at::ScalarType out_dtype) {
+                              c10::optional<at::ScalarType> bias_grad_dtype, at::ScalarType out_dtype,
+                              const c10::optional<Tensor>& q8_out, const c10::optional<Tensor>& q8_scale,
+                              const c10::optional<Tensor>& q8_amax, int64_t q8_fmt) {
   TORCH_CHECK(k_gemm_f8_supported(a, b), "gemm_f8: unsupported operands (uint8 codes, K % 128 == 0, N % 8 == 0, "
               "16-byte aligned, unit inner stride)");
   TORCH_CHECK(out_dtype == at::kBFloat16 || out_dtype == at::kHalf, "gemm_f8: bf16 / fp16 output");
@@ -1152,6 +1154,8 @@ std::vector<Tensor> k_gemm_f8(Tensor a, Tensor b, Tensor alpha_a, Tensor alpha_b
     part = at::empty({apex::gemm_part_rows((int)M), N}, a.options().dtype(at::kFloat));
     g.part = part.data_ptr<float>();
   }
+  g.q8 = q8_args(q8_out, q8_scale, q8_amax, q8_fmt, c, "gemm_f8");
+  TORCH_CHECK(!g.q8.y || gelu_fwd, "gemm_f8: q8_out needs a bias+GELU epilogue");
   check(apex::gemm_nt_f8(g, (int)fmt_a, 0, dt_code(out_dtype), cur_stream()), "gemm_f8");
   if (mul && bias_grad_dtype.has_value()) {
     extra = at::empty({N}, a.options().dtype(*bias_grad_dtype));
@@ -1346,7 +1350,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_f8_supported", &k_gemm_f8_supported);
   m.def("gemm_f8", &k_gemm_f8, py::arg("a"), py::arg("b"), py::arg("alpha_a"), py::arg("alpha_b"), py::arg("fmt_a"),
         py::arg("epi"), py::arg("bias") = py::none(), py::arg("aux") = py::none(),
-        py::arg("bias_grad_dtype") = py::none(), py::arg("out_dtype") = at::kBFloat16);
+        py::arg("bias_grad_dtype") = py::none(), py::arg("out_dtype") = at::kBFloat16, py::arg("q8_out") = py::none(),
+        py::arg("q8_scale") = py::none(), py::arg("q8_amax") = py::none(), py::arg("q8_fmt") = 0);
   m.def("fp8_quantize", &k_fp8_quantize, py::arg("x"), py::arg("fmt"), py::arg("scale"), py::arg("amax") = py::none(),
         py::arg("cur_amax") = py::none(), py::arg("scale_inv") = py::none(), py::arg("smax") = 0.0);
   m.def("fp8_quantize_t", &k_fp8_quantize_t, py::arg("x"), py::arg("fmt"), py::arg("scale"),

@@ -38,6 +38,7 @@
 //    GROUP_M=8 panel ordering, so concurrently running tiles on one XCD share A/B panels in L2.
 #include "common.h"
 #include "kernels.h"
+#include "fp8_pack.h"
 
 #include <cstdio>
 #include <cstdlib>
@@ -420,11 +421,15 @@ __device__ __forceinline__ void stage_acc(const f32x4 (&acc)[NJ][8], char* reg, 
 }
 
 // STAGED: the accumulators are already in `reg` (stage_acc), `acc` is not read
-template <typename T, int EPI, bool EDGE, int J0 = 0, int NJ = 4, bool STAGED = false>
+// Q8 (1 + fp8 format, 0 = off): the C output's fp8 codes are written too (q8.y, ldc bytes per row,
+// scaled by q8.scale[0], max|C| into q8.amax) — the next GEMM's fp8 operand without a standalone
+// quantise pass over C
+template <typename T, int EPI, bool EDGE, int J0 = 0, int NJ = 4, bool STAGED = false, int Q8 = 0>
 __device__ __forceinline__ void epilogue(const f32x4 (&acc)[NJ][8], char* reg, T* __restrict__ C, int M, int N,
                                          int64_t ldc, const T* __restrict__ bias, const T* __restrict__ aux,
                                          int64_t ldaux, T* __restrict__ aux_out, float* __restrict__ part, int m0,
-                                         int n0, int tm, int wr, int wc, int lane, float alpha = 1.f) {
+                                         int n0, int tm, int wr, int wc, int lane, float alpha = 1.f,
+                                         const Q8Out& q8 = Q8Out{}) {
   const int lr = lane & 15, lk = lane >> 4;
   // acc[j][i] holds rows wr*128 + i*16 + lr, cols wc*64 + j*16 + 4*lk .. +3 of the tile. The fp32
   // accumulators are rounded to T and transposed through the wave's own 16 KB LDS region
@@ -469,7 +474,12 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[NJ][8], char* reg, T
     return (wrow0 + r < M && ncol < N) ? (uint32_t)((r * ld + lcol) * (int64_t)sizeof(T)) : 0x80000000u;
   };
   const __amdgpu_buffer_rsrc_t rs_c = wave_res(C, ldc);
-  __amdgpu_buffer_rsrc_t rs_o = rs_c, rs_x = rs_c;
+  __amdgpu_buffer_rsrc_t rs_o = rs_c, rs_x = rs_c, rs_q = rs_c;
+  float q8s = 0.f, q8mx = 0.f;
+  if constexpr (Q8 != 0) {
+    q8s = q8.scale[0];
+    rs_q = wave_rsrc(q8.y + (int64_t)wrow0 * ldc + wcol0, (uint32_t)(128 * ldc));
+  }
   if constexpr (GELU_FWD) rs_o = wave_res(aux_out, ldc);
   if constexpr (AUX_IN) rs_x = wave_res(aux, ldaux);
   auto unpack = [&](const u32x4& x, float (&v)[8]) {
@@ -590,11 +600,25 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[NJ][8], char* reg, T
             }
           }
           out = pack(v);
-          if constexpr (COLSUM) {
+          if constexpr (COLSUM || Q8 != 0) {
             float r[8];
-            unpack(out, r);  // the bias grad sums the stored (rounded) values
+            unpack(out, r);  // the bias grad / the fp8 codes take the stored (rounded) values
+            if constexpr (COLSUM) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) csum[e] += r[e];
+              for (int e = 0; e < 8; ++e) csum[e] += r[e];
+            }
+            if constexpr (Q8 != 0) {
+              typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+              for (int e = 0; e < 8; ++e) {
+                q8mx = fmaxf(q8mx, fabsf(r[e]));
+                r[e] *= q8s;
+              }
+              const u32x2 w = u32x2{f8_pack4<Q8 - 1>(r[0], r[1], r[2], r[3]), f8_pack4<Q8 - 1>(r[4], r[5], r[6], r[7])};
+              const int qr = lrow + slot * 8;
+              const uint32_t qo = (F || (wrow0 + qr < M && ncol < N)) ? (uint32_t)(qr * ldc + lcol) : 0x80000000u;
+              __builtin_amdgcn_raw_buffer_store_b64(w, rs_q, qo, 0, 0);
+            }
           }
         }
         st(rs_c, slot, out);
@@ -620,6 +644,10 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[NJ][8], char* reg, T
         *reinterpret_cast<f32x4*>(pp + 4) = f32x4{csum[4], csum[5], csum[6], csum[7]};
       }
     }
+    if constexpr (Q8 != 0) {  // one amax atomic per wave, filtered by a plain read (amax only grows)
+      const float m = f8_wave_max(q8mx);
+      if (lane == 0 && m > 0.f && m > *(volatile float*)q8.amax) f8_atomic_max_pos(q8.amax, m);
+    }
   }
 }
 
@@ -635,14 +663,16 @@ int h_gemm_dbg = 0, h_gemm_stagger = 0;  // stagger: > 0 forced units, < 0 force
 
 // T: output / epilogue dtype; TI: operand dtype (T, or uint8_t fp8 with formats FA (A) / FB (B) and
 // the dequantisation alpha = alpha_a[0] * alpha_b[0] read on the device)
-template <typename T, int EPI, bool TR, bool EDGE, typename TI = T, int FA = -1, int FB = -1, int DBG = 0>
+template <typename T, int EPI, bool TR, bool EDGE, typename TI = T, int FA = -1, int FB = -1, int DBG = 0,
+          int Q8 = 0>
 __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(const TI* __restrict__ A, const TI* __restrict__ B,
                                                             T* __restrict__ C, int M, int N, int K, int64_t lda,
                                                             int64_t ldb, int64_t ldc, const T* __restrict__ bias,
                                                             const T* __restrict__ aux, int64_t ldaux,
                                                             T* __restrict__ aux_out, float* __restrict__ part,
                                                             int ctl, const float* __restrict__ alpha_a = nullptr,
-                                                            const float* __restrict__ alpha_b = nullptr) {
+                                                            const float* __restrict__ alpha_b = nullptr,
+                                                            Q8Out q8 = Q8Out{}) {
   __shared__ __attribute__((aligned(16))) char smem[G_LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -734,8 +764,8 @@ __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(const TI* __restrict
   }
   float alpha = 1.f;
   if constexpr (FA >= 0) alpha = alpha_a[0] * alpha_b[0];
-  epilogue<T, EPI, EDGE>(acc, smem + wid * 16384, C, M, N, ldc, bias, aux, ldaux, aux_out, part, m0, n0, tm, wr,
-                                wc, lane, alpha);
+  epilogue<T, EPI, EDGE, 0, 4, false, Q8>(acc, smem + wid * 16384, C, M, N, ldc, bias, aux, ldaux, aux_out, part, m0,
+                                         n0, tm, wr, wc, lane, alpha, q8);
 }
 
 
@@ -1296,6 +1326,31 @@ void launch_gemm(const GemmArgs& g, hipStream_t s) {
 template <typename T, int EPI, int FA, int FB>
 void launch_gemm_f8(const GemmArgs& g, hipStream_t s) {
   const int tiles = ((g.M + GB_M - 1) / GB_M) * ((g.N + GB_N - 1) / GB_N);
+  // fp8 codes of C for the next GEMM (the MLP's hidden activation, forward). Not for the input-
+  // operand epilogues (MUL / DGELU: the MLP's hidden gradient): with the codes and the bias-grad
+  // column sums live together those variants spilled ~100 VGPRs to scratch
+  constexpr bool Q8_OK = EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_TANH || EPI == EPI_BIAS_GELU_D ||
+                         EPI == EPI_BIAS_GELU_TANH_D;
+  if constexpr (Q8_OK) {
+    if (g.q8.y) {
+      auto go = [&](auto edge_c, auto q_c) {
+        hipLaunchKernelGGL((gemm_nt_kernel<T, EPI, false, decltype(edge_c)::value, uint8_t, FA, FB, 0,
+                                           decltype(q_c)::value>),
+                           dim3(tiles), dim3(G_THREADS), 0, s, (const uint8_t*)g.A, (const uint8_t*)g.B, (T*)g.C, g.M,
+                           g.N, g.K, g.lda, g.ldb, g.ldc, (const T*)g.bias, (const T*)g.aux, g.ldaux, (T*)g.aux_out,
+                           g.part, 0, g.alpha_a, g.alpha_b, g.q8);
+      };
+      const bool edge = g.M % GB_M != 0 || g.N % GB_N != 0;
+      if (g.q8.fmt == 0) {
+        if (edge) go(std::true_type{}, std::integral_constant<int, 1>{});
+        else go(std::false_type{}, std::integral_constant<int, 1>{});
+      } else {
+        if (edge) go(std::true_type{}, std::integral_constant<int, 2>{});
+        else go(std::false_type{}, std::integral_constant<int, 2>{});
+      }
+      return;
+    }
+  }
   if (g.M % GB_M != 0 || g.N % GB_N != 0)
     hipLaunchKernelGGL((gemm_nt_kernel<T, EPI, false, true, uint8_t, FA, FB>), dim3(tiles), dim3(G_THREADS), 0, s,
                        (const uint8_t*)g.A, (const uint8_t*)g.B, (T*)g.C, g.M, g.N, g.K, g.lda, g.ldb, g.ldc,

@@ -443,10 +443,40 @@ def test_blocks_fp8_producer_codes_match_standalone_path(fp8_off, monkeypatch):
     ref, hits_off = run_steps(False)
     got, hits_on = run_steps(True)
     assert hits_off == 0
-    # per step: 2 LN outputs consumed in forward + 3 dt in backward; step 0's backward slots are
-    # fresh (standalone current scaling), its forward producer slots file standalone codes
-    assert hits_on == 2 + 2 * 5, hits_on
+    # per step: 2 LN outputs + the FFN's gelu output consumed in forward, 3 dt in backward; step 0's
+    # backward slots are fresh (standalone current scaling), its forward producer slots file
+    # standalone codes
+    assert hits_on == 3 + 2 * 6, hits_on
     for (ya, ga), (yb, gb) in zip(got, ref):
         torch.testing.assert_close(ya, yb, rtol=0, atol=0)
         for a, b in zip(ga, gb):
             torch.testing.assert_close(a, b, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("epi_name", ["EPI_BIAS_GELU_D", "EPI_BIAS_GELU"])
+@pytest.mark.parametrize("M,N", [(512, 1024), (300, 520)])
+@pytest.mark.parametrize("fmt", [0, 1])
+def test_gemm_f8_q8_side_output_matches_standalone_quantize(epi_name, M, N, fmt):
+    """The fp8 GEMM's bias+GELU epilogue writing the fp8 codes of its output (full and edge tiles):
+    bit-identical to the standalone quantiser on the bf16 output with the same scale, same amax."""
+    C = _C()
+    torch.manual_seed(12)
+    K = 256
+    a = torch.randn(M, K, device=DEV)
+    w = torch.randn(N, K, device=DEV) * 0.1
+    one = torch.ones(1, device=DEV)
+    a8 = C.fp8_quantize(a.bfloat16(), 0, one)
+    w8 = C.fp8_quantize(w.bfloat16(), 0, one)
+    bias = (torch.randn(N, device=DEV) * 0.1).bfloat16()
+    epi = getattr(C, epi_name)
+    scale = torch.tensor([3.0], device=DEV)
+    amax = torch.zeros(1, device=DEV)
+    codes = torch.full((M, N), 7, device=DEV, dtype=torch.uint8)
+    out, _ = C.gemm_f8(a8, w8, one, one, 0, epi, bias, None, None, torch.bfloat16, q8_out=codes, q8_scale=scale,
+                       q8_amax=amax, q8_fmt=fmt)
+    plain, _ = C.gemm_f8(a8, w8, one, one, 0, epi, bias, None, None, torch.bfloat16)
+    assert torch.equal(out, plain)
+    amax_ref = torch.zeros(1, device=DEV)
+    ref = C.fp8_quantize(out, fmt, scale, amax_ref)
+    assert torch.equal(codes, ref)
+    assert float(amax) == float(amax_ref)
