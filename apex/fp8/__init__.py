@@ -294,14 +294,18 @@ class Fp8State:
         self._q8_last = None
         return ok
 
-    def backward_gemm(self, dy, w, epi, aux=None, bias_grad_dtype=None):
+    def backward_gemm(self, dy, w, epi, aux=None, bias_grad_dtype=None, q8=None):
         """dy [M, N] @ w[N, K] with epilogue ``epi`` (dy e5m2 x W^T e4m3) -> (out, extra) or None."""
         if not self._fits(dy, w, None, aux, w.shape[0], w.shape[1]):
             return None
         pre = self._take(dy, self._bwd) if self._pre else None
         d8, id_ = pre if pre is not None else self.quantize(dy, (self.key_of(w), "dy"), self._bwd)
         wt8, iw = self.weight_t(w)
-        return _C().gemm_f8(d8, wt8, id_, iw, self._bwd, epi, None, aux, bias_grad_dtype, dy.dtype)
+        kw = {}
+        if q8 is not None:  # (dGELU / MUL epilogues: the hidden gradient's codes for the W1 dgrad)
+            kw = dict(q8_out=q8[0], q8_scale=q8[1], q8_amax=q8[2], q8_fmt=q8[3])
+            self._q8_last = q8[0]
+        return _C().gemm_f8(d8, wt8, id_, iw, self._bwd, epi, None, aux, bias_grad_dtype, dy.dtype, **kw)
 
     # ------------------------------------------------------------------ step
     def step(self):

@@ -189,11 +189,16 @@ class _FFNSublayer(torch.autograd.Function):
             f8.register(dt, q8[0], q8[4], q8[3])
         if hb is None and act == ACT_GELU and b1dt is not None:
             tb1 = _gt(pb1)
+            # fp8: the epilogue also writes dh's e5m2 codes for the W1 dgrad (W1's own "dy" slot)
+            hkey = (f8.key_of(w1), "dy") if f8 is not None else None
+            q8h = _q8(f8, hkey, f8._bwd, dt, shape=(dt.shape[0], w1.shape[0])) if f8 is not None else None
             if _STORE_DERIV:
                 # (dt W2) * gelu'(h) (stored) and its column sums
-                dh, db1 = G.dgrad_mul(dt, w2, h, b1dt, f8=f8, bias_grad_out=tb1)
+                dh, db1 = G.dgrad_mul(dt, w2, h, b1dt, f8=f8, bias_grad_out=tb1, q8=q8h)
             else:
-                dh, db1 = G.dgrad_dgelu(dt, w2, h, b1dt, f8=f8, bias_grad_out=tb1)  # (dt W2) * gelu'(h) from h
+                dh, db1 = G.dgrad_dgelu(dt, w2, h, b1dt, f8=f8, bias_grad_out=tb1, q8=q8h)  # (dt W2) * gelu'(h) from h
+            if q8h is not None and f8.q8_written(q8h):
+                f8.register(dh, q8h[0], q8h[4], q8h[3])
             if tb1 is not None and db1 is not None and db1.data_ptr() != tb1.data_ptr():
                 db1 = tb1.copy_(db1)  # a path that could not write the slot: keep the handed-out view valid
         else:

@@ -141,13 +141,13 @@ def linear_gelu_d(x, w, b, act=ACT_GELU, f8=None, q8=None):
     return y.view(shp), gd.view(shp)
 
 
-def dgrad_mul(dy, w, gd, bias_dtype, wT=None, f8=None, bias_grad_out=None):
+def dgrad_mul(dy, w, gd, bias_dtype, wT=None, f8=None, bias_grad_out=None, q8=None):
     """(dh, db): dh = (dy @ w) * gd (gd = the stored activation derivative), db = column sums of dh
     (written into ``bias_grad_out`` on the MFMA path when given)."""
     a = _2d(dy)
     g2 = _2d(gd)
     C = _C()
-    r = f8.backward_gemm(a, w, C.EPI_MUL, g2, bias_dtype) if f8 is not None else None
+    r = f8.backward_gemm(a, w, C.EPI_MUL, g2, bias_dtype, q8=q8) if f8 is not None else None
     if r is not None:
         return r
     if _MODE != "blas" and a.is_cuda and g2.is_contiguous() and g2.dtype == a.dtype:
@@ -193,13 +193,13 @@ def dgrad_resid(dy, w, r, wT=None, f8=None):
     return torch.addmm(r2, a, w).view(*dy.shape[:-1], w.shape[1])
 
 
-def dgrad_dgelu(dy, w, h, bias_dtype, wT=None, act=ACT_GELU, f8=None, bias_grad_out=None):
+def dgrad_dgelu(dy, w, h, bias_dtype, wT=None, act=ACT_GELU, f8=None, bias_grad_out=None, q8=None):
     """(dh, db): dh = (dy @ w) * gelu'(h), db = column sums of dh (in bias_dtype; written into
     ``bias_grad_out`` on the MFMA path when given)."""
     a = _2d(dy)
     h2 = _2d(h)
     C = _C()
-    r = f8.backward_gemm(a, w, C.EPI_DGELU_TANH if act == ACT_GELU_TANH else C.EPI_DGELU, h2, bias_dtype) \
+    r = f8.backward_gemm(a, w, C.EPI_DGELU_TANH if act == ACT_GELU_TANH else C.EPI_DGELU, h2, bias_dtype, q8=q8) \
         if f8 is not None else None
     if r is not None:
         return r

@@ -606,8 +606,14 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[NJ][8], char* reg, T
             if constexpr (COLSUM) {
 #pragma unroll
               for (int e = 0; e < 8; ++e) csum[e] += r[e];
+              // fp8 codes later, from LDS: the slot's chunk (read above, this lane's alone) takes the
+              // stored value back — inline, the codes' live ranges spilled ~100 VGPRs in these variants
+              if constexpr (Q8 != 0) {
+                const int row = slot * 8 + lrow;
+                *reinterpret_cast<u32x4*>(reg + row * 128 + (((lane & 7) ^ (row & 7)) << 4)) = out;
+              }
             }
-            if constexpr (Q8 != 0) {
+            if constexpr (Q8 != 0 && !COLSUM) {
               typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
               for (int e = 0; e < 8; ++e) {
@@ -642,6 +648,23 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[NJ][8], char* reg, T
         float* pp = part + (int64_t)(tm * 2 + wr) * N + ncol;
         *reinterpret_cast<f32x4*>(pp) = f32x4{csum[0], csum[1], csum[2], csum[3]};
         *reinterpret_cast<f32x4*>(pp + 4) = f32x4{csum[4], csum[5], csum[6], csum[7]};
+      }
+    }
+    if constexpr (Q8 != 0 && COLSUM) {  // the stashed outputs -> fp8 codes
+      typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+#pragma unroll 4
+      for (int slot = 0; slot < 16; ++slot) {
+        const int row = slot * 8 + lrow;
+        float r[8];
+        unpack(*reinterpret_cast<const u32x4*>(reg + row * 128 + (((lane & 7) ^ (row & 7)) << 4)), r);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          q8mx = fmaxf(q8mx, fabsf(r[e]));
+          r[e] *= q8s;
+        }
+        const u32x2 w = u32x2{f8_pack4<Q8 - 1>(r[0], r[1], r[2], r[3]), f8_pack4<Q8 - 1>(r[4], r[5], r[6], r[7])};
+        const uint32_t qo = (F || (wrow0 + row < M && ncol < N)) ? (uint32_t)(row * ldc + lcol) : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b64(w, rs_q, qo, 0, 0);
       }
     }
     if constexpr (Q8 != 0) {  // one amax atomic per wave, filtered by a plain read (amax only grows)
@@ -1326,11 +1349,9 @@ void launch_gemm(const GemmArgs& g, hipStream_t s) {
 template <typename T, int EPI, int FA, int FB>
 void launch_gemm_f8(const GemmArgs& g, hipStream_t s) {
   const int tiles = ((g.M + GB_M - 1) / GB_M) * ((g.N + GB_N - 1) / GB_N);
-  // fp8 codes of C for the next GEMM (the MLP's hidden activation, forward). Not for the input-
-  // operand epilogues (MUL / DGELU: the MLP's hidden gradient): with the codes and the bias-grad
-  // column sums live together those variants spilled ~100 VGPRs to scratch
+  // fp8 codes of C for the next GEMM (the MLP's hidden activation forward, its gradient backward)
   constexpr bool Q8_OK = EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_TANH || EPI == EPI_BIAS_GELU_D ||
-                         EPI == EPI_BIAS_GELU_TANH_D;
+                         EPI == EPI_BIAS_GELU_TANH_D || EPI == EPI_MUL || EPI == EPI_DGELU || EPI == EPI_DGELU_TANH;
   if constexpr (Q8_OK) {
     if (g.q8.y) {
       auto go = [&](auto edge_c, auto q_c) {

@@ -443,10 +443,11 @@ def test_blocks_fp8_producer_codes_match_standalone_path(fp8_off, monkeypatch):
     ref, hits_off = run_steps(False)
     got, hits_on = run_steps(True)
     assert hits_off == 0
-    # per step: 2 LN outputs + the FFN's gelu output consumed in forward, 3 dt in backward; step 0's
+    # per step: 2 LN outputs + the FFN's gelu output consumed in forward, 3 dt + the FFN's hidden
+    # gradient in backward; step 0's
     # backward slots are fresh (standalone current scaling), its forward producer slots file
     # standalone codes
-    assert hits_on == 3 + 2 * 6, hits_on
+    assert hits_on == 3 + 2 * 7, hits_on
     for (ya, ga), (yb, gb) in zip(got, ref):
         torch.testing.assert_close(ya, yb, rtol=0, atol=0)
         for a, b in zip(ga, gb):
@@ -478,5 +479,33 @@ def test_gemm_f8_q8_side_output_matches_standalone_quantize(epi_name, M, N, fmt)
     assert torch.equal(out, plain)
     amax_ref = torch.zeros(1, device=DEV)
     ref = C.fp8_quantize(out, fmt, scale, amax_ref)
+    assert torch.equal(codes, ref)
+    assert float(amax) == float(amax_ref)
+
+
+@pytest.mark.parametrize("epi_name", ["EPI_MUL", "EPI_DGELU"])
+@pytest.mark.parametrize("M,N", [(512, 1024), (300, 520)])
+def test_gemm_f8_q8_side_output_backward_epilogues(epi_name, M, N):
+    """The backward (input-operand) epilogues' e5m2 side output, written from the LDS-stashed
+    outputs after the slot loop: codes bit-identical to the standalone quantiser, amax equal, the
+    bf16 output and the bias-gradient column sums unchanged."""
+    C = _C()
+    torch.manual_seed(13)
+    K = 256
+    one = torch.ones(1, device=DEV)
+    a8 = C.fp8_quantize(torch.randn(M, K, device=DEV).bfloat16(), 1, one)
+    w8 = C.fp8_quantize((torch.randn(N, K, device=DEV) * 0.1).bfloat16(), 0, one)
+    aux = torch.randn(M, N, device=DEV).bfloat16()
+    epi = getattr(C, epi_name)
+    scale = torch.tensor([100.0], device=DEV)
+    amax = torch.zeros(1, device=DEV)
+    codes = torch.full((M, N), 7, device=DEV, dtype=torch.uint8)
+    out, db = C.gemm_f8(a8, w8, one, one, 1, epi, None, aux, torch.float32, torch.bfloat16, q8_out=codes,
+                        q8_scale=scale, q8_amax=amax, q8_fmt=1)
+    plain, db_plain = C.gemm_f8(a8, w8, one, one, 1, epi, None, aux, torch.float32, torch.bfloat16)
+    assert torch.equal(out, plain)
+    torch.testing.assert_close(db, db_plain, rtol=0, atol=0)
+    amax_ref = torch.zeros(1, device=DEV)
+    ref = C.fp8_quantize(out, 1, scale, amax_ref)
     assert torch.equal(codes, ref)
     assert float(amax) == float(amax_ref)
