@@ -1155,7 +1155,7 @@ std::vector<Tensor> k_gemm_f8(Tensor a, Tensor b, Tensor alpha_a, Tensor alpha_b
     g.part = part.data_ptr<float>();
   }
   g.q8 = q8_args(q8_out, q8_scale, q8_amax, q8_fmt, c, "gemm_f8");
-  TORCH_CHECK(!g.q8.y || gelu_fwd, "gemm_f8: q8_out needs a bias+GELU epilogue");
+  TORCH_CHECK(!g.q8.y || gelu_fwd || mul, "gemm_f8: q8_out needs a GELU / dGELU / MUL epilogue");
   check(apex::gemm_nt_f8(g, (int)fmt_a, 0, dt_code(out_dtype), cur_stream()), "gemm_f8");
   if (mul && bias_grad_dtype.has_value()) {
     extra = at::empty({N}, a.options().dtype(*bias_grad_dtype));

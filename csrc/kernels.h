@@ -239,7 +239,7 @@ struct GemmArgs {
   int splits;        // gemm_tt: split-K slices (blockIdx.y)
   const float* alpha_a = nullptr;  // fp8: dequantisation scales (1 / quantisation scale) of A and B,
   const float* alpha_b = nullptr;  // device scalars; C = epi(alpha_a * alpha_b * A8 . B8^T)
-  Q8Out q8{};  // fp8 GEMM, bias+GELU epilogues: also write fp8 codes of C (ldc bytes per row)
+  Q8Out q8{};  // fp8 GEMM, GELU / dGELU / MUL epilogues: also write fp8 codes of C (ldc bytes per row)
 };
 bool gemm_supported(int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc);
 int64_t gemm_part_rows(int M);
