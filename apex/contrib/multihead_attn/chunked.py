@@ -21,10 +21,19 @@ import math
 import torch
 
 
-def _block_rows(B, H, Sk, budget_bytes=64 << 20):
+def _block_rows(B, H, Sq, Sk, budget_bytes=64 << 20, short_rows=1024, short_budget=2 << 30):
+    """Query rows per block. Training-length sequences (Sq <= ``short_rows``) run as ONE block —
+    no Python loop of ~15 torch ops per block forward and backward — whenever their fp32
+    temporaries fit ``short_budget`` (2 GiB, small next to 288 GB of HBM; B*H = 4096 at S = 128 is
+    1 GiB). Round 3 used the 64 MB long-sequence budget everywhere, which cut the fp32 BERT-Large
+    step into 16-row blocks (8 iterations x 24 layers x 3 micro-batches, fwd + bwd) and slowed it
+    from 1567 to 2458 ms. Longer sequences keep O(S * block) memory: power-of-two blocks of at
+    least 16 rows within ``budget_bytes``."""
     per_row = max(1, B * H * Sk * 4 * 4)  # ~4 fp32 [B, H, rows, Sk] temporaries alive per block
+    if Sq <= short_rows and per_row * Sq <= short_budget:
+        return int(Sq)
     rows = max(16, budget_bytes // per_row)
-    return int(min(1024, 1 << (int(rows).bit_length() - 1)))
+    return int(min(Sq, 1 << (int(rows).bit_length() - 1)))
 
 
 def _reduce_to(t, shape):
@@ -157,7 +166,7 @@ def chunked_attention(q, k, v, attn_bias=None, dropout_p=0.0, causal=False, scal
     B, Sq, H, d = q.shape
     Sk = k.shape[1]
     scale = 1.0 / math.sqrt(d) if scale is None else scale
-    block = block or _block_rows(B, H, Sk)
+    block = block or _block_rows(B, H, Sq, Sk)
     seed = 0
     if dropout_p > 0:
         seed = int(torch.randint(0, 2 ** 31 - 1, (1,), device="cpu").item())

@@ -89,6 +89,7 @@ class Fp8State:
         self.recipe = recipe or Fp8Recipe()
         self._next_key = 0
         self._free: list = []  # slot indices released by dead tensors, reused lowest first
+        self._dying: list = []  # released since the last step(); moved to _free (sorted) at step()
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
         self.device = torch.device(device)
@@ -103,7 +104,12 @@ class Fp8State:
         self._wcache: dict = {}
         self._fwd = self.recipe.fmt("fwd")
         self._bwd = self.recipe.fmt("bwd")
-        self._pre: dict = {}  # (data_ptr, numel) -> (tensor, version, codes, slot): producer-made codes
+        # (data_ptr, numel) -> (weakref to the tensor, version, codes, slot, fmt): producer-made codes
+        # awaiting their consuming GEMM. The tensor itself is NOT kept alive (an output nobody
+        # consumes — the last layer's y, eval loops without step() — would otherwise stay pinned);
+        # while the weakref is alive the (pointer, numel) key cannot name recycled memory.
+        self._pre: dict = {}
+        self._pre_bytes = 0
         self.prequant_hits = 0
         self._grow(128)
 
@@ -145,7 +151,10 @@ class Fp8State:
             s = st.slots.pop((key, role), None)
             if s is not None:
                 st._fresh.discard(s)
-                st._free.append(s)
+                # reusable only from the next step() on, in sorted order: finalizers run when the
+                # garbage collector gets to them, which need not be the same point on every rank
+                # of the amax reduction group — slot i must name the same role on all of them
+                st._dying.append(s)
         st._wcache.pop(key, None)
 
     def slot(self, key, fmt) -> int:
@@ -220,6 +229,7 @@ class Fp8State:
 
     # ------------------------------------------------------------------ producer-side codes
     _PRE_MAX = 64  # pending entries kept at most (an unconsumed output is dropped oldest first)
+    _PRE_MAX_BYTES = 4 << 30  # and at most this many bytes of pending codes
 
     def produce(self, key, fmt, like, shape=None):
         """Arguments for a producer kernel that writes fp8 codes of its own output ``like``:
@@ -237,9 +247,29 @@ class Fp8State:
     def register(self, t, codes, slot, fmt):
         """File producer-made codes of ``t`` (format ``fmt``, scaled by ``slot``) for the GEMM that
         consumes ``t`` next."""
-        if len(self._pre) >= self._PRE_MAX:
-            self._pre.pop(next(iter(self._pre)))
-        self._pre[(t.data_ptr(), t.numel())] = (t, t._version, codes, slot, fmt)
+        # prune entries whose tensor died unconsumed, then cap by count and bytes (oldest first)
+        for k in [k for k, e in self._pre.items() if e[0]() is None]:
+            self._drop_pre(k)
+        nb = codes.numel()
+        while self._pre and (len(self._pre) >= self._PRE_MAX or self._pre_bytes + nb > self._PRE_MAX_BYTES):
+            self._drop_pre(next(iter(self._pre)))
+        key = (t.data_ptr(), t.numel())
+        self._drop_pre(key)
+        self._pre[key] = (weakref.ref(t), t._version, codes, slot, fmt)
+        self._pre_bytes += nb
+
+    def _recycle_slots(self):
+        """Slots of tensors that died since the last step become reusable (lowest first)."""
+        if self._dying:
+            self._free.extend(self._dying)
+            self._free.sort()
+            self._dying = []
+
+    def _drop_pre(self, key):
+        e = self._pre.pop(key, None)
+        if e is not None:
+            self._pre_bytes -= e[2].numel()
+        return e
 
     def quantize_output(self, t, key, fmt):
         """First use of a producer slot: standalone current-scaled quantisation of ``t`` (records
@@ -251,11 +281,12 @@ class Fp8State:
         self.register(t, codes, s, fmt)
 
     def _take(self, a, fmt):
-        e = self._pre.pop((a.data_ptr(), a.numel()), None)
+        e = self._drop_pre((a.data_ptr(), a.numel()))
         if e is None:
             return None
-        t, ver, codes, s, cfmt = e
-        if a._version != ver or a.dtype != t.dtype or not a.is_contiguous() or cfmt != fmt:
+        ref, ver, codes, s, cfmt = e
+        t = ref()
+        if t is None or a._version != ver or a.dtype != t.dtype or not a.is_contiguous() or cfmt != fmt:
             return None
         self.prequant_hits += 1
         return codes.view(a.shape), self._view("scale_inv", s)
@@ -316,6 +347,8 @@ class Fp8State:
         self.steps += 1
         self._wcache.clear()
         self._pre.clear()
+        self._pre_bytes = 0
+        self._recycle_slots()
         if self.n == 0:
             return
         r = self.recipe

@@ -38,8 +38,11 @@ _STORE_DERIV = os.environ.get("APEX_MLP_STORE", "deriv") != "h"
 # Memory-efficient post-LN: the bias+dropout+residual+LN forward does not store its LN input s; the
 # backward rebuilds x-hat = (y - beta) / gamma from the LN output y, which is saved anyway as the next
 # sublayer's GEMM input — one [tokens, hidden] write less per sublayer (and that much less activation
-# memory). As with any output-based LayerNorm backward, a gamma entry of exactly 0 makes its column's
-# x-hat unrecoverable. APEX_LN_MEM=0 stores s.
+# memory bandwidth). As with any output-based LayerNorm backward, a gamma entry of exactly 0 makes its
+# column's x-hat unrecoverable: the forward kernel therefore also gets an (untouched) s buffer and
+# writes it only when it sees a zero in gamma, and the backward kernel makes the same test and reads
+# that s instead (csrc/fused_ops.hip, s_cond / s_alt) — exact gradients in every case, the extra
+# [tokens, hidden] write only in the degenerate one. APEX_LN_MEM=0 always stores s.
 _LN_MEM = os.environ.get("APEX_LN_MEM", "1") != "0"
 
 
@@ -93,10 +96,11 @@ class _AttnSublayer(torch.autograd.Function):
         ykey = (f8.key_of(gamma), "y") if f8 is not None else None
         q8 = _q8(f8, ykey, f8._fwd, t) if f8 is not None else None
         y, s, mean, rstd = C.bdaln_fwd(t, bo, x2.contiguous(), gamma, beta, float(eps), float(p_hidden), sh, oh,
-                                       store_s=not mem, **_q8_kw(q8))
+                                       s_cond=mem, **_q8_kw(q8))
         if f8 is not None:
             _q8_file(f8, y, q8, ykey, f8._fwd)
-        ctx.save_for_backward(x2, wqkv, qkv, o, lse, k_lens, dmask, wo, y if mem else s, gamma, mean, rstd)
+        ctx.save_for_backward(x2, wqkv, qkv, o, lse, k_lens, dmask, wo, y if mem else s, gamma, mean, rstd,
+                              s if mem else None)
         ctx.ln_beta = beta if mem else None
         ctx.f8 = f8
         ctx.params = (wqkv, bqkv, wo, bo, gamma, beta)
@@ -107,7 +111,7 @@ class _AttnSublayer(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         C = _ext.require()
-        x2, wqkv, qkv, o, lse, k_lens, dmask, wo, s, gamma, mean, rstd = ctx.saved_tensors
+        x2, wqkv, qkv, o, lse, k_lens, dmask, wo, s, gamma, mean, rstd, s_alt = ctx.saved_tensors
         B, S, E, heads, d, scale, causal, p_attn, sa, oa, p_hidden, sh, oh, has_bqkv, has_bo, bdt = ctx.cfg
         pqkv, pbqkv, pwo, pbo, pg, pb = ctx.params
         f8 = ctx.f8
@@ -116,7 +120,7 @@ class _AttnSublayer(torch.autograd.Function):
         dres, dt, dgamma, dbeta, dbo = C.bdaln_bwd(_2d(dy), s, gamma, mean, rstd, float(p_hidden), sh, oh, has_bo,
                                                    dgamma_out=_gt(pg), dbeta_out=_gt(pb),
                                                    dbias_out=_gt(pbo) if has_bo else None, beta=ctx.ln_beta,
-                                                   **_q8_kw(q8))
+                                                   s_alt=s_alt, **_q8_kw(q8))
         if q8 is not None:
             f8.register(dt, q8[0], q8[4], q8[3])
         dctx = G.dgrad(dt, wo, f8=f8).view(B, S, heads, d)
@@ -163,10 +167,10 @@ class _FFNSublayer(torch.autograd.Function):
         ykey = (f8.key_of(gamma), "y") if f8 is not None else None
         q8 = _q8(f8, ykey, f8._fwd, t) if f8 is not None else None
         y, s, mean, rstd = C.bdaln_fwd(t, b2, x2.contiguous(), gamma, beta, float(eps), float(p), seed, off,
-                                       store_s=not mem, **_q8_kw(q8))
+                                       s_cond=mem, **_q8_kw(q8))
         if f8 is not None:
             _q8_file(f8, y, q8, ykey, f8._fwd)
-        ctx.save_for_backward(x2, w1, hb, h, g, w2, y if mem else s, gamma, mean, rstd)
+        ctx.save_for_backward(x2, w1, hb, h, g, w2, y if mem else s, gamma, mean, rstd, s if mem else None)
         ctx.ln_beta = beta if mem else None
         ctx.cfg = (p, seed, off, act, b2 is not None, b1.dtype if b1 is not None else None)
         ctx.params = (w1, b1, w2, b2, gamma, beta)
@@ -175,7 +179,7 @@ class _FFNSublayer(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         C = _ext.require()
-        x2, w1, hb, h, g, w2, s, gamma, mean, rstd = ctx.saved_tensors
+        x2, w1, hb, h, g, w2, s, gamma, mean, rstd, s_alt = ctx.saved_tensors
         p, seed, off, act, has_b2, b1dt = ctx.cfg
         f8 = ctx.f8
         pw1, pb1, pw2, pb2, pg, pb = ctx.params
@@ -184,7 +188,7 @@ class _FFNSublayer(torch.autograd.Function):
         dres, dt, dgamma, dbeta, db2 = C.bdaln_bwd(_2d(dy), s, gamma, mean, rstd, float(p), seed, off, has_b2,
                                                    dgamma_out=_gt(pg), dbeta_out=_gt(pb),
                                                    dbias_out=_gt(pb2) if has_b2 else None, beta=ctx.ln_beta,
-                                                   **_q8_kw(q8))
+                                                   s_alt=s_alt, **_q8_kw(q8))
         if q8 is not None:
             f8.register(dt, q8[0], q8[4], q8[3])
         if hb is None and act == ACT_GELU and b1dt is not None:

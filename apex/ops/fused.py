@@ -117,7 +117,10 @@ def accumulate_main_grad(mg, dy2, x2):
             and dy2.is_contiguous() and x2.is_contiguous() and mg.is_contiguous()):
         mg.add_(dy2.t().float().mm(x2.float()))
         return mg
-    if _main_grad_tt(M, N, K) and _ext.require().gemm_tt_supported(dy2, x2, 1):
+    if (_main_grad_tt(M, N, K) and mg.dtype == torch.float32 and mg.dim() == 2 and tuple(mg.shape) == (N, K)
+            and mg.data_ptr() % 16 == 0 and _ext.require().gemm_tt_supported(dy2, x2, 1)):
+        # (gemm_tt_acc's 16-byte read-modify-write epilogue needs main_grad 16-byte aligned and
+        # [N, K]: an unaligned user buffer or APEX_DDP_ALIGN=0 slot takes the addmm / split-K path)
         # the transposed-read MFMA kernel with the fp32 read-modify-write epilogue: dW is added
         # into main_grad in the GEMM's own epilogue (csrc/gemm.hip EPI_F32_ACC)
         _ext.require().gemm_tt_acc(dy2, x2, mg)

@@ -107,6 +107,38 @@ class _PostScaleWork:
             self.flat.mul_(self.post)
 
 
+_MAIN_GRAD_GUARD = None
+
+
+def _install_main_grad_guard():
+    """A global optimizer step pre-hook (installed once, by the first fp32_main_grad DDP): an
+    optimizer that reads ``p.grad`` (torch.optim, or any non-apex optimizer) stepping parameters
+    whose gradients live in ``main_grad`` would silently never update them — raise instead. apex's
+    fused optimizers read main_grad; under amp O2 the optimizer holds fp32 masters (no main_grad),
+    whose grads amp fills from main_grad."""
+    global _MAIN_GRAD_GUARD
+    if _MAIN_GRAD_GUARD is not None:
+        return
+
+    def guard(opt, args, kwargs):
+        from ..optimizers._base import FusedOptimizerBase
+
+        if isinstance(opt, FusedOptimizerBase):
+            return
+        for g in opt.param_groups:
+            for p in g["params"]:
+                if p.grad is None and getattr(p, "main_grad", None) is not None:
+                    raise RuntimeError(
+                        "{} steps parameters whose gradients are in p.main_grad (apex DDP fp32_main_grad=True) "
+                        "and reads p.grad, which DDP leaves None: use an apex.optimizers fused optimizer (they "
+                        "read main_grad) or amp.initialize (O2 masters get their grads from main_grad), or "
+                        "construct DDP with fp32_main_grad=False".format(type(opt).__name__))
+
+    from torch.optim.optimizer import register_optimizer_step_pre_hook
+
+    _MAIN_GRAD_GUARD = register_optimizer_step_pre_hook(guard)
+
+
 def _group_root(group):
     """Global rank of a group's rank 0 (collective src/dst arguments are global ranks)."""
     return dist.get_global_rank(group, 0) if group is not None else 0
@@ -356,11 +388,13 @@ class DistributedDataParallel(Module):
         self.fp32_main_grad = fp32_main_grad
         self._sync_params()
         if fp32_main_grad:
-            # static layout (no first-iteration recording): main_grad must exist before the first
-            # backward so the producers can accumulate into it; reverse registration order
-            # approximates the order gradients become ready in backward
+            # main_grad must exist before the first backward so the producers can accumulate into
+            # it: a provisional layout in reverse registration order. The first backward records the
+            # order the gradients actually become ready in (as the 16-bit path does) and
+            # _end_of_backward re-lays the buffers out in that order (rank 0's order wins), so that
+            # in steady state a bucket never waits on a parameter that arrives late
             self._layout_from_order(list(reversed(range(len(self._params)))), dtype=torch.float32)
-            self._layout_ready = True
+            _install_main_grad_guard()
         self._create_hooks()
 
     # ------------------------------------------------------------ setup
@@ -411,6 +445,19 @@ class DistributedDataParallel(Module):
             yield
         finally:
             self._allreduce_enabled = old
+
+    def zero_grad_buffer(self):
+        """Zero-fill the fp32 main_grad buffers (fp32_main_grad mode; one fill per buffer)."""
+        if self.fp32_main_grad:
+            for flat in self._flat.values():
+                flat.zero_()
+
+    def zero_grad(self, set_to_none: bool = True):
+        """Module.zero_grad, plus the fp32 main_grad buffers in fp32_main_grad mode (where p.grad is
+        never used: without this, Module.zero_grad / torch.optim's zero_grad would leave main_grad
+        accumulating across steps)."""
+        super().zero_grad(set_to_none)
+        self.zero_grad_buffer()
 
     @property
     def allreduce_buffers(self):
@@ -685,6 +732,10 @@ class DistributedDataParallel(Module):
 
     # ------------------------------------------------------------ layout
     def _build_layout(self):
+        """Bucket layout in the recorded grad-ready order (the reference's first-iteration
+        recording, /root/reference/apex/parallel/distributed.py:176-203), rank 0's order broadcast
+        to every rank. In fp32_main_grad mode it replaces the provisional reverse-registration
+        layout, carrying the accumulated main_grad values over."""
         order = list(self._ready_order)
         seen = set(order)
         order += [i for i in range(len(self._params)) if i not in seen]  # never-ready params last
@@ -693,7 +744,7 @@ class DistributedDataParallel(Module):
             t = torch.tensor(order, dtype=torch.int64, device=dev if self._rccl else "cpu")
             dist.broadcast(t, _group_root(self.group), group=self.group)  # C3: rank 0's layout wins
             order = [int(x) for x in t.tolist()]
-        self._layout_from_order(order)
+        self._layout_from_order(order, dtype=torch.float32 if self.fp32_main_grad else None)
 
     def _layout_from_order(self, order, dtype=None):
         by_dtype = OrderedDict()
@@ -727,8 +778,12 @@ class DistributedDataParallel(Module):
                 else:  # e.g. channels_last conv weight: the grad view keeps the param's strides
                     v = flat[off:off + n].as_strided(p.shape, p.stride())
                 if dtype is not None:  # fp32 main_grad mode
+                    old_mg = getattr(p, "main_grad", None)
+                    if old_mg is not None:  # re-layout after the first backward: keep what accumulated
+                        v.copy_(old_mg)
                     if p.grad is not None:
-                        v.copy_(p.grad)
+                        if not p.grad._is_zerotensor():
+                            v.add_(p.grad)
                         p.grad = None
                     p.main_grad = v
                     p._apex_main_flat = flat

@@ -50,10 +50,13 @@ def chunk_ids(rank, world, layout):
 
 
 def _group_info(group):
+    """(group, size, rank in group, global ranks). ``group=None``: parallel_state's CP group when
+    parallel_state is initialised, otherwise no context parallelism (size 1) — even when
+    torch.distributed itself is initialised."""
     if group is None:
         from . import parallel_state as ps
 
-        group = ps.get_context_parallel_group()
+        group = ps.get_context_parallel_group() if ps._CONTEXT_PARALLEL_GROUP is not None else None
     if group is None:
         return None, 1, 0, [dist.get_rank() if dist.is_initialized() else 0]
     return group, dist.get_world_size(group), dist.get_rank(group), dist.get_process_group_ranks(group)
@@ -272,6 +275,9 @@ class _RingAttention(torch.autograd.Function):
             for ki, gk, gv in grads:
                 dks[ki].add_(gk)
                 dvs[ki].add_(gv)
+            if W == 1:  # no ring: the only shard is this rank's own (nothing to send to itself)
+                dkv_pending = ([], [dk_t, dv_t])
+                continue
             # travels with its K/V shard; after the last step this send brings it home
             dkv_pending = ring.start([dk_t, dv_t])
             if nxt is not None:

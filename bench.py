@@ -25,6 +25,7 @@ import argparse
 import contextlib
 import gc
 import os
+import sys
 
 import torch
 
@@ -62,7 +63,19 @@ def parse():
     ap.add_argument("--first-bucket-size", type=int, default=None)
     ap.add_argument("--ddp-fp32-allreduce", action="store_true",
                     help="reduce the bf16 gradient buckets in fp32 (A/B of the reduction precision)")
-    return ap.parse_args()
+    ap.add_argument("--cpu-rehearsal", action="store_true",
+                    help="REHEARSAL, not a measurement: the same N-rank sequence (pre-flight -> bucket probe -> "
+                         "DDP -> timed steps -> max over ranks -> one JSON line) on CPU over gloo with a tiny "
+                         "BERT, so the multi-GPU path is exercised where no GPUs are (tests/test_bench_rehearsal.py)")
+    args = ap.parse_args()
+    if args.cpu_rehearsal:
+        os.environ.setdefault("APEX_DIST_BACKEND", "gloo")
+        if "--batch" not in " ".join(sys.argv):
+            args.batch = 8
+        if "--seq" not in " ".join(sys.argv):
+            args.seq = 32
+        args.fp32_microbatch = min(args.fp32_microbatch, args.batch)
+    return args
 
 
 def build(env, cfg, fp32, message_size, fp8=False, first_bucket_size=None, fp32_allreduce=False,
@@ -112,6 +125,11 @@ def make_step(model, opt, batches, micro):
     return step
 
 
+def _sync(env):
+    if env.device.type == "cuda":
+        torch.cuda.synchronize()
+
+
 def allreduce_probe(env, numel, iters=5):
     """Bus bandwidth of one DDP-bucket-sized bf16 all-reduce on this job's communicator (the
     scaling runs' diagnostic: compare with tools/allreduce_sweep.py's curve)."""
@@ -122,11 +140,11 @@ def allreduce_probe(env, numel, iters=5):
     buf = torch.ones(numel, dtype=torch.bfloat16, device=env.device)
     for _ in range(2):
         dist.all_reduce(buf)
-    torch.cuda.synchronize()
+    _sync(env)
     t0 = time.perf_counter()
     for _ in range(iters):
         dist.all_reduce(buf)
-    torch.cuda.synchronize()
+    _sync(env)
     t = (time.perf_counter() - t0) / iters
     nbytes = numel * 2
     algbw = nbytes / t / 1e9
@@ -142,9 +160,11 @@ def main():
 
     from apex.parallel import preflight
 
-    tuned = enable_tuned_gemms()  # committed hipBLASLt/rocBLAS selections, read-only
+    rehearsal = args.cpu_rehearsal
+    tuned = enable_tuned_gemms() if not rehearsal else False  # committed hipBLASLt/rocBLAS selections
     preflight.apply_channel_cap()  # APEX_DDP_CHANNELS -> NCCL_MAX_NCHANNELS, before any communicator
-    env = init_distributed(single_rank_group=True)  # also reserves stdout for the result line
+    # (also reserves stdout for the result line)
+    env = init_distributed(single_rank_group=True, device="cpu" if rehearsal else "cuda")
     if env.world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={env.world}; using WORLD_SIZE")
     dev = env.device
@@ -152,9 +172,14 @@ def main():
     import apex
     from apex.models.bert import BertConfig, synthetic_batch
 
-    apex._ext.require()
-    cfg = BertConfig.large()
-    cfg.num_hidden_layers = args.layers
+    if rehearsal:
+        torch.set_num_threads(max(1, (os.cpu_count() or 2) // max(1, env.world)))
+        cfg = BertConfig.tiny()
+        args.layers = cfg.num_hidden_layers
+    else:
+        apex._ext.require()
+        cfg = BertConfig.large()
+        cfg.num_hidden_layers = args.layers
     world = env.world
 
     def batches_for(n):
@@ -170,7 +195,9 @@ def main():
     if world > 1:
         dist_info["preflight"] = preflight.preflight_allreduce(None, dev)
         if message_size is None:
-            probe = preflight.probe_bucket_sizes(None, dev)
+            # (rehearsal: CPU-sized candidates; the tiny model's whole gradient is ~1M elements)
+            probe = preflight.probe_bucket_sizes(None, dev, sizes=(50_000, 100_000, 200_000)) if rehearsal \
+                else preflight.probe_bucket_sizes(None, dev)
             message_size, auto_first = preflight.select_bucket_sizes(probe)
             first_bucket = first_bucket if first_bucket is not None else auto_first
             dist_info["bucket_probe"] = probe
@@ -184,24 +211,26 @@ def main():
     extra["dist"] = dist_info
     args.message_size = message_size
 
-    sampler = telemetry.GpuSampler(dev.index or 0)
-    idle = sampler.snapshot()
+    sampler = telemetry.GpuSampler(dev.index or 0) if not rehearsal else None
+    idle = sampler.snapshot() if sampler is not None else None
     if not args.fp32_only:
         model, opt = build(env, cfg, False, args.message_size, first_bucket_size=first_bucket,
                            fp32_allreduce=args.ddp_fp32_allreduce)
         batches = batches_for(args.batch)
-        timer = telemetry.StepTimer()
+        timer = telemetry.StepTimer(enabled=not rehearsal)
         elapsed, loss = time_steps(env, make_step(model, opt, batches, 0), args.steps, args.warmup,
                                    timer=timer, sampler=sampler, on_timed_start=model.reset_comm_stats)
         final_loss = float(loss.float().item())
         ms = elapsed / args.steps * 1000.0
         extra["final_loss"] = round(final_loss, 4)
-        extra["step_ms"] = timer.summary()
+        extra["step_ms"] = timer.summary() if not rehearsal else None
         extra["ddp"] = model.comm_stats()
-        extra["peak_mem_gb"] = round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1)
+        if not rehearsal:
+            extra["peak_mem_gb"] = round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1)
         del model, opt, batches, loss
         gc.collect()
-        torch.cuda.empty_cache()
+        if not rehearsal:
+            torch.cuda.empty_cache()
     if args.fp8 and not args.fp32_only:
         # per-tensor scaled fp8 forward / input-gradient GEMMs (apex.fp8): an extension beyond the
         # metric's amp O2 bf16 configuration, so it never replaces the headline value
@@ -247,7 +276,8 @@ def main():
         fp32_ms = f_el / max(1, args.fp32_steps) * 1000.0
         del model, opt, batches
         gc.collect()
-        torch.cuda.empty_cache()
+        if not rehearsal:
+            torch.cuda.empty_cache()
     if args.fp32_only:
         elapsed, ms = f_el, fp32_ms
         steps = max(1, args.fp32_steps)
@@ -259,19 +289,30 @@ def main():
             extra["fp32_seq_per_s"] = round(args.batch * world / fp32_ms * 1000.0, 2)
             extra["speedup_vs_fp32"] = round(fp32_ms / ms, 3)
             extra["fp32_config"] = f"amp O0 fp32, micro-batches of {args.fp32_microbatch} accumulated to {args.batch}"
-    extra["gpu"] = {"idle": idle, "timed": sampler.summary()}
-    tstat = telemetry.tunableop_status()
-    tstat["committed_validators_match"] = None
-    committed = telemetry.committed_validators(os.path.join(DEFAULT_DIR, "tunableop_results0.csv"))
-    if committed and tstat.get("validators"):
-        tstat["committed_validators_match"] = all(tstat["validators"].get(k) == v for k, v in committed.items())
-    extra["tunableop"] = tstat
+            from apex.contrib.multihead_attn.chunked import _block_rows
+
+            rows = _block_rows(args.fp32_microbatch, cfg.num_attention_heads, args.seq, args.seq)
+            extra["fp32_attention_path"] = (
+                f"apex.contrib.multihead_attn.chunked (fp32 torch composition on the f32 MFMA GEMMs, "
+                f"{'one block' if rows >= args.seq else f'{rows}-row query blocks'}; the MFMA flash kernels take bf16/fp16)")
+    if rehearsal:
+        extra["rehearsal"] = ("CPU/gloo rehearsal of the N-rank bench sequence with a tiny BERT "
+                              f"({cfg.num_hidden_layers}L H{cfg.hidden_size}): NOT a measurement")
+    else:
+        extra["gpu"] = {"idle": idle, "timed": sampler.summary()}
+        tstat = telemetry.tunableop_status()
+        tstat["committed_validators_match"] = None
+        committed = telemetry.committed_validators(os.path.join(DEFAULT_DIR, "tunableop_results0.csv"))
+        if committed and tstat.get("validators"):
+            tstat["committed_validators_match"] = all(tstat["validators"].get(k) == v for k, v in committed.items())
+        extra["tunableop"] = tstat
     extra["versions"] = telemetry.library_versions()
     emit(env, metric=METRIC, items_per_step=args.batch * world, unit="seq/s", steps=steps,
          warmup=args.warmup, elapsed=elapsed, baseline=BASELINE_VALUE, dtype="fp32" if args.fp32_only else "bf16",
          data="synthetic (random token ids, 15% masked positions, random NSP labels); random-init weights",
          config={
-             "model": "BERT-Large (24L, H1024, A16, FFN4096, vocab 30522)" if args.layers == 24
+             "model": f"BERT-tiny REHEARSAL ({cfg.num_hidden_layers}L, H{cfg.hidden_size}; not the metric config)"
+             if rehearsal else "BERT-Large (24L, H1024, A16, FFN4096, vocab 30522)" if args.layers == 24
              else f"BERT-Large-{args.layers}L (DEBUG, not the metric config)",
              "global_batch": args.batch * world,
              "per_gpu_batch": args.batch,

@@ -561,7 +561,7 @@ bool k_bdaln_wide_supported(int64_t cols) { return apex::bdaln_wide_supported((i
 std::vector<Tensor> k_bdaln_fwd(Tensor x, const c10::optional<Tensor>& b, Tensor res, Tensor gamma,
                                 Tensor beta, double eps, double p, int64_t seed, int64_t offset, bool store_s,
                                 const c10::optional<Tensor>& q8_out, const c10::optional<Tensor>& q8_scale,
-                                const c10::optional<Tensor>& q8_amax, int64_t q8_fmt) {
+                                const c10::optional<Tensor>& q8_amax, int64_t q8_fmt, bool s_cond) {
   TORCH_CHECK(x.is_contiguous() && res.is_contiguous() && x.sizes() == res.sizes(), "bdaln: shapes");
   const int64_t cols = cols_of(x), rows = x.numel() / std::max<int64_t>(cols, 1);
   Tensor y = at::empty_like(x), s = store_s ? at::empty_like(x) : at::empty({0}, x.options());
@@ -572,7 +572,7 @@ std::vector<Tensor> k_bdaln_fwd(Tensor x, const c10::optional<Tensor>& b, Tensor
                         y.data_ptr(), store_s ? s.data_ptr() : nullptr, mean.data_ptr<float>(), rstd.data_ptr<float>(), rows,
                         (int)cols, (float)eps, (uint64_t)seed, (uint64_t)offset, dp.first, dp.second,
                         dt_code(x.scalar_type()), dt_code(gamma.scalar_type()), cur_stream(),
-                        q8_args(q8_out, q8_scale, q8_amax, q8_fmt, y, "bdaln_fwd")),
+                        q8_args(q8_out, q8_scale, q8_amax, q8_fmt, y, "bdaln_fwd"), (store_s && s_cond) ? 1 : 0),
         "bdaln_fwd");
   return {y, s, mean, rstd};
 }
@@ -582,8 +582,10 @@ std::vector<Tensor> k_bdaln_bwd(Tensor dy, Tensor s, Tensor gamma, Tensor mean, 
                                 const c10::optional<Tensor>& dbeta_out, const c10::optional<Tensor>& dbias_out,
                                 const c10::optional<Tensor>& ds_extra, const c10::optional<Tensor>& beta,
                                 const c10::optional<Tensor>& q8_out, const c10::optional<Tensor>& q8_scale,
-                                const c10::optional<Tensor>& q8_amax, int64_t q8_fmt) {
-  // beta given: `s` is the LN output y of a store_s = false forward (x-hat = (y - beta) / gamma)
+                                const c10::optional<Tensor>& q8_amax, int64_t q8_fmt,
+                                const c10::optional<Tensor>& s_alt) {
+  // beta given: `s` is the LN output y of a store_s = false (or s_cond) forward (x-hat = (y - beta) /
+  // gamma); s_alt: the s_cond forward's conditionally stored LN input, read instead when gamma has a 0
   Tensor dyc = dy.contiguous();
   const bool from_y = beta.has_value() && beta->defined();
   if (from_y)
@@ -609,7 +611,9 @@ std::vector<Tensor> k_bdaln_bwd(Tensor dy, Tensor s, Tensor gamma, Tensor mean, 
                         dbeta.data_ptr(), has_bias ? dbias.data_ptr() : nullptr, ws.data_ptr<float>(), rows,
                         (int)cols, (uint64_t)seed, (uint64_t)offset, dp.first, dp.second,
                         dt_code(s.scalar_type()), dt_code(gamma.scalar_type()), cur_stream(),
-                        q8_args(q8_out, q8_scale, q8_amax, q8_fmt, dx, "bdaln_bwd")),
+                        q8_args(q8_out, q8_scale, q8_amax, q8_fmt, dx, "bdaln_bwd"),
+                        (from_y && s_alt.has_value() && s_alt->defined() && s_alt->numel() == s.numel())
+                            ? s_alt->data_ptr() : nullptr),
         "bdaln_bwd");
   return {dres, dx, dgamma, dbeta, dbias};
 }
@@ -1402,7 +1406,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bdaln_wide_supported", &k_bdaln_wide_supported);
   m.def("bdaln_fwd", &k_bdaln_fwd, py::arg("x"), py::arg("b"), py::arg("res"), py::arg("gamma"), py::arg("beta"),
         py::arg("eps"), py::arg("p"), py::arg("seed"), py::arg("offset"), py::arg("store_s") = true, py::arg("q8_out") = py::none(), py::arg("q8_scale") = py::none(),
-        py::arg("q8_amax") = py::none(), py::arg("q8_fmt") = 0);
+        py::arg("q8_amax") = py::none(), py::arg("q8_fmt") = 0, py::arg("s_cond") = false);
   m.def("embed_ln_fwd", &k_embed_ln_fwd);
   m.def("embed_ln_bwd", &k_embed_ln_bwd, py::arg("dy"), py::arg("s"), py::arg("gamma"), py::arg("mean"),
         py::arg("rstd"), py::arg("tids"), py::arg("tvocab"), py::arg("npos"), py::arg("p"), py::arg("seed"),
@@ -1414,7 +1418,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("p"), py::arg("seed"), py::arg("offset"), py::arg("has_bias"), py::arg("dgamma_out") = py::none(),
         py::arg("dbeta_out") = py::none(), py::arg("dbias_out") = py::none(), py::arg("ds_extra") = py::none(),
         py::arg("beta") = py::none(), py::arg("q8_out") = py::none(), py::arg("q8_scale") = py::none(),
-        py::arg("q8_amax") = py::none(), py::arg("q8_fmt") = 0);
+        py::arg("q8_amax") = py::none(), py::arg("q8_fmt") = 0, py::arg("s_alt") = py::none());
   m.def("input_normalize", &k_input_normalize);
   m.def("gemm_supported", &k_gemm_supported);
   m.def("gemm", &k_gemm, py::arg("a"), py::arg("b"), py::arg("epi") = 0, py::arg("bias") = py::none(),

@@ -198,7 +198,7 @@ __global__ void __launch_bounds__(kEwBlock) bdaln_fwd_kernel(const T* __restrict
                                                             T* __restrict__ s_out, float* __restrict__ mean,
                                                             float* __restrict__ rstd, int64_t rows, int cols,
                                                             float eps, uint64_t seed, uint64_t offset,
-                                                            uint32_t thresh, float scale, Q8Out q8) {
+                                                            uint32_t thresh, float scale, Q8Out q8, int s_cond) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) {
@@ -232,7 +232,7 @@ __global__ void __launch_bounds__(kEwBlock) bdaln_fwd_kernel(const T* __restrict
       // the LN input is stored at the activation precision and normalised from that value,
       // so backward (which reads s_out) sees exactly what forward normalised; s_out == nullptr:
       // not stored (post-LN memory-efficient mode: the backward rebuilds x-hat from y)
-      if (s_out) store_f<T, 8>(s_out + e, v[j]);
+      if (s_out && !s_cond) store_f<T, 8>(s_out + e, v[j]);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         v[j][k] = to_f(from_f<T>(v[j][k]));
@@ -263,6 +263,7 @@ __global__ void __launch_bounds__(kEwBlock) bdaln_fwd_kernel(const T* __restrict
   }
   float qs = 0.f, mx = 0.f;
   if (q8.y) qs = q8.scale[0];
+  bool gz = false;  // a gamma entry of exactly 0 (s_cond: the backward cannot rebuild x-hat from y)
 #pragma unroll
   for (int j = 0; j < VPT; ++j) {
     const int vi = j * 64 + lane;
@@ -271,7 +272,10 @@ __global__ void __launch_bounds__(kEwBlock) bdaln_fwd_kernel(const T* __restrict
       load_f<W, 8>(gamma + vi * 8, gv);
       load_f<W, 8>(beta + vi * 8, bb);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) o[k] = (v[j][k] - mu) * rs * gv[k] + bb[k];
+      for (int k = 0; k < 8; ++k) {
+        o[k] = (v[j][k] - mu) * rs * gv[k] + bb[k];
+        gz |= gv[k] == 0.f;
+      }
       store_f<T, 8>(y + row * cols + vi * 8, o);
       if (q8.y) {
         // fp8 codes of the output as stored (rounded to T first): the next GEMM's operand without
@@ -286,6 +290,17 @@ __global__ void __launch_bounds__(kEwBlock) bdaln_fwd_kernel(const T* __restrict
     }
   }
   if (q8.y) f8_block_amax(mx, q8.amax);
+  // s_cond (memory-efficient post-LN): s is stored only when gamma has a zero entry — every wave
+  // holds the whole gamma row, so the decision is the same for every row of the launch, and the
+  // backward (bdaln_bwd_kernel FROMY) makes the same test to read s instead of rebuilding x-hat.
+  // v still holds s rounded to T, i.e. exactly what the unconditional store writes.
+  if (s_out && s_cond && __any(gz)) {
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int vi = j * 64 + lane;
+      if (vi < nvec) store_f<T, 8>(s_out + row * cols + vi * 8, v[j]);
+    }
+  }
 }
 
 // part rows: [dgamma | dbeta | dbias] (3*cols floats) per block.
@@ -301,8 +316,8 @@ __global__ void __launch_bounds__(kEwBlock) bdaln_fwd_kernel(const T* __restrict
 // Q8: also write fp8 codes of dx (template flag: the runtime branch cost the plain kernel its third
 // wave per SIMD, 168 -> 170 VGPRs; the Q8 variant is held to 3 waves per SIMD explicitly — at 2 it
 // ran 210 vs 145 us at the BERT shape)
-template <typename T, typename W, int VPT, bool DROP, bool EXTRA = false, bool FROMY = false, bool Q8 = false>
-__global__ void __launch_bounds__(kEwBlock) __attribute__((amdgpu_waves_per_eu(Q8 ? 3 : 1))) bdaln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ s,
+template <typename T, typename W, int VPT, bool DROP, bool EXTRA, bool FROMY, bool Q8>
+__device__ __forceinline__ void bdaln_bwd_body(const T* __restrict__ dy, const T* __restrict__ s,
                                                             const W* __restrict__ gamma,
                                                             const W* __restrict__ beta,
                                                             const float* __restrict__ mean,
@@ -450,6 +465,46 @@ __global__ void __launch_bounds__(kEwBlock) __attribute__((amdgpu_waves_per_eu(Q
   float* out = part + (int64_t)blockIdx.x * 3 * cols;
   for (int c = threadIdx.x; c < 3 * cols; c += kEwBlock)
     out[c] = lds[c] + lds[3 * cols + c] + lds[6 * cols + c] + lds[9 * cols + c];
+}
+
+// s_alt (FROMY only): the conditionally stored LN input of an s_cond forward. A gamma entry of exactly
+// 0 makes x-hat = (y - beta) / gamma unrecoverable for its column; the forward then stored s, and
+// the launch (gamma is the same for every wave: the test agrees across the grid) runs the
+// stored-input body on it instead — exact gradients, no 0 * inf NaNs.
+template <typename T, typename W, int VPT, bool DROP, bool EXTRA = false, bool FROMY = false, bool Q8 = false>
+__global__ void __launch_bounds__(kEwBlock) __attribute__((amdgpu_waves_per_eu(Q8 ? 3 : 1))) bdaln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ s,
+                                                            const W* __restrict__ gamma,
+                                                            const W* __restrict__ beta,
+                                                            const float* __restrict__ mean,
+                                                            const float* __restrict__ rstd,
+                                                            const T* __restrict__ dse,
+                                                            T* __restrict__ dres, T* __restrict__ dx,
+                                                            float* __restrict__ part, int64_t rows, int cols,
+                                                            int rows_per_wave, uint64_t seed,
+                                                            uint64_t offset, uint32_t thresh, float scale,
+                                                            Q8Out q8, const T* __restrict__ s_alt) {
+  if constexpr (FROMY) {
+    if (s_alt) {
+      const int lane = threadIdx.x & 63, nvec = cols >> 3;
+      bool gz = false;
+#pragma unroll
+      for (int j = 0; j < VPT; ++j) {
+        if (j * 64 + lane < nvec) {
+          float gv[8];
+          load_f<W, 8>(gamma + (j * 64 + lane) * 8, gv);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) gz |= gv[k] == 0.f;
+        }
+      }
+      if (__any(gz)) {
+        bdaln_bwd_body<T, W, VPT, DROP, EXTRA, false, Q8>(dy, s_alt, gamma, nullptr, mean, rstd, dse, dres, dx, part,
+                                                           rows, cols, rows_per_wave, seed, offset, thresh, scale, q8);
+        return;
+      }
+    }
+  }
+  bdaln_bwd_body<T, W, VPT, DROP, EXTRA, FROMY, Q8>(dy, s, gamma, beta, mean, rstd, dse, dres, dx, part, rows, cols,
+                                                     rows_per_wave, seed, offset, thresh, scale, q8);
 }
 
 // Wide rows (2056..4096 cols, VPT 5..8 vectors per lane: Megatron H = 2560): the fast kernel's
@@ -986,7 +1041,8 @@ int bdaln_wide_supported(int cols) { return bdaln_wide_vpt(cols) > 0; }
 
 int bdaln_fwd(const void* x, const void* b, const void* res, const void* gamma, const void* beta, void* y,
               void* s_out, float* mean, float* rstd, int64_t rows, int cols, float eps, uint64_t seed,
-              uint64_t offset, uint32_t thresh, float scale, int xdt, int wdt, hipStream_t s, Q8Out q8) {
+              uint64_t offset, uint32_t thresh, float scale, int xdt, int wdt, hipStream_t s, Q8Out q8,
+              int s_cond) {
   if (rows == 0) return 0;
   const int vpt = bdaln_vpt(cols);
   const dim3 grid((unsigned)((rows + 3) / 4));
@@ -996,11 +1052,11 @@ int bdaln_fwd(const void* x, const void* b, const void* res, const void* gamma, 
       if (thresh)
         hipLaunchKernelGGL((bdaln_fwd_kernel<T, W, VPT, true>), grid, dim3(kEwBlock), 0, s, (const T*)x,
                            (const W*)b, (const T*)res, (const W*)gamma, (const W*)beta, (T*)y, (T*)s_out,
-                           mean, rstd, rows, cols, eps, seed, offset, thresh, scale, q8);
+                           mean, rstd, rows, cols, eps, seed, offset, thresh, scale, q8, s_cond);
       else
         hipLaunchKernelGGL((bdaln_fwd_kernel<T, W, VPT, false>), grid, dim3(kEwBlock), 0, s, (const T*)x,
                            (const W*)b, (const T*)res, (const W*)gamma, (const W*)beta, (T*)y, (T*)s_out,
-                           mean, rstd, rows, cols, eps, seed, offset, thresh, scale, q8);
+                           mean, rstd, rows, cols, eps, seed, offset, thresh, scale, q8, s_cond);
     })));
     return (int)hipGetLastError();
   }
@@ -1008,11 +1064,11 @@ int bdaln_fwd(const void* x, const void* b, const void* res, const void* gamma, 
     if (thresh)
       hipLaunchKernelGGL((bdaln_fwd_kernel<T, W, VPT, true>), grid, dim3(kEwBlock), 0, s, (const T*)x,
                          (const W*)b, (const T*)res, (const W*)gamma, (const W*)beta, (T*)y, (T*)s_out,
-                         mean, rstd, rows, cols, eps, seed, offset, thresh, scale, q8);
+                         mean, rstd, rows, cols, eps, seed, offset, thresh, scale, q8, s_cond);
     else
       hipLaunchKernelGGL((bdaln_fwd_kernel<T, W, VPT, false>), grid, dim3(kEwBlock), 0, s, (const T*)x,
                          (const W*)b, (const T*)res, (const W*)gamma, (const W*)beta, (T*)y, (T*)s_out,
-                         mean, rstd, rows, cols, eps, seed, offset, thresh, scale, q8);
+                         mean, rstd, rows, cols, eps, seed, offset, thresh, scale, q8, s_cond);
   })));
   return (int)hipGetLastError();
 }
@@ -1033,7 +1089,7 @@ int64_t bdaln_ws_floats(int64_t rows, int cols) {
 int bdaln_bwd(const void* dy, const void* s_in, const void* gamma, const void* beta, const float* mean,
               const float* rstd, const void* dse, void* dres, void* dx, void* dgamma, void* dbeta, void* dbias,
               float* ws, int64_t rows, int cols, uint64_t seed, uint64_t offset, uint32_t thresh, float scale,
-              int xdt, int wdt, hipStream_t s, Q8Out q8) {
+              int xdt, int wdt, hipStream_t s, Q8Out q8, const void* s_alt) {
   if (rows == 0) return 0;
   const int vpt = bdaln_vpt(cols);
   const int rpw = bdaln_rpw(rows);
@@ -1068,11 +1124,11 @@ int bdaln_bwd(const void* dy, const void* s_in, const void* gamma, const void* b
       if (q8.y && !E)
         hipLaunchKernelGGL((bdaln_bwd_kernel<T, W, VPT, D, false, false, true>), dim3(parts), dim3(kEwBlock), lds, s,
                            (const T*)dy, (const T*)s_in, (const W*)gamma, (const W*)nullptr, mean, rstd,
-                           (const T*)dse, (T*)dres, (T*)dx, ws, rows, cols, rpw, seed, offset, thresh, scale, q8);
+                           (const T*)dse, (T*)dres, (T*)dx, ws, rows, cols, rpw, seed, offset, thresh, scale, q8, (const T*)nullptr);
       else
         hipLaunchKernelGGL((bdaln_bwd_kernel<T, W, VPT, D, E>), dim3(parts), dim3(kEwBlock), lds, s, (const T*)dy,
                            (const T*)s_in, (const W*)gamma, (const W*)nullptr, mean, rstd, (const T*)dse, (T*)dres,
-                           (T*)dx, ws, rows, cols, rpw, seed, offset, thresh, scale, q8);
+                           (T*)dx, ws, rows, cols, rpw, seed, offset, thresh, scale, q8, (const T*)nullptr);
     };
     if (beta) {
       auto launch_y = [&](auto drop_tag) {
@@ -1081,12 +1137,12 @@ int bdaln_bwd(const void* dy, const void* s_in, const void* gamma, const void* b
           hipLaunchKernelGGL((bdaln_bwd_kernel<T, W, VPT, D, false, true, true>), dim3(parts), dim3(kEwBlock), lds,
                              s, (const T*)dy, (const T*)s_in, (const W*)gamma, (const W*)beta, mean, rstd,
                              (const T*)nullptr, (T*)dres, (T*)dx, ws, rows, cols, rpw, seed, offset, thresh, scale,
-                             q8);
+                             q8, (const T*)s_alt);
         else
           hipLaunchKernelGGL((bdaln_bwd_kernel<T, W, VPT, D, false, true>), dim3(parts), dim3(kEwBlock), lds, s,
                              (const T*)dy, (const T*)s_in, (const W*)gamma, (const W*)beta, mean, rstd,
                              (const T*)nullptr, (T*)dres, (T*)dx, ws, rows, cols, rpw, seed, offset, thresh, scale,
-                             q8);
+                             q8, (const T*)s_alt);
       };
       if (thresh) launch_y(std::true_type{});
       else launch_y(std::false_type{});

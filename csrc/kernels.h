@@ -146,7 +146,8 @@ int bdaln_wide_supported(int cols);  // 2056..4096 columns (bdaln fwd/bwd only, 
 int bdaln_fwd(const void* x, const void* b, const void* res, const void* gamma, const void* beta, void* y,
               void* s_out, float* mean, float* rstd, int64_t rows, int cols, float eps, uint64_t seed,
               uint64_t offset, uint32_t thresh, float scale, int xdt, int wdt, hipStream_t s,
-              Q8Out q8 = Q8Out{});  // q8: fp8 codes of y (narrow rows only)
+              Q8Out q8 = Q8Out{},  // q8: fp8 codes of y (narrow rows only)
+              int s_cond = 0);      // 1: s_out written only when gamma has a zero entry (post-LN mem mode)
 // BERT embeddings: s = Ww[id] + Wp[row % S] + Wt[type]; y = dropout(LN(s)); backward -> ds, dWp, dWt
 // (type vocab <= 2), dgamma, dbeta; embed_segsum: word rows from the id-sorted token list
 int embed_ln_fwd(const int* ids, const int* tids, const void* Ww, const void* Wp, const void* Wt, const void* gamma,
@@ -166,7 +167,8 @@ int bdaln_bwd(const void* dy, const void* s_in, const void* gamma, const void* b
               const float* rstd, const void* dse, void* dres, void* dx, void* dgamma, void* dbeta, void* dbias,
               float* ws, int64_t rows, int cols, uint64_t seed, uint64_t offset, uint32_t thresh, float scale,
               int xdt, int wdt, hipStream_t s,  // beta != nullptr: s_in is the LN output y (post-LN, narrow)
-              Q8Out q8 = Q8Out{});  // q8: fp8 codes of dx (narrow rows only)
+              Q8Out q8 = Q8Out{},  // q8: fp8 codes of dx (narrow rows only)
+              const void* s_alt = nullptr);  // beta given: the s of an s_cond forward (zero-gamma fallback)
 
 // ----------------------------- weight norm / RNN cells / SyncBN ------------
 int weight_norm_fwd(const void* v, const void* g, void* w, float* norms, int64_t R, int64_t C, int row_mode,

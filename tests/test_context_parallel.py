@@ -120,3 +120,24 @@ def _groups_and_dropout(rank, world):
 
 def test_context_parallel_groups_and_dropout():
     _spawn(_groups_and_dropout, 4)
+
+
+@pytest.mark.parametrize("causal", [False, True])
+def test_ring_attention_cp1_without_process_group(causal):
+    """CP size 1 with torch.distributed NOT initialised and no parallel_state: ring_attention falls
+    back to a one-rank ring (no send to itself in the backward) and matches full attention."""
+    from apex.transformer import context_parallel as cp
+
+    assert not dist.is_initialized()
+    torch.manual_seed(3)
+    q, k, v = (torch.randn(2, 16, 2, 8, dtype=torch.float64) for _ in range(3))
+    leaves = [t.clone().requires_grad_() for t in (q, k, v)]
+    ref = [t.clone().requires_grad_() for t in (q, k, v)]
+    out = cp.ring_attention(*leaves, causal=causal)
+    want = _full_attention(*ref, causal, 1.0 / 8 ** 0.5)
+    torch.testing.assert_close(out, want)
+    do = torch.randn_like(out)
+    out.backward(do)
+    want.backward(do)
+    for a, b in zip(leaves, ref):
+        torch.testing.assert_close(a.grad, b.grad)

@@ -72,3 +72,12 @@ def test_ring_attention_single_rank_is_flash():
     q, k, v = (torch.randn(2, 256, 4, 64, device="cuda", dtype=torch.bfloat16) for _ in range(3))
     out = cp._RingAttention.apply(q, k, v, None, [0], 0, True, 0.125, 0.0, "contiguous")
     torch.testing.assert_close(out, flash_attention(q, k, v, causal=True, scale=0.125), atol=0, rtol=0)
+    # backward at CP size 1 (no process group, torch.distributed not initialised): no ring send to
+    # itself; equal to the flash backward up to the fp32 accumulation of the single block
+    qa, ka, va = (t.clone().requires_grad_() for t in (q, k, v))
+    qb, kb, vb = (t.clone().requires_grad_() for t in (q, k, v))
+    do = torch.randn_like(q)
+    cp.ring_attention(qa, ka, va, causal=True, scale=0.125).backward(do)
+    flash_attention(qb, kb, vb, causal=True, scale=0.125).backward(do)
+    for a, b in ((qa, qb), (ka, kb), (va, vb)):
+        torch.testing.assert_close(a.grad.float(), b.grad.float(), atol=2e-2, rtol=2e-2)

@@ -102,7 +102,9 @@ def test_state_dict_by_parameter_name():
 def test_slot_keys_survive_id_reuse_and_recycle():
     """Slots are keyed by a counter stored on the tensor, not id(): a tensor re-created every
     step (an O1 cast) reuses the freed slot instead of growing the buffers, and a new tensor never
-    inherits a dead one's scale history."""
+    inherits a dead one's scale history. A freed slot is reusable only after the next step()
+    boundary (_recycle_slots), in sorted order, so every rank of the amax reduction group agrees
+    on slot numbers whatever order its garbage collector ran the finalizers in."""
     st = fp8.Fp8State(device="cpu")
     for step in range(50):
         w = torch.randn(4, 4)  # a fresh per-step weight copy
@@ -110,7 +112,11 @@ def test_slot_keys_survive_id_reuse_and_recycle():
         assert s in st._fresh  # new tensor: fresh (current scaling), no inherited history
         st.scale[s] = 5.0
         del w
-    assert st.n == 1  # one slot, recycled 50 times
+        w2 = torch.randn(4, 4)  # created after w died, same step: must not get w's slot yet
+        assert st.slot((st.key_of(w2), "x"), fp8.E4M3) != s
+        del w2
+        st._recycle_slots()  # the step boundary
+    assert st.n == 2  # two slots, recycled 50 times
     keep = torch.randn(4, 4)
     sk = st.slot((st.key_of(keep), "x"), fp8.E4M3)
     assert float(st.scale[sk]) == 1.0  # the recycled slot was reset

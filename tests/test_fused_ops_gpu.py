@@ -229,3 +229,39 @@ def test_bdaln_bwd_from_output_matches_stored_input(dt, cols, p):
         for a, r, name in ((got[0], rr.grad, "dres"), (got[2], gr.grad, "dgamma"), (got[3], ber.grad, "dbeta")):
             err = (a.float() - r).abs().max().item() / (r.abs().max().item() + 1e-6)
             assert err < 4 * tol, (name, err)
+
+
+@pytest.mark.parametrize("zero", [False, True])
+@pytest.mark.parametrize("cols,p", [(1024, 0.1), (512, 0.0)])
+def test_bdaln_conditional_s_zero_gamma(zero, cols, p):
+    """s_cond forward / s_alt backward (the memory-efficient post-LN default): with a gamma entry of
+    exactly 0 the forward stores s and the backward reads it (no 0 * inf NaNs, gradients equal to the
+    stored-input backward); without one, s stays unwritten and the backward rebuilds x-hat from y."""
+    C = _C()
+    dt = torch.bfloat16
+    torch.manual_seed(cols + int(zero))
+    rows = 777
+    t = torch.randn(rows, cols, device=DEV).to(dt)
+    b = torch.randn(cols, device=DEV).to(dt)
+    res = torch.randn(rows, cols, device=DEV).to(dt)
+    g = (1 + 0.2 * torch.randn(cols, device=DEV)).to(dt)
+    if zero:
+        g[5] = 0
+        g[cols - 3] = 0
+    be = (0.3 * torch.randn(cols, device=DEV)).to(dt)
+    dy = torch.randn(rows, cols, device=DEV).to(dt)
+    y, s, mean, rstd = C.bdaln_fwd(t, b, res, g, be, 1e-12, p, 11, 3)
+    sentinel = torch.full((rows, cols), 7.0, device=DEV, dtype=dt)
+    y2, s2, mean2, rstd2 = C.bdaln_fwd(t, b, res, g, be, 1e-12, p, 11, 3, s_cond=True)
+    assert torch.equal(y, y2) and torch.equal(rstd, rstd2) and s2.shape == s.shape
+    if zero:
+        assert torch.equal(s2, s)  # written because gamma has a zero
+    ref = C.bdaln_bwd(dy, s, g, mean, rstd, p, 11, 3, True)
+    got = C.bdaln_bwd(dy, y2, g, mean2, rstd2, p, 11, 3, True, beta=be, s_alt=s2 if zero else sentinel)
+    for a, r, name in zip(got, ref, ("dres", "dx", "dgamma", "dbeta", "dbias")):
+        assert torch.isfinite(a.float()).all(), name
+        if zero:
+            assert torch.equal(a, r), name  # the same stored-input body on the same s
+        else:
+            err = (a.float() - r.float()).abs().max().item() / (r.float().abs().max().item() + 1e-6)
+            assert err < 2e-2, (name, err)  # rebuilt from y (the sentinel s_alt is never read)

@@ -169,3 +169,92 @@ def test_fp32_main_grad_tied_weight_keeps_other_uses():
     for p in ps:
         p.join(timeout=30)
     assert all(r[1] == "ok" for r in res), res
+
+
+class _Crossed(torch.nn.Module):
+    """Registered a, b, c but used as a(c(b(x))): grads become ready a, c, b — not the reverse
+    registration order c, b, a the provisional main_grad layout assumes."""
+
+    def __init__(self):
+        super().__init__()
+        self.a = torch.nn.Linear(8, 8, bias=False)
+        self.b = torch.nn.Linear(8, 8, bias=False)
+        self.c = torch.nn.Linear(8, 8, bias=False)
+
+    def forward(self, x):
+        return self.a(torch.tanh(self.c(torch.tanh(self.b(x)))))
+
+
+def _order_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.set_num_threads(1)
+        from apex.parallel import DistributedDataParallel as DDP
+
+        torch.manual_seed(0)
+        net = _Crossed()
+        arrived = []
+        for name, p in net.named_parameters():  # registered before DDP's hooks: runs first
+            p.register_post_accumulate_grad_hook(lambda p, n=name.split(".")[0]: arrived.append(n))
+        model = DDP(net, message_size=64, fp32_main_grad=True)  # one 8x8 weight per bucket
+        names = {id(p): n.split(".")[0] for n, p in net.named_parameters()}
+        launches = []
+        orig = model._start_bucket
+
+        def spy(b, lane):
+            launches.append(([names[id(model._params[i])] for i in b.params], len(arrived)))
+            return orig(b, lane)
+
+        model._start_bucket = spy
+        x = torch.randn(4, 8)
+        for it in range(3):
+            arrived.clear()
+            launches.clear()
+            model.zero_grad()
+            model(x + rank).pow(2).sum().backward()
+            assert arrived == ["a", "c", "b"], arrived
+            mg = {n: p.main_grad.clone() for n, p in net.named_parameters()}
+            if it == 0:
+                # first backward: order recorded, buffers re-laid out in it, values carried over
+                layout = [[names[id(model._params[i])] for i in bk.params] for bk in model._buckets]
+                assert layout == [["a"], ["c"], ["b"]], layout
+            else:
+                # steady state: bucket k goes on the wire as soon as the k-th gradient is ready
+                assert launches == [(["a"], 1), (["c"], 2), (["b"], 3)], launches
+            # against plain fp32 autograd averaged over ranks
+            twin = _Crossed()
+            twin.load_state_dict(net.state_dict())
+            tot = {n: torch.zeros_like(p) for n, p in twin.named_parameters()}
+            for r in range(world):
+                twin.zero_grad()
+                twin(x + r).pow(2).sum().backward()
+                for n, p in twin.named_parameters():
+                    tot[n] += p.grad / world
+            for n in tot:
+                torch.testing.assert_close(mg[n], tot[n], rtol=1e-5, atol=1e-6)
+        # torch.optim reads p.grad (None in main_grad mode): the guard raises instead of a silent no-op
+        opt = torch.optim.SGD(net.parameters(), lr=0.1)
+        try:
+            opt.step()
+            raise AssertionError("torch.optim step on main_grad params did not raise")
+        except RuntimeError as e:
+            assert "main_grad" in str(e)
+        q.put((rank, "ok"))
+    except Exception:
+        q.put((rank, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_fp32_main_grad_layout_follows_grad_ready_order():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_order_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=180) for _ in ps]
+    for p in ps:
+        p.join(timeout=30)
+    assert all(r[1] == "ok" for r in res), res
