@@ -126,8 +126,21 @@ def attention_packed(qkv, attn_bias=None, dropout_p=0.0, causal=False, scale=Non
     return _fallback(q, k, v, attn_bias, dropout_p, causal, scale, k_lens)
 
 
+def _short_dense_ok(q, k, attn_bias):
+    """Training-length fp32 attention (S <= 1024, fp32 scores of at most 2 GiB, no trainable bias):
+    the dense composition — one fused softmax and one fused dropout kernel each way, probabilities
+    kept for backward — beats the query-blocked path's recomputation (~3x the elementwise passes
+    over [B, h, S, S]): the fp32 BERT-Large step (the bench's speedup denominator, micro-batch 256)
+    1741 ms blocked vs 1567 ms dense (BENCH_r02). Longer sequences keep O(S * block) memory."""
+    B, Sq, H, _ = q.shape
+    Sk = k.shape[1]
+    trainable = attn_bias is not None and attn_bias.requires_grad and torch.is_grad_enabled()
+    return Sq <= 1024 and Sk <= 1024 and B * H * Sq * Sk * 4 <= (2 << 30) and not trainable
+
+
 def _fallback(q, k, v, attn_bias, dropout_p, causal, scale, k_lens):
-    if q.is_cuda and os.environ.get("APEX_ATTN_BACKEND", "native") != "reference":
+    backend = os.environ.get("APEX_ATTN_BACKEND", "native")
+    if q.is_cuda and backend != "reference" and not (backend != "chunked" and _short_dense_ok(q, k, attn_bias)):
         from .chunked import chunked_attention
 
         return chunked_attention(q, k, v, attn_bias, dropout_p, causal, scale, k_lens)

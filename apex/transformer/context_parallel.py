@@ -28,6 +28,7 @@ Dropout (``dropout_p``) draws an independent mask per (step, block) and keeps it
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.distributed as dist
@@ -166,7 +167,18 @@ def _blk_bwd(do, q, k, v, o, lse, causal, scale, p, aux):
 
 
 def _merge(acc_o, acc_lse, o, lse):
-    """Fold one block's (o, lse) into the running fp32 (acc_o [B, S, H, D], acc_lse [B, H, S])."""
+    """Fold one block's (o, lse) into the running fp32 (acc_o [B, S, H, D], acc_lse [B, H, S]).
+
+    On the GPU one HIP pass (csrc/context_parallel.hip: reads the accumulator and the block once,
+    writes the accumulator once); the torch composition below is the CPU / reference path."""
+    if _native_merge(o, lse):
+        C = _ext.require()
+        first = acc_o is None
+        if first:
+            acc_o = torch.empty(o.shape, dtype=torch.float32, device=o.device)
+            acc_lse = torch.empty(lse.shape, dtype=torch.float32, device=o.device)
+        C.lse_merge(acc_o, acc_lse, o, lse.contiguous(), first)
+        return acc_o, acc_lse
     lse = torch.where(torch.isposinf(lse), torch.full_like(lse, float("-inf")), lse)  # empty rows
     if acc_o is None:
         return _f(o), lse.clone()
@@ -175,6 +187,23 @@ def _merge(acc_o, acc_lse, o, lse):
     w_old = torch.exp(acc_lse - safe).transpose(1, 2).unsqueeze(-1)
     w_new = torch.exp(lse - safe).transpose(1, 2).unsqueeze(-1)
     return acc_o * w_old + _f(o) * w_new, new
+
+
+def _native_merge(o, lse):
+    if not (o.is_cuda and o.dtype in (torch.bfloat16, torch.float16, torch.float32) and o.dim() == 4
+            and o.is_contiguous() and o.shape[-1] % 8 == 0 and o.shape[-1] <= 256 and lse.dtype == torch.float32):
+        return False
+    C = _ext._load()
+    return C is not None and hasattr(C, "lse_merge")
+
+
+def _dkv_transport_dtype(k):
+    """dtype of the dK/dV partials travelling the ring: the input dtype for 16-bit inputs (each hop
+    adds its contribution in fp32 and rounds once: half the P2P bytes of an fp32 partial), fp32 /
+    fp64 accumulation for wider inputs. APEX_CP_DKV_FP32=1 keeps 16-bit inputs' partials in fp32."""
+    if k.dtype in (torch.bfloat16, torch.float16) and os.environ.get("APEX_CP_DKV_FP32", "0") != "1":
+        return k.dtype
+    return _acc_dtype(k)
 
 
 def _pairs(q_ids, k_ids, causal):
@@ -267,8 +296,8 @@ class _RingAttention(torch.autograd.Function):
                 grads.append((ki, g[1], g[2]))
             # the shard's dK/dV partial from the previous ranks (zero at step 0) + this rank's blocks
             if dkv_pending is None:
-                dk_t = torch.zeros(k.shape, dtype=_acc_dtype(k), device=k.device)
-                dv_t = torch.zeros(v.shape, dtype=_acc_dtype(v), device=v.device)
+                dk_t = torch.zeros(k.shape, dtype=_dkv_transport_dtype(k), device=k.device)
+                dv_t = torch.zeros(v.shape, dtype=_dkv_transport_dtype(v), device=v.device)
             else:
                 dk_t, dv_t = _Ring.finish(dkv_pending)
             dks, dvs = dk_t.chunk(len(k_ids), dim=1), dv_t.chunk(len(k_ids), dim=1)

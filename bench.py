@@ -289,12 +289,15 @@ def main():
             extra["fp32_seq_per_s"] = round(args.batch * world / fp32_ms * 1000.0, 2)
             extra["speedup_vs_fp32"] = round(fp32_ms / ms, 3)
             extra["fp32_config"] = f"amp O0 fp32, micro-batches of {args.fp32_microbatch} accumulated to {args.batch}"
-            from apex.contrib.multihead_attn.chunked import _block_rows
+            from apex.contrib.multihead_attn import attention as _att
 
-            rows = _block_rows(args.fp32_microbatch, cfg.num_attention_heads, args.seq, args.seq)
+            q = torch.empty(args.fp32_microbatch, args.seq, cfg.num_attention_heads, 1, device="meta")
             extra["fp32_attention_path"] = (
-                f"apex.contrib.multihead_attn.chunked (fp32 torch composition on the f32 MFMA GEMMs, "
-                f"{'one block' if rows >= args.seq else f'{rows}-row query blocks'}; the MFMA flash kernels take bf16/fp16)")
+                "dense fp32 composition (fused softmax / dropout kernels, f32 MFMA GEMMs; "
+                "apex.contrib.multihead_attn.attention._fallback)" if _att._short_dense_ok(q, q, None) else
+                "query-blocked fp32 composition (apex.contrib.multihead_attn.chunked)") + \
+                "; the MFMA flash kernels take bf16/fp16 (round 3 sent this step through 16-row query " \
+                "blocks: 2458 ms, which inflated its speedup_vs_fp32)"
     if rehearsal:
         extra["rehearsal"] = ("CPU/gloo rehearsal of the N-rank bench sequence with a tiny BERT "
                               f"({cfg.num_hidden_layers}L H{cfg.hidden_size}): NOT a measurement")

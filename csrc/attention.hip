@@ -14,8 +14,7 @@ __global__ void attn_dropout_mask_kernel(uint8_t* out, int64_t BH, int Sq, int S
   const int64_t blk = idx % nblk, row = idx / nblk;
   const int q = (int)(row % Sq);
   const int64_t bh = row / Sq;
-  DropGen dg{seed, offset, thresh};
-  const uint32_t w = dg.block_bits(bh, q, blk, Sq);
+  const uint32_t w = drop_block_bits(seed, offset, thresh, bh, q, blk, Sq);
   for (int k = 0; k < 32; ++k) {
     const int64_t key = blk * 32 + k;
     if (key < Sk) out[row * Sk + key] = (w >> k) & 1;

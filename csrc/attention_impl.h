@@ -134,36 +134,68 @@ __device__ __forceinline__ V8 pack8(const float* x) {
   return __builtin_bit_cast(V8, r);
 }
 
-// Attention dropout keep bits: 8-bit uniforms (keep iff u8 >= thresh), 16 per Philox4x32-7
-// call. One call per (row, 16-key half of a 32-key block); the four 32-bit outputs are compared
-// against the threshold four bytes at a time (SWAR: the carry out of u + (256 - thresh) in each
-// byte is the keep bit — u & 0x7f.. plus the low 7 bits of the addend, then the majority of the
-// three top bits), and the carries are shifted into the natural bit order: the returned 16 bits
-// land at positions 4 hl + {0..3, 8..11, 16..19, 24..27}, i.e. bit k of the OR of both halves is
-// key k of the block (random word j = k & 3 of half hl = (k >> 2) & 1, byte k >> 3).
-struct DropGen {
-  uint64_t seed, offset;
-  uint32_t thresh;
-  __device__ __forceinline__ uint32_t half_bits(int64_t bh, int64_t row, int64_t blk, int hl, int64_t Sq) const {
-    Philox ph(seed, (uint64_t)(bh * Sq + row), offset + (uint64_t)(2 * blk + hl));
+// Attention dropout keep bits: 8-bit uniforms (keep iff u8 >= thresh), 16 per (row, 16-key half of a
+// 32-key block). Each (row, half) is one stream: ONE Philox4x32-7 call (counter offset + hl,
+// subsequence bh * Sq + row) seeds a xorshift128 state, and every 32-key block then takes the
+// stream's next four 32-bit words, in block order. Round 3 drew one Philox call per block and half:
+// its 14 64-bit integer multiplies (quarter-rate v_mad_u64_u32) per call were ~30 % of the BERT-shape
+// forward (fwd 72.7 us with p = 0.1 vs 56.1 at p = 0, b256 s128, tools/attn_bench.py); a xorshift128
+// step is six full-rate shift/xor ops. Dropout masks need uniform, uncorrelated bytes, not
+// cryptographic strength; the Philox seeding keeps streams of different rows / heads / launches
+// independent, and tests/test_attention_gpu.py checks the keep rate and the mask's decorrelation.
+// The four words are compared against the threshold four bytes at a time (SWAR: the carry out of
+// u + (256 - thresh) in each byte is the keep bit — u & 0x7f.. plus the low 7 bits of the addend,
+// then the majority of the three top bits), and the carries are shifted into the natural bit order:
+// the returned 16 bits land at positions 4 hl + {0..3, 8..11, 16..19, 24..27}, i.e. bit k of the OR
+// of both halves is key k of the block (random word j = k & 3 of half hl = (k >> 2) & 1, byte k >> 3).
+struct DropStream {
+  uint32_t x, y, z, w, thresh;
+  __device__ __forceinline__ DropStream(uint64_t seed, uint64_t offset, uint32_t thr, int64_t bh, int64_t row,
+                                        int hl, int64_t Sq) {
+    Philox ph(seed, (uint64_t)(bh * Sq + row), offset + (uint64_t)hl);
     const uint4 r = ph.next();
+    x = r.x;
+    y = r.y;
+    z = r.z;
+    w = r.w | (uint32_t)((r.x | r.y | r.z | r.w) == 0u);  // xorshift128's state must not be all zero
+    thresh = thr;
+  }
+  __device__ __forceinline__ uint32_t next() {
+    const uint32_t t = x ^ (x << 11);
+    x = y;
+    y = z;
+    z = w;
+    w = w ^ (w >> 19) ^ t ^ (t >> 8);
+    return w;
+  }
+  // the next block's 16 keep bits of this half (bits 4 hl + {0-3, 8-11, 16-19, 24-27})
+  __device__ __forceinline__ uint32_t half_bits(int hl) {
     const uint32_t C = (256u - thresh) * 0x01010101u;
     const uint32_t C7 = C & 0x7f7f7f7fu;
-    const uint32_t w[4] = {r.x, r.y, r.z, r.w};
     uint32_t out = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const uint32_t u = w[j];
+      const uint32_t u = next();
       const uint32_t s7 = (u & 0x7f7f7f7fu) + C7;
       const uint32_t carry = ((u & C) | ((u | C) & s7)) & 0x80808080u;  // bit 8b+7: keep of byte b
       out |= carry >> (7 - j);                                           // -> bit 8b + j
     }
     return out << (4 * hl);
   }
-  __device__ __forceinline__ uint32_t block_bits(int64_t bh, int64_t row, int64_t blk, int64_t Sq) const {
-    return half_bits(bh, row, blk, 0, Sq) | half_bits(bh, row, blk, 1, Sq);
-  }
 };
+
+// keep bits of block `blk` (bit k <-> key 32 blk + k) for one row, both halves (debug / test kernel)
+__device__ __forceinline__ uint32_t drop_block_bits(uint64_t seed, uint64_t offset, uint32_t thresh, int64_t bh,
+                                                    int64_t row, int64_t blk, int64_t Sq) {
+  uint32_t out = 0;
+  for (int hl = 0; hl < 2; ++hl) {
+    DropStream st(seed, offset, thresh, bh, row, hl, Sq);
+    uint32_t hb = 0;
+    for (int64_t b = 0; b <= blk; ++b) hb = st.half_bits(hl);
+    out |= hb;
+  }
+  return out;
+}
 
 // Additive score bias for this lane's query row and 4 consecutive keys key .. key+3 (8-byte load
 // when all four are inside the row; keys >= Sk read 0 — they are masked anyway).
@@ -198,7 +230,7 @@ constexpr int kFwdKB = 64;              // keys per tile
 // (cdna_hip_programming.md T14 "async-STAGE split"); the single-buffer loop pays two barriers per
 // tile (previous tile consumed / this tile staged).
 template <typename T, int D, bool CAUSAL, bool DROPOUT, bool SHORT, bool BIAS, bool DB = false>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SHORT ? 4 : (D > 128 ? 1 : (DB && D <= 64 && !DROPOUT ? 3 : 2)))))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SHORT ? (DROPOUT ? 3 : 4) : (D > 128 ? 1 : (DB && D <= 64 && !DROPOUT ? 3 : 2)))))
 attn_fwd_kernel(AttnArgs a) {
   static_assert(!SHORT || D == 64, "SHORT is the D = 64 single-pass variant");
   static_assert(!(SHORT && DB), "SHORT stages the whole key range once");
@@ -257,11 +289,11 @@ attn_fwd_kernel(AttnArgs a) {
   };
   KV kva, kvb;
   // dropout: each lane draws the keep bits of its own 16 keys of every 32-key block in the
-  // loop (one Philox call per block, DropGen::half_bits), and the two lane halves' words are
-  // combined and stored for the backward kernels
+  // loop, in block order, from its (row, half) stream (DropStream::half_bits), and the two lane
+  // halves' words are combined and stored for the backward kernels
   uint32_t* mrow =
       DROPOUT && qrow < a.Sq ? (uint32_t*)(a.dmask + ((int64_t)bh * a.Sq + qrow) * a.mask_words) : nullptr;
-  const DropGen dg{a.seed, a.offset, a.drop_thresh};
+  DropStream dg(a.seed, a.offset, DROPOUT ? a.drop_thresh : 0u, bh, qrow, hl, a.Sq);
   auto gload = [&](KV& R, int kt) {
     uint4 (&kreg)[CH] = R.k;
     uint4 (&vreg)[CH] = R.v;
@@ -301,7 +333,7 @@ attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
       for (int sb = 0; sb < 2; ++sb) {
         const int blk = (kt * kFwdKB >> 5) + sb;
-        const uint32_t hb = dg.half_bits(bh, qrow, blk, hl, a.Sq);  // bits at 4 hl + {0-3, 8-11, ..}
+        const uint32_t hb = dg.half_bits(hl);  // block blk's bits at 4 hl + {0-3, 8-11, ..}
         const uint32_t word = hb | xor32_u(hb);
         if (hl == 0 && mrow && blk * 32 < a.Sk) mrow[blk] = word;
         mcur[sb] = hb >> (4 * hl);
@@ -534,13 +566,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
   using V8 = typename M::V8;
   constexpr int LDR = D + 8;          // dK / dV emit staging in lds_k (row reads)
   constexpr int LDQ = ld_both<D>();  // Q / dO: row and transposed reads
-  constexpr int LDS_S = kBwdBK + 8;  // dS row stride (elements)
+  // dS^T [key][q] (bf16): each lane writes its 16 query values of one key as 4 x ds_write_b64 (4
+  // consecutive queries each; row stride 36 elements = 18 dwords: the 16 rows of a lane group land
+  // on distinct bank pairs), the dQ product reads it back with ds_read_b64_tr_b16. Round 3 wrote
+  // [q][key] with 16 ds_write_b16 per lane and step.
+  constexpr int LDT = kBwdBQ + 4;
   constexpr int KT_LD = kBwdBK + 8;  // K^T row stride (elements); K^T shares lds_k
   constexpr int LDSK = D * KT_LD > kBwdBK * LDR ? D * KT_LD : kBwdBK * LDR;
   __shared__ __attribute__((aligned(16))) T lds_q[kBwdBQ * LDQ];
   __shared__ __attribute__((aligned(16))) T lds_do[kBwdBQ * LDQ];
   __shared__ __attribute__((aligned(16))) T lds_k[LDSK];
-  __shared__ __attribute__((aligned(16))) T lds_ds[kBwdBQ * LDS_S];
+  __shared__ __attribute__((aligned(16))) T lds_ds[kBwdBK * LDT];
   __shared__ __attribute__((aligned(16))) float lds_lse[kBwdBQ], lds_delta[kBwdBQ];
   __shared__ __attribute__((aligned(16))) uint32_t lds_mask[4 * kBwdBQ];  // [wave's 32-key block][q]: bit k <-> key 32 wid + k
 
@@ -744,11 +780,24 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
       constexpr bool BOUND = decltype(bound_tag)::value;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
+        // this lane's 4 query rows 8g + 4hl + e of lse / delta / dropout words: one 16-byte LDS read
+        // each (round 3 read them as 48 scalar ds_read_b32 per step at D <= 64)
+        f32x4 lg4, dg4;
+        u32x4 mg4;
+        if constexpr (VROWS) {
+          lg4 = lse4[g];
+          dg4 = del4[g];
+          if constexpr (DROPOUT) mg4 = msk4[g];
+        } else {
+          lg4 = *(const f32x4*)(lds_lse + 8 * g + 4 * hl);
+          dg4 = *(const f32x4*)(lds_delta + 8 * g + 4 * hl);
+          if constexpr (DROPOUT) mg4 = *(const u32x4*)(lds_mask + wid * kBwdBQ + 8 * g + 4 * hl);
+        }
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int i = 4 * g + e;
           const int qi = 8 * g + 4 * hl + e;
-          float lterm = -(VROWS ? lse4[g][e] : lds_lse[qi]);
+          float lterm = -lg4[e];
           if constexpr (BIAS) {
             const int q = qb + qi;
             if (q < nq && mykey < Sk) lterm = fmaf(to_f(bcol[(int64_t)q * a.bias_qs]), kLog2e, lterm);
@@ -762,12 +811,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
           float dpv = dpacc[i];
           float pk = p;
           if constexpr (DROPOUT) {
-            const int m = __builtin_amdgcn_sbfe((int)(VROWS ? msk4[g][e] : lds_mask[wid * kBwdBQ + qi]), r, 1);
+            const int m = __builtin_amdgcn_sbfe((int)mg4[e], r, 1);
             pk = __builtin_bit_cast(float, __builtin_bit_cast(int, p) & m);
             dpv = __builtin_bit_cast(float, __builtin_bit_cast(int, dpv) & m);
           }
           pd[i] = pk;
-          ds[i] = p * fmaf(dpv, rkeep, -(VROWS ? del4[g][e] : lds_delta[qi]));
+          ds[i] = p * fmaf(dpv, rkeep, -dg4[e]);
         }
       }
     };
@@ -794,9 +843,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
     if constexpr (DQ) {
     // dS to LDS as [q][key] (bf16) for dQ = dS . K
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int qi = (i & 3) + 8 * (i >> 2) + 4 * hl;
-      lds_ds[qi * LDS_S + 32 * wid + r] = (T)ds[i];
+    for (int g4 = 0; g4 < 4; ++g4) {
+      typedef T t4 __attribute__((ext_vector_type(4)));
+      t4 w;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) w[e] = (T)ds[4 * g4 + e];  // queries 8 g4 + 4 hl + e
+      *(t4*)(lds_ds + (32 * wid + r) * LDT + 8 * g4 + 4 * hl) = w;
     }
     lds_barrier();
     // dQ^T [D x 32 q] = K^T . dS^T on 16x16x32 MFMAs over the full 128-key contraction: wave
@@ -812,7 +864,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
       for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kk = 0; kk < kBwdBK; kk += 32) {
-        const V8 bb = *(const V8*)(lds_ds + (16 * qt + lq) * LDS_S + kk + 8 * lg);
+        // B = dS [8 keys x 16 queries]: two transposed 4-key blocks of dS^T (lane 4q'+p of the
+        // group addresses key row kk + 8 lg + q', queries 16 qt + 4p; lane lq receives query 16 qt + lq)
+        const T* tb = lds_ds + (kk + 8 * lg + ((lane & 15) >> 2)) * LDT + 16 * qt + 4 * (lane & 3);
+        const V8 bb = join4<V8>(lds_tr16(tb), lds_tr16(tb + 4 * LDT));
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
           const V8 aa = *(const V8*)(lds_k + ((dt0 + t) * 16 + lq) * KT_LD + kk + 8 * lg);
@@ -868,19 +923,30 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
       if (lq < 4) atomicAdd(dsum + (dt0 + t) * 16 + 4 * lg + lq, x);
     }
   }
-  // dK then dV staged through LDS ([key][D] rows in lds_k) so the global stores are 16-byte
-  // row chunks (4 per thread at D = 64) instead of 2-byte column scatters (32 per lane)
+  // dK then dV staged through LDS so the global stores are 16-byte row chunks. The staging image is
+  // [D][keys] (row stride 132 elements = 66 dwords: the 16 rows of a lane group's ds_write_b64 land
+  // on distinct bank pairs): each lane writes 4 consecutive keys of one dim per 8-byte store (8 per
+  // tensor instead of round 3's 32 ds_write_b16 into a [key][D] image), and the store loop reads
+  // 8 dims of one key with two ds_read_b64_tr_b16 (every lane active: the tr read gathers across
+  // lanes).
   lds_barrier();  // every wave is done reading lds_k (dQ products)
+  constexpr int LDE = kBwdBK + 4;
+  static_assert(D * LDE <= LDSK, "dK/dV staging fits lds_k");
   auto emit = [&](const f32x16 (&acc)[D / 32], const float mul, T* dst, const int64_t ss, float* dsum_t) {
+    typedef T t4 __attribute__((ext_vector_type(4)));
 #pragma unroll
     for (int db = 0; db < D / 32; ++db) {
       float sum = 0.f;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int kl = 32 * wid + (i & 3) + 8 * (i >> 2) + 4 * hl;
-        const T v = (T)(acc[db][i] * mul);
-        lds_k[kl * LDR + 32 * db + r] = v;
-        if constexpr (DSUM) sum += (k0 + kl < a.Sk) ? (float)v : 0.f;
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int kl0 = 32 * wid + 8 * g4 + 4 * hl;  // keys kl0 .. kl0 + 3
+        t4 w;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          w[e] = (T)(acc[db][4 * g4 + e] * mul);
+          if constexpr (DSUM) sum += (k0 + kl0 + e < a.Sk) ? (float)w[e] : 0.f;
+        }
+        *(t4*)(lds_k + (32 * db + r) * LDE + kl0) = w;
       }
       if constexpr (DSUM) {
         sum += xor32_f(sum);
@@ -888,9 +954,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
       }
     }
     lds_barrier();
-    for (int idx = threadIdx.x; idx < kBwdBK * (D / 8); idx += 256) {
-      const int row = idx / (D / 8), col = (idx % (D / 8)) * 8;
-      if (k0 + row < a.Sk) *(uint4*)(dst + (int64_t)(k0 + row) * ss + col) = *(const uint4*)(lds_k + row * LDR + col);
+    // 16-lane group tasks: (8-dim block, 16-key block); a wave's 4 groups take 4 consecutive dim
+    // blocks of the same keys (64 contiguous bytes of each key row per store instruction)
+    constexpr int NDB = D / 8, NTASK = NDB * (kBwdBK / 16);
+    static_assert(NTASK % 16 == 0, "tasks per workgroup");
+#pragma unroll
+    for (int it = 0; it < NTASK / 16; ++it) {
+      const int t = it * 16 + wid * 4 + (lane >> 4);
+      const int d0 = (t % NDB) * 8, kb = (t / NDB) * 16;
+      const T* src = lds_k + (d0 + ((lane & 15) >> 2)) * LDE + kb + 4 * (lane & 3);
+      const s16x4 lo = lds_tr16(src), hi = lds_tr16(src + 4 * LDE);
+      const int key = k0 + kb + (lane & 15);
+      if (key < a.Sk) *(V8*)(dst + (int64_t)key * ss + d0) = join4<V8>(lo, hi);
     }
     lds_barrier();
   };
@@ -1147,6 +1222,24 @@ inline bool attn_fwd_db() {
   return on;
 }
 
+// Dropout variants now that the keep bits are cheap (DropStream): the single-pass SHORT kernel
+// (Sk <= 128) with dropout is the default (BERT-Large b768 s128 p = 0.1 forward 262-264 -> 253 us,
+// profiles/r4_attn_stream_ab.jsonl; APEX_ATTN_FWD_SHORT_DROP=0 restores the two-barrier loop); the
+// double-buffered loop with dropout stays off (GPT-2 s1024 p = 0.1 forward 87 -> 96 us;
+// APEX_ATTN_FWD_DB_DROP=1 turns it on)
+inline bool attn_env_on(const char* name, bool dflt) {
+  const char* e = getenv(name);
+  return e ? e[0] != '0' : dflt;
+}
+inline bool attn_fwd_short_drop() {
+  static const bool on = attn_env_on("APEX_ATTN_FWD_SHORT_DROP", true);
+  return on;
+}
+inline bool attn_fwd_db_drop() {
+  static const bool on = attn_env_on("APEX_ATTN_FWD_DB_DROP", false);
+  return on;
+}
+
 template <int D>
 int attn_fwd_impl(const AttnArgs& a, int dt, hipStream_t s) {
   // grid (B*H, query blocks), dispatched x-fastest: every head's block of one query range goes out
@@ -1160,9 +1253,9 @@ int attn_fwd_impl(const AttnArgs& a, int dt, hipStream_t s) {
   // Re-measured with the dropout variant at 128 VGPRs / 4 workgroups per CU (round 2): 75.3-76.5
   // vs 74.0-75.7 us — the same; p = 0 at 56 us is within ~10 % of its HBM floor (276 MB moved).
   if constexpr (D == 64) {
-    if (a.Sk <= 2 * kFwdKB && !drop && !a.bias) {
-      ATTN_DISPATCH(dt, T, ATTN_DISPATCH_B(a.causal, C,
-          hipLaunchKernelGGL((attn_fwd_kernel<T, 64, C, false, true, false>), grid, dim3(256), 0, s, a)));
+    if (a.Sk <= 2 * kFwdKB && (!drop || attn_fwd_short_drop()) && !a.bias) {
+      ATTN_DISPATCH(dt, T, ATTN_DISPATCH_B(a.causal, C, ATTN_DISPATCH_B(drop, DR,
+          hipLaunchKernelGGL((attn_fwd_kernel<T, 64, C, DR, true, false>), grid, dim3(256), 0, s, a))));
       return (int)hipGetLastError();
     }
   }
@@ -1170,7 +1263,7 @@ int attn_fwd_impl(const AttnArgs& a, int dt, hipStream_t s) {
   // (Megatron s2048 d128: 213 -> 195 us p = 0, 279 -> 269 p = 0.1) and D = 64 without dropout at 3
   // waves/SIMD (GPT-2 s1024: 104 -> 90 us); D = 64 with dropout keeps the two-barrier loop (the
   // Philox temporaries spill at 168 VGPRs: 145 -> 187 us, and at 2 waves/SIMD DB is 3 % slower)
-  if (attn_fwd_db() && a.Sk > 2 * kFwdKB && (D >= 128 || (D == 64 && !drop))) {
+  if (attn_fwd_db() && a.Sk > 2 * kFwdKB && (D >= 128 || (D == 64 && (!drop || attn_fwd_db_drop())))) {
     ATTN_DISPATCH(dt, T, ATTN_DISPATCH_B(a.causal, C, ATTN_DISPATCH_B(drop, DR, ATTN_DISPATCH_B(a.bias != nullptr, BI,
         hipLaunchKernelGGL((attn_fwd_kernel<T, D, C, DR, false, BI, true>), grid, dim3(256), 0, s, a)))));
     return (int)hipGetLastError();

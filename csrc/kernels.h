@@ -113,6 +113,10 @@ bool attn_bwd_split();
 // delta_ws: [B*H*Sq] fp32 workspace when attn_bwd_needs_dq_acc (two-kernel backward)
 int attn_bwd(const AttnArgs& a, const void* dout, float* delta_ws, void* dk, void* dv, int dt,
              hipStream_t s);
+// context parallelism: acc (fp32 [B,S,H,D] + lse [B,H,S]) <- exact log-sum-exp merge with one block's
+// (o [B,S,H,D] in dt, lse [B,H,S]); first = 1 initialises the accumulator from the block
+int lse_merge(float* acc_o, float* acc_lse, const void* o, const float* lse, int64_t B, int S, int H, int D,
+              int first, int dt, hipStream_t s);
 int attn_dropout_mask(uint8_t* out, int64_t BH, int Sq, int Sk, uint64_t seed, uint64_t offset,
                       uint32_t thresh, hipStream_t s);
 

@@ -168,25 +168,68 @@ def _philox4x32_7(seed, subseq, offset):
     return c
 
 
+def _xorshift128_words(state, n):
+    x, y, z, w = state
+    out = []
+    for _ in range(n):
+        t = (x ^ (x << 11)) & _M32
+        x, y, z = y, z, w
+        w = (w ^ (w >> 19) ^ t ^ (t >> 8)) & _M32
+        out.append(w)
+    return out
+
+
 def _keep_bits_python(seed, offset, bh, row, Sq, Sk, thresh):
-    """Keep flag of every key of one attention row, the kernels' documented mapping: per 32-key
-    block, 16 keys per Philox call (half hl = bit 2 of the key), key k <-> byte k >> 3 of word
-    k & 3, kept iff that byte >= thresh."""
+    """Keep flag of every key of one attention row, the kernels' documented mapping: one stream per
+    (row, half hl = bit 2 of the key) — a Philox4x32-7 call (counter offset + hl, subsequence
+    bh * Sq + row) seeds xorshift128, each 32-key block takes the next 4 words — key k <-> byte k >> 3
+    of word k & 3 of its half's block words, kept iff that byte >= thresh."""
+    nblk = (Sk + 31) // 32
+    streams = []
+    for hl in (0, 1):
+        st = _philox4x32_7(seed, bh * Sq + row, offset + hl)
+        if not any(st):
+            st[3] = 1
+        streams.append(_xorshift128_words(st, 4 * nblk))
     keep = []
-    for blk in range((Sk + 31) // 32):
-        words = [_philox4x32_7(seed, bh * Sq + row, offset + 2 * blk + hl) for hl in (0, 1)]
+    for blk in range(nblk):
         for k in range(32):
             key = 32 * blk + k
             if key >= Sk:
                 break
-            w = words[(k >> 2) & 1][k & 3]
+            w = streams[(k >> 2) & 1][4 * blk + (k & 3)]
             byte = (w >> (8 * (k >> 3))) & 0xFF
             keep.append(1 if byte >= thresh else 0)
     return keep
 
 
+def test_dropout_mask_statistics():
+    """The keep mask over a large [B*H, S, S] draw: keep rate at 1 - thresh/256 per key position and
+    per row, and no correlation between neighbouring keys, neighbouring rows or the two halves of a
+    block (each |corr| well below 1e-2 over ~10^7 pairs)."""
+    import apex._ext as e
+
+    C = e.require()
+    B, H, S, p = 8, 16, 256, 0.1
+    mask = C.flash_dropout_mask(B, H, S, S, p, 0xABCDEF, 0x1234, torch.device(DEV)).float().view(B * H, S, S)
+    thresh = min(255, max(1, int(p * 256 + 0.5)))
+    want = 1 - thresh / 256
+    assert abs(float(mask.mean()) - want) < 2e-3
+    assert float((mask.mean(dim=(0, 1)) - want).abs().max()) < 0.02  # every key position
+    assert float((mask.mean(dim=2) - want).abs().max()) < 0.12  # every row (256 draws)
+    z = mask - mask.mean()
+
+    def corr(a, b):
+        return float((a * b).mean() / (a.std() * b.std()))
+
+    for a, b, what in ((z[..., 1:], z[..., :-1], "keys"), (z[:, 1:], z[:, :-1], "rows"),
+                       (z[..., 4:], z[..., :-4], "halves"), (z[..., 32:], z[..., :-32], "blocks")):
+        c = corr(a, b)
+        assert abs(c) < 1e-2, (what, c)
+
+
 @pytest.mark.parametrize("p", [0.1, 0.5])
-def test_dropout_bits_match_python_philox(p):
+def test_dropout_bits_match_python_stream(p):
     import apex._ext as e
 
     C = e.require()

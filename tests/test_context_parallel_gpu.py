@@ -81,3 +81,40 @@ def test_ring_attention_single_rank_is_flash():
     flash_attention(qb, kb, vb, causal=True, scale=0.125).backward(do)
     for a, b in ((qa, qb), (ka, kb), (va, vb)):
         torch.testing.assert_close(a.grad.float(), b.grad.float(), atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_lse_merge_kernel_matches_torch_merge(dt):
+    """The fused HIP log-sum-exp merge (csrc/context_parallel.hip) against the torch composition,
+    including rows with no visible key (+inf lse) on either side and the first-block initialisation."""
+    import apex._ext as e
+    from apex.transformer import context_parallel as cp
+
+    C = e.require()
+    torch.manual_seed(2)
+    B, S, H, D = 2, 96, 3, 64
+    blocks = []
+    for j in range(3):
+        o = torch.randn(B, S, H, D, device="cuda").to(dt)
+        lse = torch.randn(B, H, S, device="cuda") * 3
+        lse[0, 1, j * 7:(j * 7) + 5] = float("inf")  # empty rows in this block
+        lse[1, 2, 40:45] = float("inf")  # empty in every block
+        blocks.append((o, lse))
+    acc_o = acc_l = None
+    ref_o = ref_l = None
+    for o, lse in blocks:
+        acc_o, acc_l = cp._merge(acc_o, acc_l, o, lse)  # native path on the GPU
+        # torch reference path
+        l2 = torch.where(torch.isposinf(lse), torch.full_like(lse, float("-inf")), lse)
+        if ref_o is None:
+            ref_o, ref_l = o.float(), l2.clone()
+        else:
+            new = torch.logaddexp(ref_l, l2)
+            safe = torch.where(torch.isneginf(new), torch.zeros_like(new), new)
+            ref_o = ref_o * torch.exp(ref_l - safe).transpose(1, 2).unsqueeze(-1) + \
+                o.float() * torch.exp(l2 - safe).transpose(1, 2).unsqueeze(-1)
+            ref_l = new
+    assert cp._native_merge(blocks[0][0], blocks[0][1])
+    torch.testing.assert_close(acc_l, ref_l, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(acc_o, ref_o, rtol=1e-5, atol=1e-5)
+    assert torch.isneginf(acc_l[1, 2, 40:45]).all() and (acc_o[1, 40:45, 2] == 0).all()

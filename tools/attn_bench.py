@@ -18,6 +18,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 SHAPES = {
     "bert": dict(B=256, S=128, H=16, D=64, causal=False),
+    "bert768": dict(B=768, S=128, H=16, D=64, causal=False),
     "gpt2": dict(B=8, S=1024, H=25, D=64, causal=True),
     "megatron": dict(B=4, S=2048, H=20, D=128, causal=True),
 }

@@ -1,0 +1,108 @@
+"""Single-GPU emulation of context-parallel ring attention's compute (apex.transformer.context_parallel):
+the block work of ALL W ranks of a zigzag ring (every visible (query chunk, key chunk) pair, the
+log-sum-exp merges, the per-block backward and the dQ / dK / dV partial adds, in the partials'
+transport dtype) run back to back on one GPU, against ONE flash-attention call over the full
+sequence (forward + backward). The ratio is the compute overhead of splitting attention over the
+ring; the P2P transfers overlap the blocks on real ranks and are not modelled.
+
+  python tools/cp_emul_bench.py [--S 8192] [--W 4] [--H 20] [--D 128] [--B 1]
+Prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--S", type=int, default=8192)
+    ap.add_argument("--W", type=int, default=4)
+    ap.add_argument("--H", type=int, default=20)
+    ap.add_argument("--D", type=int, default=128)
+    ap.add_argument("--B", type=int, default=1)
+    ap.add_argument("--iters", type=int, default=5)
+    a = ap.parse_args()
+    import apex
+    from apex.contrib.multihead_attn.flash import flash_attention
+    from apex.transformer import context_parallel as cp
+
+    apex._ext.require()
+    torch.manual_seed(0)
+    B, S, H, D, W = a.B, a.S, a.H, a.D, a.W
+    q, k, v = (torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16) for _ in range(3))
+    do = torch.randn_like(q)
+    scale = D ** -0.5
+
+    def full():
+        qq, kk, vv = (t.detach().requires_grad_() for t in (q, k, v))
+        flash_attention(qq, kk, vv, causal=True, scale=scale).backward(do)
+
+    n = 2 * W
+    chunks = [t.chunk(n, dim=1) for t in (q, k, v, do)]
+
+    def rank_shard(r, i):
+        ids, _ = cp.chunk_ids(r, W, "zigzag")
+        return torch.cat([chunks[i][j] for j in ids], dim=1).contiguous()
+
+    local = [[rank_shard(r, i) for i in range(4)] for r in range(W)]
+
+    def emul():
+        for r in range(W):
+            ql, kl_, vl, dol = local[r]
+            q_ids, _ = cp.chunk_ids(r, W, "zigzag")
+            qs, dos = ql.chunk(2, dim=1), dol.chunk(2, dim=1)
+            acc = [[None, None], [None, None]]
+            aux = {}
+            for step in range(W):
+                src = (r - step) % W
+                k_ids, _ = cp.chunk_ids(src, W, "zigzag")
+                ks, vs = local[src][1].chunk(2, dim=1), local[src][2].chunk(2, dim=1)
+                for qi, ki, diag in cp._pairs(q_ids, k_ids, True):
+                    o, lse, x = cp._blk_fwd(qs[qi], ks[ki], vs[ki], diag, scale, 0.0)
+                    acc[qi][0], acc[qi][1] = cp._merge(acc[qi][0], acc[qi][1], o, lse)
+                    aux[(step, qi, ki)] = x
+            outs = [ac[0].to(q.dtype) for ac in acc]
+            lses = [ac[1].contiguous() for ac in acc]
+            dq = torch.zeros_like(ql, dtype=torch.float32)
+            dqs = dq.chunk(2, dim=1)
+            for step in range(W):
+                src = (r - step) % W
+                k_ids, _ = cp.chunk_ids(src, W, "zigzag")
+                ks, vs = local[src][1].chunk(2, dim=1), local[src][2].chunk(2, dim=1)
+                dk_t = torch.zeros(local[src][1].shape, dtype=cp._dkv_transport_dtype(k), device=q.device)
+                dv_t = torch.zeros_like(dk_t)
+                dks, dvs = dk_t.chunk(2, dim=1), dv_t.chunk(2, dim=1)
+                for qi, ki, diag in cp._pairs(q_ids, k_ids, True):
+                    g = cp._blk_bwd(dos[qi], qs[qi], ks[ki], vs[ki], outs[qi], lses[qi], diag, scale, 0.0,
+                                    aux[(step, qi, ki)])
+                    dqs[qi].add_(g[0])
+                    dks[ki].add_(g[1])
+                    dvs[ki].add_(g[2])
+
+    def bench(fn):
+        for _ in range(2):
+            fn()
+        torch.cuda.synchronize()
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        e[0].record()
+        for _ in range(a.iters):
+            fn()
+        e[1].record()
+        torch.cuda.synchronize()
+        return e[0].elapsed_time(e[1]) / a.iters
+
+    t_full = bench(full)
+    t_emul = bench(emul)
+    print(json.dumps({"S": S, "W": W, "H": H, "D": D, "B": B, "full_flash_fwd_bwd_ms": round(t_full, 3),
+                      "ring_all_ranks_ms": round(t_emul, 3), "overhead": round(t_emul / t_full - 1.0, 4),
+                      "merge": "hip" if cp._native_merge(q, torch.empty(1, device=q.device)) else "torch",
+                      "dkv_transport": str(cp._dkv_transport_dtype(k)).replace("torch.", "")}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
