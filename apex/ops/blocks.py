@@ -88,8 +88,16 @@ class _AttnSublayer(torch.autograd.Function):
         qkv = G.linear(x2, wqkv, bqkv, f8=f8)
         q, k, v = qkv.view(B, S, 3, heads, d).unbind(2)
         sa, oa = _seed(x.device) if p_attn > 0 else (0, 0)
-        o, lse, dmask = C.flash_attn_fwd(q, k, v, bool(causal), scale, float(p_attn), sa, oa, k_lens)
+        # fp8: the flash forward also writes the e4m3 codes of its output, the attention-out GEMM's
+        # operand (slot = that GEMM's "x" slot), instead of a standalone quantise pass over [tokens, E]
+        okey = (f8.key_of(wo), "x") if f8 is not None else None
+        q8o = _q8(f8, okey, f8._fwd, qkv, shape=(B, S, heads, d)) if f8 is not None else None
+        o, lse, dmask = C.flash_attn_fwd(q, k, v, bool(causal), scale, float(p_attn), sa, oa, k_lens,
+                                         **({} if q8o is None else dict(q8_out=q8o[0], q8_scale=q8o[1],
+                                                                        q8_amax=q8o[2], q8_fmt=q8o[3])))
         o2 = o.view(B * S, E)
+        if f8 is not None:
+            _q8_file(f8, o2, None if q8o is None else (q8o[0].view(B * S, E),) + tuple(q8o[1:]), okey, f8._fwd)
         t = G.linear(o2, wo, f8=f8)
         sh, oh = _seed(x.device) if p_hidden > 0 else (0, 0)
         mem = _ln_mem(C, E)
@@ -131,8 +139,18 @@ class _AttnSublayer(torch.autograd.Function):
         # the attention backward also emits per-sequence column sums of dq/dk/dv (the QKV bias
         # gradient before the sum over the batch) — no separate pass over dqkv
         dsum = torch.zeros(B, 3 * E, device=dqkv.device, dtype=torch.float32) if has_bqkv else None
-        C.flash_attn_bwd(dctx, q, k, v, o, lse, dq, dk, dv, bool(causal), scale, float(p_attn), sa, oa, k_lens,
-                         dmask, dsum)
+        # fp8: the e5m2 codes of dq / dk / dv for the QKV input-gradient GEMM (its "dy" slot), written by
+        # the flash backward itself where it runs as one kernel (Sk <= 128)
+        qkey = (f8.key_of(wqkv), "dy") if f8 is not None else None
+        q8d = _q8(f8, qkey, f8._bwd, dqkv) if f8 is not None else None
+        kw = {}
+        if q8d is not None:
+            cq, ck, cv = q8d[0].view(B, S, 3, heads, d).unbind(2)
+            kw = dict(q8_dq=cq, q8_dk=ck, q8_dv=cv, q8_scale=q8d[1], q8_amax=q8d[2], q8_fmt=q8d[3])
+        written = C.flash_attn_bwd(dctx, q, k, v, o, lse, dq, dk, dv, bool(causal), scale, float(p_attn), sa, oa,
+                                   k_lens, dmask, dsum, **kw)
+        if q8d is not None and written:
+            f8.register(dqkv, q8d[0], q8d[4], q8d[3])
         dbqkv = C.partial_colsum(dsum, bdt, _gt(pbqkv)) if has_bqkv else None
         dx = G.dgrad_resid(dqkv, wqkv, dres, f8=f8)  # residual grad accumulated in the GEMM epilogue
         dwqkv = _wgrad(dqkv, x2, param=pqkv)

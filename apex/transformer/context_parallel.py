@@ -217,6 +217,34 @@ def _pairs(q_ids, k_ids, causal):
     return out
 
 
+def _step_calls(r, src, W, layout, causal):
+    """The flash calls of one ring step: [(q_sel, k_sel, diag)] where q_sel / k_sel is a local chunk
+    index or None for ALL this rank's (resp. the incoming shard's) chunks, and diag = causal mask in
+    local coordinates. With the zigzag layout every step is ONE call (the pairs it replaces ran as up
+    to four launches of half the size — each well under the chip's 256 CUs at Megatron shapes):
+      no mask:      all queries x all keys
+      causal, src == r: all queries x all keys, causal in local coordinates — [chunk r, chunk 2W-1-r]
+                    on both sides, so j <= i masks exactly the invisible pairs (the late keys for
+                    the early queries) and the two diagonal blocks
+      src < r:      all queries x the shard's EARLY chunk (its late chunk is after both of ours)
+      src > r:      our LATE chunk x all the shard's keys (our early chunk sees none of them)
+    The contiguous layout keeps one (query chunk, key chunk) pair per step."""
+    if layout == "zigzag":
+        if not causal:
+            return [(None, None, False)]
+        if src == r:
+            return [(None, None, True)]
+        if src < r:
+            return [(None, 0, False)]
+        return [(1, None, False)]
+    return [(qi, ki, diag) for qi, ki, diag in _pairs(*(chunk_ids(x, W, layout)[0] for x in (r, src)), causal)]
+
+
+def _rows(t, sel, n, dim):
+    """Chunk ``sel`` of ``t`` along ``dim`` (``t`` itself for sel None), contiguous."""
+    return t if sel is None else t.chunk(n, dim=dim)[sel].contiguous()
+
+
 class _Ring:
     """Async exchange with the ring neighbours (send to rank + 1, receive from rank - 1)."""
 
@@ -246,19 +274,22 @@ class _RingAttention(torch.autograd.Function):
         ring = _Ring(group, ranks, r)
         q_ids, _ = chunk_ids(r, W, layout)
         nq = len(q_ids)
-        qs = q.chunk(nq, dim=1)
         acc = [[None, None] for _ in range(nq)]
         aux = {}
         cur = [k.contiguous(), v.contiguous()]
         for step in range(W):
             src = (r - step) % W
             nxt = ring.start(cur) if step < W - 1 else None  # the transfer overlaps this step's blocks
-            k_ids, _ = chunk_ids(src, W, layout)
-            ks, vs = cur[0].chunk(len(k_ids), dim=1), cur[1].chunk(len(k_ids), dim=1)
-            for qi, ki, diag in _pairs(q_ids, k_ids, causal):
-                o, lse, a = _blk_fwd(qs[qi], ks[ki], vs[ki], diag, scale, p)
-                acc[qi][0], acc[qi][1] = _merge(acc[qi][0], acc[qi][1], o, lse)
-                aux[(step, qi, ki)] = a
+            nk = len(chunk_ids(src, W, layout)[0])
+            for q_sel, k_sel, diag in _step_calls(r, src, W, layout, causal):
+                o, lse, a = _blk_fwd(_rows(q, q_sel, nq, 1), _rows(cur[0], k_sel, nk, 1), _rows(cur[1], k_sel, nk, 1),
+                                     diag, scale, p)
+                sel = range(nq) if q_sel is None else [q_sel]
+                os_ = o.chunk(len(sel), dim=1) if q_sel is None else [o]
+                ls_ = lse.chunk(len(sel), dim=2) if q_sel is None else [lse]
+                for qi, oo, ll in zip(sel, os_, ls_):
+                    acc[qi][0], acc[qi][1] = _merge(acc[qi][0], acc[qi][1], oo.contiguous(), ll.contiguous())
+                aux[(step, q_sel, k_sel)] = a
             if nxt is not None:
                 cur = _Ring.finish(nxt)
         out = torch.cat([a[0] for a in acc], dim=1).to(q.dtype)
@@ -277,33 +308,30 @@ class _RingAttention(torch.autograd.Function):
         q_ids, _ = chunk_ids(r, W, layout)
         nq = len(q_ids)
         do = do.contiguous()
-        qs, dos, outs = q.chunk(nq, dim=1), do.chunk(nq, dim=1), out.chunk(nq, dim=1)
-        lses = [t.contiguous() for t in lse.chunk(nq, dim=2)]
+        lse = lse.contiguous()
         dq = torch.zeros(q.shape, dtype=_acc_dtype(q), device=q.device)
-        dqs = dq.chunk(nq, dim=1)
         cur = [k.contiguous(), v.contiguous()]
         dkv_pending = None  # the dK/dV partial of the shard arriving with `cur`, still in flight
         for step in range(W):
             src = (r - step) % W
             nxt = ring.start(cur) if step < W - 1 else None
-            k_ids, _ = chunk_ids(src, W, layout)
-            ks, vs = cur[0].chunk(len(k_ids), dim=1), cur[1].chunk(len(k_ids), dim=1)
+            nk = len(chunk_ids(src, W, layout)[0])
             grads = []
-            for qi, ki, diag in _pairs(q_ids, k_ids, causal):
-                g = _blk_bwd(dos[qi], qs[qi], ks[ki], vs[ki], outs[qi], lses[qi], diag, scale, p,
-                             ctx.aux.get((step, qi, ki)))
-                dqs[qi].add_(g[0])
-                grads.append((ki, g[1], g[2]))
+            for q_sel, k_sel, diag in _step_calls(r, src, W, layout, causal):
+                g = _blk_bwd(_rows(do, q_sel, nq, 1), _rows(q, q_sel, nq, 1), _rows(cur[0], k_sel, nk, 1),
+                             _rows(cur[1], k_sel, nk, 1), _rows(out, q_sel, nq, 1), _rows(lse, q_sel, nq, 2), diag,
+                             scale, p, ctx.aux.get((step, q_sel, k_sel)))
+                (dq if q_sel is None else dq.chunk(nq, dim=1)[q_sel]).add_(g[0])
+                grads.append((k_sel, g[1], g[2]))
             # the shard's dK/dV partial from the previous ranks (zero at step 0) + this rank's blocks
             if dkv_pending is None:
                 dk_t = torch.zeros(k.shape, dtype=_dkv_transport_dtype(k), device=k.device)
                 dv_t = torch.zeros(v.shape, dtype=_dkv_transport_dtype(v), device=v.device)
             else:
                 dk_t, dv_t = _Ring.finish(dkv_pending)
-            dks, dvs = dk_t.chunk(len(k_ids), dim=1), dv_t.chunk(len(k_ids), dim=1)
-            for ki, gk, gv in grads:
-                dks[ki].add_(gk)
-                dvs[ki].add_(gv)
+            for k_sel, gk, gv in grads:
+                (dk_t if k_sel is None else dk_t.chunk(nk, dim=1)[k_sel]).add_(gk)
+                (dv_t if k_sel is None else dv_t.chunk(nk, dim=1)[k_sel]).add_(gv)
             if W == 1:  # no ring: the only shard is this rank's own (nothing to send to itself)
                 dkv_pending = ([], [dk_t, dv_t])
                 continue

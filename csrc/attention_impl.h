@@ -25,6 +25,7 @@
 //   share a query block (Sk > 128), fp32 atomics.
 #pragma once
 #include "common.h"
+#include "fp8_pack.h"
 #include "kernels.h"
 
 #include <cstdlib>
@@ -507,9 +508,12 @@ attn_fwd_kernel(AttnArgs a) {
   }
   // ---- epilogue
   const float ltot = l + xor32_f(l);
+  float q8mx = 0.f;
   if (qrow < a.Sq) {
     const float inv = ltot > 0.f ? (DROPOUT ? a.drop_scale : 1.f) / ltot : 0.f;
-    T* op = (T*)a.o + b * a.o_bs + h * a.o_hs + (int64_t)qrow * a.o_ss;
+    const int64_t ooff = b * a.o_bs + h * a.o_hs + (int64_t)qrow * a.o_ss;
+    T* op = (T*)a.o + ooff;
+    const float qs = a.q8o ? a.q8_scale[0] : 0.f;
 #pragma unroll
     for (int db = 0; db < D / 32; ++db) {
 #pragma unroll
@@ -519,11 +523,23 @@ attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) w[e] = (T)(o[db][4 * g + e] * inv);
         *(t4*)(op + 32 * db + 8 * g + 4 * hl) = w;
+        if (a.q8o) {  // fp8 codes of the stored (rounded) values: the attention-out GEMM's operand
+          float r[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            r[e] = (float)w[e];
+            q8mx = fmaxf(q8mx, fabsf(r[e]));
+          }
+          *(uint32_t*)(a.q8o + ooff + 32 * db + 8 * g + 4 * hl) =
+              a.q8_fmt == 0 ? f8_pack4<0>(r[0] * qs, r[1] * qs, r[2] * qs, r[3] * qs)
+                            : f8_pack4<1>(r[0] * qs, r[1] * qs, r[2] * qs, r[3] * qs);
+        }
       }
     }
     if (hl == 0 && a.lse)
       a.lse[(int64_t)bh * a.Sq + qrow] = ltot > 0.f ? (m * sl2 + log2f(ltot)) * kLn2 : INFINITY;
   }
+  if (a.q8o) f8_block_amax(q8mx, a.q8_amax);  // every thread of the block reaches this
 }
 
 // ---------------------------------------------------------------------------
@@ -705,6 +721,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
   if (D < 128) load_kv();
 
   float dqcs[D / 32][4] = {};  // DSUM: this lane's dq dims (see the dQ section) summed over queries
+  // fp8 producer-side codes of dq / dk / dv (AttnArgs::q8dq..): running max|value| of this lane
+  float q8mx = 0.f;
+  const float q8s = a.q8dq ? a.q8_scale[0] : 0.f;
   auto body = [&](Pf& P, const int qb) {
     uint4 (&pf_q)[NLD] = P.q;
     uint4 (&pf_do)[NLD] = P.d;
@@ -877,7 +896,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
       // this workgroup is the sole writer of these query rows (single key block): final dtype
       const int q = qb + 16 * qt + lq;
       if (q < nq) {
-        T* dqp = (T*)a.dq + b * a.dq_bs + h * a.dq_hs + (int64_t)q * a.dq_ss;
+        const int64_t qoff = b * a.dq_bs + h * a.dq_hs + (int64_t)q * a.dq_ss;
+        T* dqp = (T*)a.dq + qoff;
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
           typedef T t4 __attribute__((ext_vector_type(4)));
@@ -885,6 +905,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
 #pragma unroll
           for (int i = 0; i < 4; ++i) w[i] = (T)(acc[t][i] * a.scale);
           *(t4*)(dqp + (dt0 + t) * 16 + 4 * lg) = w;
+          if (a.q8dq) {  // fp8 codes of dq as stored (the QKV input-gradient GEMM's operand)
+            float r[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              r[i] = (float)w[i];
+              q8mx = fmaxf(q8mx, fabsf(r[i]));
+            }
+            *(uint32_t*)(a.q8dq + qoff + (dt0 + t) * 16 + 4 * lg) =
+                a.q8_fmt == 0 ? f8_pack4<0>(r[0] * q8s, r[1] * q8s, r[2] * q8s, r[3] * q8s)
+                              : f8_pack4<1>(r[0] * q8s, r[1] * q8s, r[2] * q8s, r[3] * q8s);
+          }
           if constexpr (DSUM) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) dqcs[t][i] += (float)w[i];
@@ -932,7 +963,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
   lds_barrier();  // every wave is done reading lds_k (dQ products)
   constexpr int LDE = kBwdBK + 4;
   static_assert(D * LDE <= LDSK, "dK/dV staging fits lds_k");
-  auto emit = [&](const f32x16 (&acc)[D / 32], const float mul, T* dst, const int64_t ss, float* dsum_t) {
+  auto emit = [&](const f32x16 (&acc)[D / 32], const float mul, T* dst, const int64_t ss, float* dsum_t,
+                  uint8_t* q8dst) {
     typedef T t4 __attribute__((ext_vector_type(4)));
 #pragma unroll
     for (int db = 0; db < D / 32; ++db) {
@@ -965,12 +997,29 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
       const T* src = lds_k + (d0 + ((lane & 15) >> 2)) * LDE + kb + 4 * (lane & 3);
       const s16x4 lo = lds_tr16(src), hi = lds_tr16(src + 4 * LDE);
       const int key = k0 + kb + (lane & 15);
-      if (key < a.Sk) *(V8*)(dst + (int64_t)key * ss + d0) = join4<V8>(lo, hi);
+      if (key < a.Sk) {
+        const V8 x = join4<V8>(lo, hi);
+        *(V8*)(dst + (int64_t)key * ss + d0) = x;
+        if (q8dst) {  // fp8 codes of the stored values (the same element offset in the code array)
+          typedef T t8 __attribute__((ext_vector_type(8)));
+          const t8 xv = __builtin_bit_cast(t8, x);
+          float r[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            r[e] = (float)xv[e];
+            q8mx = fmaxf(q8mx, fabsf(r[e]));
+          }
+          f8_store8(q8dst + (int64_t)key * ss + d0, r, q8s, a.q8_fmt);
+        }
+      }
     }
     lds_barrier();
   };
-  emit(dk, a.scale, dkp, a.dk_ss, DSUM ? dsum + (int64_t)a.H * D : nullptr);
-  emit(dv, rkeep, dvp, a.dv_ss, DSUM ? dsum + (int64_t)2 * a.H * D : nullptr);
+  emit(dk, a.scale, dkp, a.dk_ss, DSUM ? dsum + (int64_t)a.H * D : nullptr,
+       a.q8dk ? a.q8dk + b * a.dk_bs + h * a.dk_hs : nullptr);
+  emit(dv, rkeep, dvp, a.dv_ss, DSUM ? dsum + (int64_t)2 * a.H * D : nullptr,
+       a.q8dv ? a.q8dv + b * a.dv_bs + h * a.dv_hs : nullptr);
+  if (a.q8dq) f8_block_amax(q8mx, a.q8_amax);  // every thread of the block reaches this
 }
 
 // dQ for key ranges longer than one backward key block: query-stationary, the forward's

@@ -363,9 +363,32 @@ void attn_set_bias(apex::AttnArgs& a, const c10::optional<Tensor>& bias, const T
   a.bias_qs = t.size(2) == 1 ? 0 : t.stride(2);
 }
 
+// fp8 producer-side codes of an attention output (apex.fp8): a uint8 tensor with `like`'s sizes AND
+// strides (so a code sits at its value's element offset), plus the slot's scale / amax
+static uint8_t* attn_q8(const c10::optional<Tensor>& codes, const Tensor& like, const char* what) {
+  if (!codes.has_value() || !codes->defined()) return nullptr;
+  TORCH_CHECK(codes->scalar_type() == at::kByte && codes->sizes() == like.sizes() &&
+                  codes->strides() == like.strides() && codes->device() == like.device(),
+              what, ": fp8 codes must be a uint8 tensor with the output's sizes and strides");
+  return codes->data_ptr<uint8_t>();
+}
+static void attn_q8_scale(apex::AttnArgs& a, const c10::optional<Tensor>& scale, const c10::optional<Tensor>& amax,
+                          int64_t fmt, const Tensor& like) {
+  TORCH_CHECK(scale.has_value() && amax.has_value() && scale->scalar_type() == at::kFloat &&
+                  amax->scalar_type() == at::kFloat && scale->numel() >= 1 && amax->numel() >= 1 &&
+                  scale->device() == like.device() && amax->device() == like.device(),
+              "flash attention fp8 codes: q8_scale / q8_amax fp32 device tensors");
+  TORCH_CHECK(fmt == 0 || fmt == 1, "flash attention fp8 codes: q8_fmt 0 (e4m3) or 1 (e5m2)");
+  a.q8_scale = scale->data_ptr<float>();
+  a.q8_amax = amax->data_ptr<float>();
+  a.q8_fmt = (int)fmt;
+}
+
 std::vector<Tensor> flash_attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, double scale,
                                    double p_drop, int64_t seed, int64_t offset,
-                                   const c10::optional<Tensor>& k_lens, const c10::optional<Tensor>& bias) {
+                                   const c10::optional<Tensor>& k_lens, const c10::optional<Tensor>& bias,
+                                   const c10::optional<Tensor>& q8_out, const c10::optional<Tensor>& q8_scale,
+                                   const c10::optional<Tensor>& q8_amax, int64_t q8_fmt) {
   apex::AttnArgs a = attn_common(q, k, v, causal, scale, p_drop, seed, offset, k_lens);
   attn_set_bias(a, bias, q);
   Tensor o = at::empty({a.B, a.Sq, a.H, a.D}, q.options());
@@ -373,6 +396,8 @@ std::vector<Tensor> flash_attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, do
   a.o = o.data_ptr();
   attn_set(a, o, a.o_bs, a.o_ss, a.o_hs);
   a.lse = lse.data_ptr<float>();
+  a.q8o = attn_q8(q8_out, o, "flash_attn_fwd");
+  if (a.q8o) attn_q8_scale(a, q8_scale, q8_amax, q8_fmt, o);
   a.mask_words = 2 * (((int64_t)a.Sk + 31) / 32);
   Tensor dmask;  // dropout keep bits, consumed by the backward pass
   if (a.drop_thresh) {
@@ -385,11 +410,15 @@ std::vector<Tensor> flash_attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, do
   return {o, lse, dmask};
 }
 
-void flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor dq,
+// returns true when the fp8 codes of dq / dk / dv were written (q8_* given and the single-kernel
+// backward ran: Sk <= 128; longer key ranges compute dq in a separate kernel without codes)
+bool flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor dq,
                     Tensor dk, Tensor dv, bool causal, double scale, double p_drop, int64_t seed,
                     int64_t offset, const c10::optional<Tensor>& k_lens,
                     const c10::optional<Tensor>& dmask, const c10::optional<Tensor>& dsum, int64_t dbg,
-                    const c10::optional<Tensor>& bias) {
+                    const c10::optional<Tensor>& bias, const c10::optional<Tensor>& q8_dq,
+                    const c10::optional<Tensor>& q8_dk, const c10::optional<Tensor>& q8_dv,
+                    const c10::optional<Tensor>& q8_scale, const c10::optional<Tensor>& q8_amax, int64_t q8_fmt) {
   apex::AttnArgs a = attn_common(q, k, v, causal, scale, p_drop, seed, offset, k_lens);
   a.dbg = (int)dbg;
   attn_set_bias(a, bias, q);
@@ -416,10 +445,21 @@ void flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor 
   }
   const int64_t rows = (int64_t)a.B * a.H * a.Sq;
   Tensor delta_ws;  // rowsum(dO * O), one pre-pass kernel, read by the dK/dV and dQ kernels
-  if (apex::attn_bwd_needs_dq_acc(a)) delta_ws = at::empty({rows}, q.options().dtype(at::kFloat));
+  const bool two_kernel = apex::attn_bwd_needs_dq_acc(a);
+  if (two_kernel) delta_ws = at::empty({rows}, q.options().dtype(at::kFloat));
+  bool q8 = false;
+  if (!two_kernel && !apex::attn_bwd_split() && q8_dq.has_value() && q8_dq->defined()) {
+    a.q8dq = attn_q8(q8_dq, dq, "flash_attn_bwd dq");
+    a.q8dk = attn_q8(q8_dk, dk, "flash_attn_bwd dk");
+    a.q8dv = attn_q8(q8_dv, dv, "flash_attn_bwd dv");
+    TORCH_CHECK(a.q8dk && a.q8dv, "flash_attn_bwd: q8_dq, q8_dk and q8_dv go together");
+    attn_q8_scale(a, q8_scale, q8_amax, q8_fmt, dq);
+    q8 = true;
+  }
   check(apex::attn_bwd(a, dout.data_ptr(), delta_ws.defined() ? delta_ws.data_ptr<float>() : nullptr,
                        dk.data_ptr(), dv.data_ptr(), dt_code(q.scalar_type()), cur_stream()),
         "attn_bwd");
+  return q8;
 }
 
 // --------------------------------------------------------------------------
@@ -1380,12 +1420,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fp8_update_scales", &k_fp8_update_scales);
   m.def("flash_attn_fwd", &flash_attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("causal"),
         py::arg("scale"), py::arg("p_drop"), py::arg("seed"), py::arg("offset"), py::arg("k_lens"),
-        py::arg("bias") = py::none());
+        py::arg("bias") = py::none(), py::arg("q8_out") = py::none(), py::arg("q8_scale") = py::none(),
+        py::arg("q8_amax") = py::none(), py::arg("q8_fmt") = 0);
   m.def("gemm_set_dbg", [](int64_t v) { check(apex::gemm_set_dbg((int)v), "gemm_set_dbg"); });
   m.def("flash_attn_bwd", &flash_attn_bwd, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"),
         py::arg("o"), py::arg("lse"), py::arg("dq"), py::arg("dk"), py::arg("dv"), py::arg("causal"),
         py::arg("scale"), py::arg("p_drop"), py::arg("seed"), py::arg("offset"), py::arg("k_lens"),
-        py::arg("dmask"), py::arg("dsum") = py::none(), py::arg("dbg") = 0, py::arg("bias") = py::none());
+        py::arg("dmask"), py::arg("dsum") = py::none(), py::arg("dbg") = 0, py::arg("bias") = py::none(),
+        py::arg("q8_dq") = py::none(), py::arg("q8_dk") = py::none(), py::arg("q8_dv") = py::none(),
+        py::arg("q8_scale") = py::none(), py::arg("q8_amax") = py::none(), py::arg("q8_fmt") = 0);
   m.def("partial_colsum", &k_partial_colsum, py::arg("part"), py::arg("out_dtype"), py::arg("out") = py::none());
   m.def("flash_dropout_mask", &flash_dropout_mask);
   m.def("lse_merge", &k_lse_merge, py::arg("acc_o"), py::arg("acc_lse"), py::arg("o"), py::arg("lse"),

@@ -101,6 +101,18 @@ struct AttnArgs {
                          // of dq, dk, dv — the packed-QKV projection's bias gradient, per batch
   const void* bias;      // optional additive score bias (input dtype), element (b, h, q, key) at
   int64_t bias_bs, bias_hs, bias_qs;  // b*bias_bs + h*bias_hs + q*bias_qs + key (0 = broadcast)
+  // fp8 producer-side codes (apex.fp8): the kernels also write fp8 codes of what they store, for the
+  // GEMM that consumes it next (no standalone quantise pass): forward -> O (the attention-out GEMM's
+  // e4m3 operand), backward -> dq / dk / dv (the QKV input-gradient GEMM's e5m2 operand). Each code
+  // array has its tensor's element layout (same strides); codes = sat(value * q8_scale[0]), max|value|
+  // folded into q8_amax[0]. Null: off.
+  uint8_t* q8o;
+  uint8_t* q8dq;
+  uint8_t* q8dk;
+  uint8_t* q8dv;
+  const float* q8_scale;
+  float* q8_amax;
+  int q8_fmt;  // 0 = e4m3, 1 = e5m2
 };
 inline uint32_t attn_drop_thresh(double p) {  // 8-bit keep threshold in [1, 255], 0 = off
   if (p <= 0.0) return 0u;

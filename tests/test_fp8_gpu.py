@@ -401,6 +401,52 @@ def test_bdaln_q8_side_output_matches_standalone_quantize(fmt, p):
         assert float(damax) == float(damax_ref)
 
 
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_flash_attention_fp8_codes_match_standalone_quantize(p):
+    """The flash forward's fp8 side output (e4m3 codes of O, the attention-out GEMM's operand) and the
+    single-kernel backward's (e5m2 codes of dq / dk / dv in the packed QKV layout, the QKV
+    input-gradient GEMM's operand): bit-identical to the standalone quantiser on the stored bf16
+    tensors with the same scale, the same amax, and the side outputs change nothing else."""
+    C = _C()
+    torch.manual_seed(5)
+    B, S, H, D = 4, 128, 4, 64
+    dt = torch.bfloat16
+    qkv = torch.randn(B * S, 3 * H * D, device=DEV, dtype=dt)
+    q, k, v = qkv.view(B, S, 3, H, D).unbind(2)
+    scale = torch.tensor([7.25], device=DEV)
+    amax = torch.zeros(1, device=DEV)
+    codes = torch.empty(B, S, H, D, device=DEV, dtype=torch.uint8)
+    o, lse, dmask = C.flash_attn_fwd(q, k, v, False, D ** -0.5, p, 3, 4, None, q8_out=codes, q8_scale=scale,
+                                     q8_amax=amax, q8_fmt=0)
+    o_ref, lse_ref, _ = C.flash_attn_fwd(q, k, v, False, D ** -0.5, p, 3, 4, None)
+    assert torch.equal(o, o_ref) and torch.equal(lse, lse_ref)
+    amax_ref = torch.zeros(1, device=DEV)
+    assert torch.equal(codes, C.fp8_quantize(o, 0, scale, amax_ref))
+    assert float(amax) == float(amax_ref)
+    do = torch.randn_like(o)
+    dqkv, dqkv_ref = torch.empty_like(qkv), torch.empty_like(qkv)
+    dcodes = torch.empty(B * S, 3 * H * D, device=DEV, dtype=torch.uint8)
+    damax = torch.zeros(1, device=DEV)
+    cq, ck, cv = dcodes.view(B, S, 3, H, D).unbind(2)
+    g = dqkv.view(B, S, 3, H, D).unbind(2)
+    written = C.flash_attn_bwd(do, q, k, v, o, lse, *g, False, D ** -0.5, p, 3, 4, None, dmask, q8_dq=cq,
+                               q8_dk=ck, q8_dv=cv, q8_scale=scale, q8_amax=damax, q8_fmt=1)
+    assert written
+    C.flash_attn_bwd(do, q, k, v, o, lse, *dqkv_ref.view(B, S, 3, H, D).unbind(2), False, D ** -0.5, p, 3, 4,
+                     None, dmask)
+    assert torch.equal(dqkv, dqkv_ref)
+    damax_ref = torch.zeros(1, device=DEV)
+    assert torch.equal(dcodes, C.fp8_quantize(dqkv, 1, scale, damax_ref))
+    assert float(damax) == float(damax_ref)
+    # a long key range runs the two-kernel backward: no codes, reported as such
+    q2, k2, v2 = (torch.randn(2, 256, H, D, device=DEV, dtype=dt) for _ in range(3))
+    o2, lse2, dm2 = C.flash_attn_fwd(q2, k2, v2, False, D ** -0.5, 0.0, 0, 0, None)
+    g2 = [torch.empty_like(q2) for _ in range(3)]
+    c2 = [torch.empty(q2.shape, device=DEV, dtype=torch.uint8) for _ in range(3)]
+    assert not C.flash_attn_bwd(torch.randn_like(o2), q2, k2, v2, o2, lse2, *g2, False, D ** -0.5, 0.0, 0, 0, None,
+                                dm2, q8_dq=c2[0], q8_dk=c2[1], q8_dv=c2[2], q8_scale=scale, q8_amax=damax, q8_fmt=1)
+
+
 def test_blocks_fp8_producer_codes_match_standalone_path(fp8_off, monkeypatch):
     """BERT sublayers under fp8 for three optimizer steps with the LN kernels writing the fp8 codes
     (APEX_FP8_PRODUCER default) vs the standalone quantise passes: identical outputs and gradients

@@ -52,37 +52,39 @@ def main():
     local = [[rank_shard(r, i) for i in range(4)] for r in range(W)]
 
     def emul():
+        # every rank's ring steps as apex.transformer.context_parallel runs them: one flash call per
+        # step (_step_calls), the fused merges, the block backward and the partial adds
         for r in range(W):
-            ql, kl_, vl, dol = local[r]
-            q_ids, _ = cp.chunk_ids(r, W, "zigzag")
-            qs, dos = ql.chunk(2, dim=1), dol.chunk(2, dim=1)
+            ql, _, _, dol = local[r]
             acc = [[None, None], [None, None]]
             aux = {}
             for step in range(W):
                 src = (r - step) % W
-                k_ids, _ = cp.chunk_ids(src, W, "zigzag")
-                ks, vs = local[src][1].chunk(2, dim=1), local[src][2].chunk(2, dim=1)
-                for qi, ki, diag in cp._pairs(q_ids, k_ids, True):
-                    o, lse, x = cp._blk_fwd(qs[qi], ks[ki], vs[ki], diag, scale, 0.0)
-                    acc[qi][0], acc[qi][1] = cp._merge(acc[qi][0], acc[qi][1], o, lse)
-                    aux[(step, qi, ki)] = x
-            outs = [ac[0].to(q.dtype) for ac in acc]
-            lses = [ac[1].contiguous() for ac in acc]
+                kl_, vl = local[src][1], local[src][2]
+                for q_sel, k_sel, diag in cp._step_calls(r, src, W, "zigzag", True):
+                    o, lse, x = cp._blk_fwd(cp._rows(ql, q_sel, 2, 1), cp._rows(kl_, k_sel, 2, 1),
+                                            cp._rows(vl, k_sel, 2, 1), diag, scale, 0.0)
+                    sel = range(2) if q_sel is None else [q_sel]
+                    os_ = o.chunk(2, dim=1) if q_sel is None else [o]
+                    ls_ = lse.chunk(2, dim=2) if q_sel is None else [lse]
+                    for qi, oo, ll in zip(sel, os_, ls_):
+                        acc[qi][0], acc[qi][1] = cp._merge(acc[qi][0], acc[qi][1], oo.contiguous(), ll.contiguous())
+                    aux[(step, q_sel, k_sel)] = x
+            out = torch.cat([ac[0] for ac in acc], dim=1).to(q.dtype)
+            lse = torch.cat([ac[1] for ac in acc], dim=2).contiguous()
             dq = torch.zeros_like(ql, dtype=torch.float32)
-            dqs = dq.chunk(2, dim=1)
             for step in range(W):
                 src = (r - step) % W
-                k_ids, _ = cp.chunk_ids(src, W, "zigzag")
-                ks, vs = local[src][1].chunk(2, dim=1), local[src][2].chunk(2, dim=1)
-                dk_t = torch.zeros(local[src][1].shape, dtype=cp._dkv_transport_dtype(k), device=q.device)
+                kl_, vl = local[src][1], local[src][2]
+                dk_t = torch.zeros(kl_.shape, dtype=cp._dkv_transport_dtype(k), device=q.device)
                 dv_t = torch.zeros_like(dk_t)
-                dks, dvs = dk_t.chunk(2, dim=1), dv_t.chunk(2, dim=1)
-                for qi, ki, diag in cp._pairs(q_ids, k_ids, True):
-                    g = cp._blk_bwd(dos[qi], qs[qi], ks[ki], vs[ki], outs[qi], lses[qi], diag, scale, 0.0,
-                                    aux[(step, qi, ki)])
-                    dqs[qi].add_(g[0])
-                    dks[ki].add_(g[1])
-                    dvs[ki].add_(g[2])
+                for q_sel, k_sel, diag in cp._step_calls(r, src, W, "zigzag", True):
+                    g = cp._blk_bwd(cp._rows(dol, q_sel, 2, 1), cp._rows(ql, q_sel, 2, 1), cp._rows(kl_, k_sel, 2, 1),
+                                    cp._rows(vl, k_sel, 2, 1), cp._rows(out, q_sel, 2, 1), cp._rows(lse, q_sel, 2, 2),
+                                    diag, scale, 0.0, aux[(step, q_sel, k_sel)])
+                    (dq if q_sel is None else dq.chunk(2, dim=1)[q_sel]).add_(g[0])
+                    (dk_t if k_sel is None else dk_t.chunk(2, dim=1)[k_sel]).add_(g[1])
+                    (dv_t if k_sel is None else dv_t.chunk(2, dim=1)[k_sel]).add_(g[2])
 
     def bench(fn):
         for _ in range(2):
