@@ -15,9 +15,12 @@ Every bf16/fp16 device call runs the MFMA flash-attention kernels in apex._C
   (True = attend) and becomes a 0 / -inf bias;
 * ``k_lens``: per-batch valid key lengths (right padding) skip whole key tiles.
 
-Device calls the flash kernels do not take — fp32 inputs, head dims > 256, an ``attn_bias`` that
-itself requires a gradient (the kernels treat the bias as a constant) — run the query-blocked
-memory-efficient path (``chunked.chunked_attention``: O(S * block) memory, backward by
+fp32 device inputs (head dims up to 128) run the f32-MFMA flash kernels (csrc/attention_f32.hip:
+exact f32 products and accumulation, the same masks / bias / dropout semantics).
+
+Device calls the flash kernels do not take — fp32 head dims > 128, head dims > 256, an
+``attn_bias`` that itself requires a gradient (the kernels treat the bias as a constant) — run
+the query-blocked memory-efficient path (``chunked.chunked_attention``: O(S * block) memory, backward by
 recomputation from the saved log-sum-exp, bias gradient = the score gradient), never the O(S^2)
 composition. The reference composition (``attention_reference``: matmul -> softmax in fp32 ->
 dropout -> matmul) runs on CPU tensors; ``APEX_ATTN_BACKEND=reference`` forces it (A/B, numerics
@@ -44,12 +47,19 @@ def _padded_dim(d):
 
 
 def _native_ok(t, bias):
-    if os.environ.get("APEX_ATTN_BACKEND", "native") in ("reference", "sdpa"):
+    if os.environ.get("APEX_ATTN_BACKEND", "native") in ("reference", "sdpa", "chunked"):
         return False
-    if not (t.is_cuda and t.dtype in (torch.float16, torch.bfloat16)):
+    if not t.is_cuda:
         return False
     d = t.shape[-1]
     if d % 8 or _padded_dim(d) is None:
+        return False
+    if t.dtype == torch.float32:
+        # fp32: the f32-MFMA kernels (csrc/attention_f32.hip), head dims up to 128;
+        # APEX_ATTN_F32=0 selects the torch compositions (A/B)
+        if os.environ.get("APEX_ATTN_F32", "1") == "0" or _padded_dim(d) > 128:
+            return False
+    elif t.dtype not in (torch.float16, torch.bfloat16):
         return False
     if bias is not None and bias.requires_grad and torch.is_grad_enabled():
         return False
@@ -75,7 +85,7 @@ def prepare_bias(bias, B, H, Sq, Sk, dtype):
             raise ValueError(f"attention bias of shape {tuple(bias.shape)} does not broadcast to "
                              f"[{B}, {H}, {Sq}, {Sk}]")
     ok = bias.stride(-1) == 1 and all(bias.stride(i) % 4 == 0 or bias.shape[i] == 1 for i in range(3)) and \
-        bias.data_ptr() % 8 == 0
+        bias.data_ptr() % (16 if dtype == torch.float32 else 8) == 0
     if not ok:
         sk4 = (Sk + 3) // 4 * 4
         buf = torch.zeros(*bias.shape[:-1], sk4, dtype=dtype, device=bias.device)

@@ -291,13 +291,18 @@ def main():
             extra["fp32_config"] = f"amp O0 fp32, micro-batches of {args.fp32_microbatch} accumulated to {args.batch}"
             from apex.contrib.multihead_attn import attention as _att
 
-            q = torch.empty(args.fp32_microbatch, args.seq, cfg.num_attention_heads, 1, device="meta")
-            extra["fp32_attention_path"] = (
-                "dense fp32 composition (fused softmax / dropout kernels, f32 MFMA GEMMs; "
-                "apex.contrib.multihead_attn.attention._fallback)" if _att._short_dense_ok(q, q, None) else
-                "query-blocked fp32 composition (apex.contrib.multihead_attn.chunked)") + \
-                "; the MFMA flash kernels take bf16/fp16 (round 3 sent this step through 16-row query " \
-                "blocks: 2458 ms, which inflated its speedup_vs_fp32)"
+            d_head = cfg.hidden_size // cfg.num_attention_heads
+            q = torch.empty(args.fp32_microbatch, args.seq, cfg.num_attention_heads, d_head, device="meta")
+            if os.environ.get("APEX_ATTN_F32", "1") != "0" and d_head <= 128 and not rehearsal:
+                path = "f32-MFMA flash kernels (csrc/attention_f32.hip)"
+            elif _att._short_dense_ok(q, q, None):
+                path = ("dense fp32 composition (fused softmax / dropout kernels, f32 MFMA GEMMs; "
+                        "apex.contrib.multihead_attn.attention._fallback)")
+            else:
+                path = "query-blocked fp32 composition (apex.contrib.multihead_attn.chunked)"
+            extra["fp32_attention_path"] = path + (
+                "; history: round 3 sent this step through 16-row query blocks (2458 ms, which inflated "
+                "its speedup_vs_fp32), round 4 first the dense composition (1558 ms), then the f32 kernels")
     if rehearsal:
         extra["rehearsal"] = ("CPU/gloo rehearsal of the N-rank bench sequence with a tiny BERT "
                               f"({cfg.num_hidden_layers}L H{cfg.hidden_size}): NOT a measurement")

@@ -33,6 +33,7 @@ int attn_dropout_mask(uint8_t* out, int64_t BH, int Sq, int Sk, uint64_t seed, u
 int attn_fwd(const AttnArgs& a, int dt, hipStream_t s) {
   if (a.B * a.H == 0 || a.Sq == 0) return 0;
   if (a.drop_thresh > 0 && !a.dmask) return -3;
+  if (dt == kF32) return attn_fwd_f32(a, s);
   switch (a.D) {
     case 32: return attn_fwd_d32(a, dt, s);
     case 64: return attn_fwd_d64(a, dt, s);
@@ -57,6 +58,7 @@ int attn_bwd(const AttnArgs& a, const void* dout, float* delta_ws, void* dk, voi
              hipStream_t s) {
   if (a.B * a.H == 0 || a.Sq == 0) return 0;
   if (a.drop_thresh > 0 && !a.dmask) return -3;  // backward needs the forward's dropout bits
+  if (dt == kF32) return attn_bwd_f32(a, dout, delta_ws, dk, dv, s);
   switch (a.D) {
     case 32: return attn_bwd_d32(a, dout, delta_ws, dk, dv, dt, s);
     case 64: return attn_bwd_d64(a, dout, delta_ws, dk, dv, dt, s);

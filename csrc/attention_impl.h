@@ -1373,5 +1373,8 @@ int attn_bwd_d32(const AttnArgs& a, const void* dout, float* delta_ws, void* dk,
 int attn_bwd_d64(const AttnArgs& a, const void* dout, float* delta_ws, void* dk, void* dv, int dt, hipStream_t s);
 int attn_bwd_d128(const AttnArgs& a, const void* dout, float* delta_ws, void* dk, void* dv, int dt, hipStream_t s);
 int attn_bwd_d256(const AttnArgs& a, const void* dout, float* delta_ws, void* dk, void* dv, int dt, hipStream_t s);
+// fp32 inputs (attention_f32.hip: f32 MFMA), head dims 32 / 64 / 128
+int attn_fwd_f32(const AttnArgs& a, hipStream_t s);
+int attn_bwd_f32(const AttnArgs& a, const void* dout, float* delta_ws, void* dk, void* dv, hipStream_t s);
 
 }  // namespace apex

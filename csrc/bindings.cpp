@@ -328,6 +328,7 @@ apex::AttnArgs attn_common(const Tensor& q, const Tensor& k, const Tensor& v, bo
               "k/v shape mismatch");
   TORCH_CHECK(a.D == 32 || a.D == 64 || a.D == 128 || a.D == 256,
               "flash attention supports head dims 32, 64, 128, 256 (pad others)");
+  TORCH_CHECK(q.scalar_type() != at::kFloat || a.D <= 128, "fp32 flash attention supports head dims up to 128");
   a.causal = causal;
   a.scale = (float)scale;
   a.scale_log2 = (float)(scale * 1.4426950408889634);
@@ -357,6 +358,8 @@ void attn_set_bias(apex::AttnArgs& a, const c10::optional<Tensor>& bias, const T
               "attention bias does not broadcast to [B, H, Sq, Sk]");
   TORCH_CHECK(((uintptr_t)t.data_ptr() & 7) == 0 && t.stride(2) % 4 == 0 && t.stride(1) % 4 == 0 && t.stride(0) % 4 == 0,
               "attention bias rows must be 8-byte aligned");
+  TORCH_CHECK(t.scalar_type() != at::kFloat || ((uintptr_t)t.data_ptr() & 15) == 0,
+              "fp32 attention bias rows must be 16-byte aligned");
   a.bias = t.data_ptr();
   a.bias_bs = t.size(0) == 1 ? 0 : t.stride(0);
   a.bias_hs = t.size(1) == 1 ? 0 : t.stride(1);
@@ -397,6 +400,7 @@ std::vector<Tensor> flash_attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, do
   attn_set(a, o, a.o_bs, a.o_ss, a.o_hs);
   a.lse = lse.data_ptr<float>();
   a.q8o = attn_q8(q8_out, o, "flash_attn_fwd");
+  TORCH_CHECK(!(a.q8o && q.scalar_type() == at::kFloat), "flash_attn_fwd: fp8 codes are a 16-bit-input feature");
   if (a.q8o) attn_q8_scale(a, q8_scale, q8_amax, q8_fmt, o);
   a.mask_words = 2 * (((int64_t)a.Sk + 31) / 32);
   Tensor dmask;  // dropout keep bits, consumed by the backward pass
@@ -445,7 +449,8 @@ bool flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor 
   }
   const int64_t rows = (int64_t)a.B * a.H * a.Sq;
   Tensor delta_ws;  // rowsum(dO * O), one pre-pass kernel, read by the dK/dV and dQ kernels
-  const bool two_kernel = apex::attn_bwd_needs_dq_acc(a);
+  // fp32 (attention_f32.hip) always runs the delta pre-pass + dK/dV + dQ kernels
+  const bool two_kernel = q.scalar_type() == at::kFloat || apex::attn_bwd_needs_dq_acc(a);
   if (two_kernel) delta_ws = at::empty({rows}, q.options().dtype(at::kFloat));
   bool q8 = false;
   if (!two_kernel && !apex::attn_bwd_split() && q8_dq.has_value() && q8_dq->defined()) {

@@ -489,11 +489,11 @@ def test_blocks_fp8_producer_codes_match_standalone_path(fp8_off, monkeypatch):
     ref, hits_off = run_steps(False)
     got, hits_on = run_steps(True)
     assert hits_off == 0
-    # per step: 2 LN outputs + the FFN's gelu output consumed in forward, 3 dt + the FFN's hidden
-    # gradient in backward; step 0's
-    # backward slots are fresh (standalone current scaling), its forward producer slots file
-    # standalone codes
-    assert hits_on == 3 + 2 * 7, hits_on
+    # per step, forward: 2 LN outputs + the FFN's gelu output + the 2 attention outputs (flash
+    # forward codes) = 5; backward: 3 dt + the FFN's hidden gradient + the 2 dQKV (flash backward
+    # codes) = 6. Step 0's backward slots are fresh (standalone current scaling), its forward
+    # producer slots file standalone codes.
+    assert hits_on == 5 + 2 * (5 + 6), hits_on
     for (ya, ga), (yb, gb) in zip(got, ref):
         torch.testing.assert_close(ya, yb, rtol=0, atol=0)
         for a, b in zip(ga, gb):
