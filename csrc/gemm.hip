@@ -42,6 +42,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 namespace apex {
@@ -1283,6 +1284,184 @@ __global__ void __launch_bounds__(W_THREADS, 2) gemm_w2g_kernel(const T* __restr
                          lane);
 }
 
+// ============================================================================================
+// "m32" variant of the 8-wave ping-pong kernel: identical tiles, LDS image, staging, phases, waits
+// and epilogue, but the fragments are v_mfma_f32_32x32x16 instead of 16x16x32. Per K-tile and
+// wave the 128 x 64 sub-tile is 4 x 2 blocks of 32 x 32 over 4 K-steps of 16: 32 MFMAs of 32
+// cycles (vs 64 of 16) against the same 24 ds_read_b128 (a 32 x 16 fragment is also 16 B per
+// lane: row rb + (lane & 31), K chunk 2 s + (lane >> 5), conflict-free under the same XOR
+// swizzle) — the LDS bytes per FLOP are fixed by the wave tile, not the fragment shape; what
+// changes is that each MFMA holds the SIMD's issue for 8 of 32 cycles instead of 8 of 16, so the
+// partner wave's ds_reads / glds issue gets 3x the free slots per MFMA
+// (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost'). Swapped operands as in the 16x16 kernel:
+// the accumulator of block (n-block jb, m-block ib) holds, in lane l, M-row 32 ib + (l & 31) and
+// N-columns 32 jb + 8 g + 4 (l >> 5) + e in register 4 g + e, which stage_acc32 writes into the
+// epilogue's LDS image (the shared epilogue() then runs unchanged with STAGED = true).
+typedef float f32x16g __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ f32x16g mfma32_bf16(const s16x8& a, const s16x8& b, const f32x16g& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+template <typename T>
+__device__ __forceinline__ void mainloop_m32(const T* __restrict__ A, const T* __restrict__ B, int M, int N, int K,
+                                             int64_t lda, int64_t ldb, int m0, int n0, char* smem, int wid, int wr,
+                                             int wc, int lane, f32x16g (&acc)[2][4]) {
+  constexpr int BKE = 64;
+  const int nt = K / BKE;
+  const int l32 = lane & 31, lh = lane >> 5;
+  stage_pieces<T, false>(A, lda, m0, M, 0, smem, wid, lane, 0);
+  stage_pieces<T, false>(A, lda, m0, M, 0, smem, wid, lane, 2);
+  stage_pieces<T, false>(B, ldb, n0, N, 0, smem + G_TILE_BYTES, wid, lane, 0);
+  stage_pieces<T, false>(B, ldb, n0, N, 0, smem + G_TILE_BYTES, wid, lane, 2);
+  if (nt > 1) {
+    stage_pieces<T, false>(B, ldb, n0, N, BKE, smem + G_BUF_BYTES + G_TILE_BYTES, wid, lane, 0);
+    stage_pieces<T, false>(B, ldb, n0, N, BKE, smem + G_BUF_BYTES + G_TILE_BYTES, wid, lane, 2);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  bar();
+  if (wr == 1) bar();
+
+  s16x8 fa[2][4], fb0[4], fb1[4];
+  for (int t = 0; t < nt; ++t) {
+    char* cur = smem + (t & 1) * G_BUF_BYTES;
+    char* oth = smem + ((t + 1) & 1) * G_BUF_BYTES;
+    const char* ta = cur;
+    const char* tb = cur + G_TILE_BYTES;
+    const bool ld_a = t + 1 < nt, ld_b = t + 2 < nt;
+    // p1: A rows 0..63 of the wave, B cols 0..31; stage A(t+1) pieces 0,1
+#pragma unroll
+    for (int s = 0; s < 4; ++s) fb0[s] = lds_frag(tb, wc * 64 + l32, 2 * s + lh);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) fa[i][s] = lds_frag(ta, wr * 128 + i * 32 + l32, 2 * s + lh);
+    if (ld_a) stage_pieces<T, false>(A, lda, m0, M, (t + 1) * BKE, oth, wid, lane, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) acc[0][i] = mfma32_bf16(fb0[s], fa[i][s], acc[0][i]);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+    // p2: B cols 32..63; stage A(t+1) pieces 2,3
+#pragma unroll
+    for (int s = 0; s < 4; ++s) fb1[s] = lds_frag(tb, wc * 64 + 32 + l32, 2 * s + lh);
+    if (ld_a) stage_pieces<T, false>(A, lda, m0, M, (t + 1) * BKE, oth, wid, lane, 2);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) acc[1][i] = mfma32_bf16(fb1[s], fa[i][s], acc[1][i]);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+    // p3: A rows 64..127; stage B(t+2) pieces 0,1 into this buffer
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) fa[i][s] = lds_frag(ta, wr * 128 + 64 + i * 32 + l32, 2 * s + lh);
+    if (ld_b) stage_pieces<T, false>(B, ldb, n0, N, (t + 2) * BKE, cur + G_TILE_BYTES, wid, lane, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) acc[1][2 + i] = mfma32_bf16(fb1[s], fa[i][s], acc[1][2 + i]);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+    // p4: stage B(t+2) pieces 2,3; retire A(t+1), B(t+1)
+    if (ld_b) {
+      stage_pieces<T, false>(B, ldb, n0, N, (t + 2) * BKE, cur + G_TILE_BYTES, wid, lane, 2);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    bar();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) acc[0][2 + i] = mfma32_bf16(fb0[s], fa[i][s], acc[0][2 + i]);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+  }
+}
+
+// the m32 accumulators into the epilogue's LDS image (see stage_acc: element (row, col) of the
+// wave tile, col = 4 q + e, lives at row * 128 + ((q >> 1) ^ (row & 7)) * 16 + ((q & 1) ^ ((row >> 3) & 1)) * 8)
+template <typename T>
+__device__ __forceinline__ void stage_acc32(const f32x16g (&acc)[2][4], char* reg, int lane) {
+  const int l32 = lane & 31, lh = lane >> 5;
+#pragma unroll
+  for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+    for (int ib = 0; ib < 4; ++ib) {
+      const int row = ib * 32 + l32;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int chunk = (4 * jb + g) ^ (row & 7);
+        const int half = lh ^ ((row >> 3) & 1);
+        Pack<T, 4> pk;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pk.v[e] = from_f<T>(acc[jb][ib][4 * g + e]);
+        *reinterpret_cast<Pack<T, 4>*>(reg + row * 128 + chunk * 16 + half * 8) = pk;
+      }
+    }
+}
+
+template <typename T, int EPI, bool EDGE, int DBG = 0>
+__global__ void __launch_bounds__(G_THREADS) gemm_m32_kernel(const T* __restrict__ A, const T* __restrict__ B,
+                                                             T* __restrict__ C, int M, int N, int K, int64_t lda,
+                                                             int64_t ldb, int64_t ldc, const T* __restrict__ bias,
+                                                             const T* __restrict__ aux, int64_t ldaux,
+                                                             T* __restrict__ aux_out, float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) char smem[G_LDS_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+  const int tiles_m = (M + GB_M - 1) / GB_M, tiles_n = (N + GB_N - 1) / GB_N;
+  const int nwg = tiles_m * tiles_n;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
+  const int wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  const int group = G_GROUP_M * tiles_n;
+  const int first_m = (wg / group) * G_GROUP_M;
+  const int gm = min(tiles_m - first_m, G_GROUP_M);
+  const int tm = first_m + (wg % group) % gm;
+  const int tn = (wg % group) / gm;
+  const int m0 = tm * GB_M, n0 = tn * GB_N;
+  f32x16g acc[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[j][i] = f32x16g{};
+  mainloop_m32<T>(A, B, M, N, K, lda, ldb, m0, n0, smem, wid, wr, wc, lane, acc);
+  if (wr == 0) bar();
+  bar();
+  if constexpr (DBG & 512) {  // keep the accumulators live, store nothing
+    float t = 0.f;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) t += acc[j][i][e];
+    if (t == 1.2345e-30f) C[0] = from_f<T>(t);
+    return;
+  }
+  char* reg = smem + wid * 16384;
+  stage_acc32<T>(acc, reg, lane);
+  const f32x4 dummy[4][8] = {};
+  epilogue<T, EPI, EDGE, 0, 4, true>(dummy, reg, C, M, N, ldc, bias, aux, ldaux, aux_out, part, m0, n0, tm, wr, wc,
+                                     lane);
+}
+
 // 2-D transpose out[C][R] = in[R][C] (16-bit elements). Each lane transposes an 8x8 block in
 // registers: 8 x 16-B row loads, 8 x 16-B row stores. A wave is 8 (along C) x 8 (along R) blocks,
 // so every load and every store instruction moves whole 128-B row runs. Edge blocks fall back to
@@ -1330,9 +1509,47 @@ inline int host_stagger(int epi) {
   return table[epi];
 }
 
+// epilogues that run on the 32x32x16-fragment kernel (gemm_m32_kernel), bf16 NT only: bit EPI of
+// APEX_GEMM_M32 ("all", "none" or a comma list of epilogue ids; read once), default kM32Default
+constexpr int kM32Default = 0;
+inline bool host_m32(int epi) {
+  static int mask = -1;
+  if (mask == -1) {
+    mask = kM32Default;
+    if (const char* e = getenv("APEX_GEMM_M32")) {
+      if (!strcmp(e, "all")) {
+        mask = 0xffff;
+      } else {
+        mask = 0;
+        const char* p = e;
+        while (*p) {
+          int ep = 0;
+          if (sscanf(p, "%d", &ep) == 1 && ep >= 0 && ep < 16) mask |= 1 << ep;
+          while (*p && *p != ',') ++p;
+          if (*p == ',') ++p;
+        }
+      }
+    }
+  }
+  return (mask >> epi) & 1;
+}
+
 template <typename T, int EPI, bool TR = false>
 void launch_gemm(const GemmArgs& g, hipStream_t s) {
   const int tiles = ((g.M + GB_M - 1) / GB_M) * ((g.N + GB_N - 1) / GB_N);
+  if constexpr (!TR && std::is_same<T, bf16>::value && EPI != EPI_F32 && EPI != EPI_F32_ACC) {
+    if (host_m32(EPI)) {
+      if (g.M % GB_M != 0 || g.N % GB_N != 0)
+        hipLaunchKernelGGL((gemm_m32_kernel<T, EPI, true>), dim3(tiles), dim3(G_THREADS), 0, s, (const T*)g.A,
+                           (const T*)g.B, (T*)g.C, g.M, g.N, g.K, g.lda, g.ldb, g.ldc, (const T*)g.bias,
+                           (const T*)g.aux, g.ldaux, (T*)g.aux_out, g.part);
+      else
+        hipLaunchKernelGGL((gemm_m32_kernel<T, EPI, false>), dim3(tiles), dim3(G_THREADS), 0, s, (const T*)g.A,
+                           (const T*)g.B, (T*)g.C, g.M, g.N, g.K, g.lda, g.ldb, g.ldc, (const T*)g.bias,
+                           (const T*)g.aux, g.ldaux, (T*)g.aux_out, g.part);
+      return;
+    }
+  }
   const int units = h_gemm_stagger > 0 ? h_gemm_stagger : h_gemm_stagger < 0 ? 0 : host_stagger(EPI);
   const int stagger = (units & 0xffff) | (h_gemm_dbg << 16);  // the kernel's ctl word
   const bool edge = !TR && (g.M % GB_M != 0 || g.N % GB_N != 0);  // (gemm_tt shapes are tile multiples)
