@@ -183,7 +183,42 @@ struct DropStream {
     }
     return out << (4 * hl);
   }
+  // half_bits plus the same decisions as byte masks for the P operand: byte b of bm[j] is 0xFF
+  // iff element 4 b + j of the lane's 16 (key j + 8 b + 4 hl of the block) is kept. The forward
+  // ANDs them into the packed bf16 P words (drop_pack): one v_perm + one v_and per pair of
+  // probabilities instead of a bit test, compare and select per element on the fp32 values (which
+  // also split the v_cvt_pk pairs: BERT-shape forward, 19 VALU instructions per score).
+  __device__ __forceinline__ uint32_t half_masks(int hl, uint32_t (&bm)[4]) {
+    const uint32_t C = (256u - thresh) * 0x01010101u;
+    const uint32_t C7 = C & 0x7f7f7f7fu;
+    uint32_t out = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t u = next();
+      const uint32_t s7 = (u & 0x7f7f7f7fu) + C7;
+      const uint32_t carry = ((u & C) | ((u | C) & s7)) & 0x80808080u;
+      out |= carry >> (7 - j);
+      bm[j] = carry | (carry - (carry >> 7));  // 0x80 -> 0xFF per kept byte (no borrow across bytes)
+    }
+    return out << (4 * hl);
+  }
 };
+
+// Dropout on 8 packed 16-bit probabilities (elements 8 s2 .. 8 s2 + 7 of a lane's 16, word w =
+// elements 2w, 2w + 1): word w &= the byte masks of its two elements, gathered by v_perm_b32
+// (bytes 0-1 <- byte b of bm[j], bytes 2-3 <- byte b of bm[j + 1], b = (8 s2 + 2w) >> 2)
+template <typename V8>
+__device__ __forceinline__ V8 drop_pack(V8 pf, const uint32_t (&bm)[4], int s2) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 w = __builtin_bit_cast(u32x4, pf);
+#pragma unroll
+  for (int ww = 0; ww < 4; ++ww) {
+    const uint32_t b = 2 * s2 + (ww >> 1), j = 2 * (ww & 1);
+    const uint32_t sel = b | (b << 8) | ((4 + b) << 16) | ((4 + b) << 24);
+    w[ww] &= __builtin_amdgcn_perm(bm[j + 1], bm[j], sel);
+  }
+  return __builtin_bit_cast(V8, w);
+}
 
 // keep bits of block `blk` (bit k <-> key 32 blk + k) for one row, both halves (debug / test kernel)
 __device__ __forceinline__ uint32_t drop_block_bits(uint64_t seed, uint64_t offset, uint32_t thresh, int64_t bh,
@@ -329,15 +364,14 @@ attn_fwd_kernel(AttnArgs a) {
   // math of key tile kt, read from LDS rows lr0 ..; mid() runs right after the S products (DB)
   auto compute = [&](const int kt, auto&& mid) {
     const int lr0 = SHORT ? kt * kFwdKB : DB ? (kt & 1) * kFwdKB : 0;
-    uint32_t mcur[2] = {0u, 0u};
+    uint32_t bm[2][4];
     if (DROPOUT) {
 #pragma unroll
       for (int sb = 0; sb < 2; ++sb) {
         const int blk = (kt * kFwdKB >> 5) + sb;
-        const uint32_t hb = dg.half_bits(hl);  // block blk's bits at 4 hl + {0-3, 8-11, ..}
+        const uint32_t hb = dg.half_masks(hl, bm[sb]);  // block blk's bits at 4 hl + {0-3, 8-11, ..}
         const uint32_t word = hb | xor32_u(hb);
         if (hl == 0 && mrow && blk * 32 < a.Sk) mrow[blk] = word;
-        mcur[sb] = hb >> (4 * hl);
       }
     }
     const int kb = kt * kFwdKB;
@@ -432,12 +466,9 @@ attn_fwd_kernel(AttnArgs a) {
       for (int i = 0; i < 16; ++i) {
         const float p = __builtin_amdgcn_exp2f(fmaf(st[sb][i], sl2, mscaled));
         psum += p;
-        // dropped: keep bit i selects p or +0 (bfe sign-extends the bit to an all-ones mask);
-        // the 1/(1-p) rescale is applied once in the epilogue
-        // element i = key (i & 3) + 8 (i >> 2) + 4 hl: bit (i & 3) + 8 (i >> 2) of the shifted word
-        st[sb][i] = DROPOUT ? __builtin_bit_cast(float, __builtin_bit_cast(int, p) &
-                                                            __builtin_amdgcn_sbfe((int)mcur[sb], (i & 3) + 8 * (i >> 2), 1))
-                            : p;
+        // dropout is applied to the packed P operand below (drop_pack); the 1/(1-p) rescale once
+        // in the epilogue
+        st[sb][i] = p;
       }
     }
     l = l * alpha + psum;
@@ -453,7 +484,8 @@ attn_fwd_kernel(AttnArgs a) {
         float pv[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) pv[j] = st[sb][8 * s2 + j];
-        const V8 pf = pack8<T, V8>(pv);
+        V8 pf = pack8<T, V8>(pv);
+        if constexpr (DROPOUT) pf = drop_pack(pf, bm[sb], s2);
         const int k0 = lr0 + 32 * sb + 16 * s2 + 4 * hl + ((lane & 15) >> 2);
 #pragma unroll
         for (int db = 0; db < D / 32; ++db) {

@@ -561,9 +561,13 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[NJ][8], char* reg, T
           } else if constexpr (GELU_FWD) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] += bv[e];
-            const u32x4 hraw = pack(v);
-            if constexpr (!GELU_D) st(rs_o, slot, hraw);
-            unpack(hraw, v);  // GELU of the (rounded) pre-activation, as the unfused composition
+            if constexpr (!GELU_D) {
+              const u32x4 hraw = pack(v);
+              st(rs_o, slot, hraw);
+              unpack(hraw, v);  // GELU of the stored (rounded) pre-activation: what the backward's dGELU sees
+            }
+            // GELU_D stores no pre-activation: gelu and gelu' both come from the fp32 H here (no
+            // round trip through 16 bits: 12 VALU instructions per 8 elements fewer)
             float gd[8];
 #pragma unroll
             for (int e = 0; e < 8; e += 2) {

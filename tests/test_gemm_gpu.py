@@ -92,13 +92,15 @@ def _gelu_grad_ref(h, tanh):
 @pytest.mark.parametrize("tanh", [False, True])
 @pytest.mark.parametrize("M,N,K", [(1000, 1600, 1600), (4096, 4096, 1024), (300, 200, 128)])
 def test_gemm_bias_gelu_stores_derivative(M, N, K, tanh):
-    """EPI_BIAS_GELU_D: y = gelu(h), aux = gelu'(h) at the rounded h (fp32 reference)."""
+    """EPI_BIAS_GELU_D: y = gelu(h), aux = gelu'(h) (fp32 reference). h = the GEMM output rounded
+    to 16 bits (the epilogue's LDS transposition) + bias, NOT rounded again: no pre-activation is
+    stored, so the kernel evaluates gelu / gelu' on the fp32 sum."""
     C = _C()
     a = (torch.randn(M, K, device=DEV) / K ** 0.5).bfloat16()
     b = torch.randn(N, K, device=DEV).bfloat16()
     bias = torch.randn(N, device=DEV).bfloat16()
     y, gd = C.gemm(a, b, C.EPI_BIAS_GELU_TANH_D if tanh else C.EPI_BIAS_GELU_D, bias)
-    href = (_ref_mm(a, b) + bias.float()).bfloat16().float()  # the kernel rounds h first
+    href = _ref_mm(a, b).bfloat16().float() + bias.float()
     _close(y, F.gelu(href, approximate="tanh" if tanh else "none"), 1.5e-2)
     _close(gd, _gelu_grad_ref(href, tanh), 1.5e-2)
 
