@@ -12,15 +12,16 @@ Every bf16/fp16 device call runs the MFMA flash-attention kernels in apex._C
 * ``attn_bias``: an additive score bias broadcastable to [B, h, Sq, Sk] (attention masks as
   -inf, ALiBi, relative-position biases) is added inside the kernel — no [B, h, Sq, Sk] score
   tensor is materialised; a boolean mask follows scaled_dot_product_attention's convention
-  (True = attend) and becomes a 0 / -inf bias;
+  (True = attend) and becomes a 0 / -inf bias. A bias that requires a gradient gets it from the
+  backward kernels: dS written into an fp32 tensor of the bias's (broadcast) shape, atomically
+  added over the broadcast dims;
 * ``k_lens``: per-batch valid key lengths (right padding) skip whole key tiles.
 
 fp32 device inputs (head dims up to 128) run the f32-MFMA flash kernels (csrc/attention_f32.hip:
 exact f32 products and accumulation, the same masks / bias / dropout semantics).
 
-Device calls the flash kernels do not take — fp32 head dims > 128, head dims > 256, an
-``attn_bias`` that itself requires a gradient (the kernels treat the bias as a constant) — run
-the query-blocked memory-efficient path (``chunked.chunked_attention``: O(S * block) memory, backward by
+Device calls the flash kernels do not take — fp32 head dims > 128, head dims > 256 — run the
+query-blocked memory-efficient path (``chunked.chunked_attention``: O(S * block) memory, backward by
 recomputation from the saved log-sum-exp, bias gradient = the score gradient), never the O(S^2)
 composition. The reference composition (``attention_reference``: matmul -> softmax in fp32 ->
 dropout -> matmul) runs on CPU tensors; ``APEX_ATTN_BACKEND=reference`` forces it (A/B, numerics
@@ -61,8 +62,6 @@ def _native_ok(t, bias):
             return False
     elif t.dtype not in (torch.float16, torch.bfloat16):
         return False
-    if bias is not None and bias.requires_grad and torch.is_grad_enabled():
-        return False
     C = _ext._load()
     return C is not None and hasattr(C, "flash_attn_fwd")
 
@@ -75,7 +74,8 @@ def prepare_bias(bias, B, H, Sq, Sk, dtype):
         return None
     if bias.dtype == torch.bool:
         bias = torch.zeros(bias.shape, dtype=dtype, device=bias.device).masked_fill(~bias, float("-inf"))
-    bias = bias.detach().to(dtype)
+    # (no detach: a trainable bias keeps its graph; the flash backward returns dS for this view)
+    bias = bias.to(dtype)
     while bias.dim() < 4:
         bias = bias.unsqueeze(0)
     if bias.shape[-1] != Sk:

@@ -18,9 +18,22 @@ def _seed_pair(p, device=None):
     return philox_seed_offset(device)
 
 
+def _dbias_buffer(ctx, bias, idx):
+    """Zeroed fp32 gradient buffer of the bias's (broadcast) sizes when the bias needs a gradient;
+    the backward kernels add dS into it."""
+    if bias is None or not ctx.needs_input_grad[idx]:
+        return None
+    return torch.zeros(bias.shape, dtype=torch.float32, device=bias.device)
+
+
+def _dbias_out(dbias, bias):
+    return None if dbias is None else dbias.to(bias.dtype)
+
+
 class FlashAttnFunc(torch.autograd.Function):
     """q, k, v: [B, S, H, D] views (D contiguous) -> o [B, Sq, H, D]; ``bias``: optional additive
-    score bias (apex.contrib.multihead_attn.attention.prepare_bias layout), a constant."""
+    score bias (apex.contrib.multihead_attn.attention.prepare_bias layout); when it requires a
+    gradient the backward returns dS reduced to its shape."""
 
     @staticmethod
     def forward(ctx, q, k, v, dropout_p, causal, scale, k_lens, bias=None):
@@ -41,9 +54,10 @@ class FlashAttnFunc(torch.autograd.Function):
         dq = torch.empty_like(q, memory_format=torch.contiguous_format) if not q.is_contiguous() else torch.empty_like(q)
         dk = torch.empty_like(k, memory_format=torch.contiguous_format) if not k.is_contiguous() else torch.empty_like(k)
         dv = torch.empty_like(v, memory_format=torch.contiguous_format) if not v.is_contiguous() else torch.empty_like(v)
+        dbias = _dbias_buffer(ctx, bias, 7)
         C.flash_attn_bwd(do, q, k, v, o, lse, dq, dk, dv, bool(causal), float(scale), float(p), seed,
-                         offset, k_lens, dmask, None, 0, bias)
-        return dq, dk, dv, None, None, None, None, None
+                         offset, k_lens, dmask, None, 0, bias, dbias=dbias)
+        return dq, dk, dv, None, None, None, None, _dbias_out(dbias, bias)
 
 
 class FlashAttnPackedFunc(torch.autograd.Function):
@@ -71,9 +85,10 @@ class FlashAttnPackedFunc(torch.autograd.Function):
         q, k, v = qkv.unbind(2)
         dqkv = torch.empty(qkv.shape, dtype=qkv.dtype, device=qkv.device)
         dq, dk, dv = dqkv.unbind(2)
+        dbias = _dbias_buffer(ctx, bias, 5)
         C.flash_attn_bwd(do, q, k, v, o, lse, dq, dk, dv, bool(causal), float(scale), float(p), seed,
-                         offset, k_lens, dmask, None, 0, bias)
-        return dqkv, None, None, None, None, None
+                         offset, k_lens, dmask, None, 0, bias, dbias=dbias)
+        return dqkv, None, None, None, None, _dbias_out(dbias, bias)
 
 
 def flash_attention_packed(qkv, dropout_p=0.0, causal=False, scale=None, k_lens=None, bias=None):

@@ -342,6 +342,18 @@ __global__ void __launch_bounds__(256) attn_f32_bwd_dkdv_kernel(AttnArgs a, cons
         ds[i] = pv * (dpv - del[e]);
       }
     }
+    if (BIAS && a.dbias) {  // trainable bias: its gradient is dS (see attention_impl.h)
+      float* dcol = a.dbias + b * a.dbias_bs + h * a.dbias_hs + key;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int q = qb + kappa(i, hl);
+        if (q < a.Sq && key < a.Sk) {
+          float* dst = dcol + (int64_t)q * a.dbias_qs;
+          if (a.dbias_atomic) atomicAdd(dst, ds[i]);
+          else *dst = ds[i];
+        }
+      }
+    }
     mm_acc<D>(lds_dot, r, hl, p, dvt);   // dV^T += dO^T . P (dropped: the 1/(1-p) in the epilogue)
     mm_acc<D>(lds_qt, r, hl, ds, dkt);   // dK^T += (scale Q)^T . dS
   }

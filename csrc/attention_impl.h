@@ -875,6 +875,22 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
       elementwise(std::false_type{});
     else
       elementwise(std::true_type{});
+    if constexpr (BIAS) {
+      // trainable bias: its gradient is dS (natural domain, before the softmax scale). Lanes of a
+      // half hold 32 consecutive keys of one query row per element: coalesced 128-B runs.
+      if (a.dbias && mykey < a.Sk) {
+        float* dcol = a.dbias + b * a.dbias_bs + h * a.dbias_hs + mykey;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int q = qb + 8 * (i >> 2) + 4 * hl + (i & 3);
+          if (q < nq) {
+            float* dst = dcol + (int64_t)q * a.dbias_qs;
+            if (a.dbias_atomic) atomicAdd(dst, ds[i]);
+            else *dst = ds[i];
+          }
+        }
+      }
+    }
     // dV += P^T . dO : accumulator-as-A (contraction over q = rows), B = dO via tr reads
     // dK += dS^T . Q : same with Q
 #pragma unroll

@@ -422,10 +422,25 @@ bool flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor 
                     const c10::optional<Tensor>& dmask, const c10::optional<Tensor>& dsum, int64_t dbg,
                     const c10::optional<Tensor>& bias, const c10::optional<Tensor>& q8_dq,
                     const c10::optional<Tensor>& q8_dk, const c10::optional<Tensor>& q8_dv,
-                    const c10::optional<Tensor>& q8_scale, const c10::optional<Tensor>& q8_amax, int64_t q8_fmt) {
+                    const c10::optional<Tensor>& q8_scale, const c10::optional<Tensor>& q8_amax, int64_t q8_fmt,
+                    const c10::optional<Tensor>& dbias) {
   apex::AttnArgs a = attn_common(q, k, v, causal, scale, p_drop, seed, offset, k_lens);
   a.dbg = (int)dbg;
   attn_set_bias(a, bias, q);
+  if (dbias.has_value() && dbias->defined()) {
+    // gradient of a trainable bias: a zeroed fp32 tensor with the bias's sizes, contiguous; the
+    // kernels add dS into it (atomically where the bias broadcasts over batch, heads or queries)
+    const Tensor& t = *dbias;
+    TORCH_CHECK(a.bias, "flash_attn_bwd: dbias needs the bias");
+    TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.dim() == 4 &&
+                    t.sizes() == bias->sizes(),
+                "flash_attn_bwd: dbias must be a zeroed contiguous fp32 tensor of the bias's sizes");
+    a.dbias = t.data_ptr<float>();
+    a.dbias_bs = t.size(0) == 1 ? 0 : t.stride(0);
+    a.dbias_hs = t.size(1) == 1 ? 0 : t.stride(1);
+    a.dbias_qs = t.size(2) == 1 ? 0 : t.stride(2);
+    a.dbias_atomic = (t.size(0) == 1 && a.B > 1) || (t.size(1) == 1 && a.H > 1) || (t.size(2) == 1 && a.Sq > 1);
+  }
   TORCH_CHECK(!(a.bias && dsum.has_value() && dsum->defined()), "flash_attn_bwd: dsum with a score bias is not supported");
   if (dsum.has_value() && dsum->defined()) {
     TORCH_CHECK(dsum->is_cuda() && dsum->scalar_type() == at::kFloat && dsum->is_contiguous() &&
@@ -1433,7 +1448,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("scale"), py::arg("p_drop"), py::arg("seed"), py::arg("offset"), py::arg("k_lens"),
         py::arg("dmask"), py::arg("dsum") = py::none(), py::arg("dbg") = 0, py::arg("bias") = py::none(),
         py::arg("q8_dq") = py::none(), py::arg("q8_dk") = py::none(), py::arg("q8_dv") = py::none(),
-        py::arg("q8_scale") = py::none(), py::arg("q8_amax") = py::none(), py::arg("q8_fmt") = 0);
+        py::arg("q8_scale") = py::none(), py::arg("q8_amax") = py::none(), py::arg("q8_fmt") = 0,
+        py::arg("dbias") = py::none());
   m.def("partial_colsum", &k_partial_colsum, py::arg("part"), py::arg("out_dtype"), py::arg("out") = py::none());
   m.def("flash_dropout_mask", &flash_dropout_mask);
   m.def("lse_merge", &k_lse_merge, py::arg("acc_o"), py::arg("acc_lse"), py::arg("o"), py::arg("lse"),

@@ -101,6 +101,12 @@ struct AttnArgs {
                          // of dq, dk, dv — the packed-QKV projection's bias gradient, per batch
   const void* bias;      // optional additive score bias (input dtype), element (b, h, q, key) at
   int64_t bias_bs, bias_hs, bias_qs;  // b*bias_bs + h*bias_hs + q*bias_qs + key (0 = broadcast)
+  // optional gradient of a trainable bias (backward): fp32, element (b, h, q, key) at
+  // b*dbias_bs + h*dbias_hs + q*dbias_qs + key; the score gradient dS (natural domain, before the
+  // softmax scale) is stored there, or atomically added when a dimension is broadcast (dbias_atomic)
+  float* dbias;
+  int64_t dbias_bs, dbias_hs, dbias_qs;
+  int dbias_atomic;
   // fp8 producer-side codes (apex.fp8): the kernels also write fp8 codes of what they store, for the
   // GEMM that consumes it next (no standalone quantise pass): forward -> O (the attention-out GEMM's
   // e4m3 operand), backward -> dq / dk / dv (the QKV input-gradient GEMM's e5m2 operand). Each code
