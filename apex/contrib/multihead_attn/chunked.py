@@ -1,6 +1,7 @@
-"""Memory-efficient (query-blocked) attention for what the MFMA flash kernels do not take:
-fp32 inputs on the GPU, an ``attn_bias`` that requires a gradient (trainable ALiBi / relative
-position biases), head dims above 256.
+"""Memory-efficient (query-blocked) attention for what the MFMA flash kernels do not take: head
+dims above 256 (above 128 for fp32 inputs), ``APEX_ATTN_BACKEND=chunked`` / ``APEX_ATTN_F32=0``
+A/B runs. (Rounds 1-3 also sent fp32 inputs and trainable biases here; both now run on the
+kernels: csrc/attention_f32.hip, and the backward kernels' bias-gradient output.)
 
 The reference composition materialises the whole [B, h, Sq, Sk] score tensor (and autograd keeps
 the softmax AND the dropout mask for backward): O(S^2) memory, 2 GB for B*h = 64 at S = 2048 in
