@@ -1466,6 +1466,149 @@ __global__ void __launch_bounds__(G_THREADS) gemm_m32_kernel(const T* __restrict
                                      lane);
 }
 
+// ============================================================================================
+// "w8p": the 8-wave kernel without the ping-pong. Same 256 x 256 x 64 tiles, LDS image, glds
+// staging, wave tiles (128 x 64, 8 x 4 fragments of 16x16x32) and epilogue, but every wave
+// software-pipelines its own fragment reads one K-step (32 of K) ahead of its MFMAs, and the
+// workgroup meets at ONE barrier per K-tile instead of eight:
+//   k-step 0 of tile t: 32 MFMAs on F0(t) | the 12 ds_read_b128 of F1(t) interleaved
+//   vmcnt(0) (tile t+1 landed) + lgkmcnt(0) (F1(t) in registers) | barrier
+//   issue tile t+2's glds into tile t's buffer (free: every wave is past its reads of it)
+//   k-step 1 of tile t: 32 MFMAs on F1(t) | the 12 reads of F0(t+1) from the other buffer
+// The ping-pong's read sections end in lgkmcnt(0) + a barrier each, so their LDS latency (and the
+// 12-read section's queueing) is exposed whenever it outlasts the partner group's 16-MFMA section
+// (profiles/r3_gemmlab_w8_ablation.txt: no ds_read -29 %, i.e. the reads are not hidden). Here a
+// read has a whole K-step (32 MFMAs of its own wave, 64 on the SIMD) to land. Costs: 96 VGPRs of
+// double-buffered fragments next to the 128 accumulators, and tile t+1's copies get one K-tile
+// (~1 us) of flight time instead of the ping-pong's two for B.
+// Registers: fragments are double-buffered per HALF K-step (A: 4 row fragments of one 64-row half,
+// B: the 4 column fragments of one K-step), 64 VGPRs next to the 128 accumulators — a whole
+// K-step of both (96 VGPRs) did not fit the 256 of a two-waves-per-SIMD kernel (334 spilled).
+// Four stages per K-tile (K-step s, row half h), 16 MFMAs each, the next stage's fragments read
+// during the current one:
+//   (0,0) reads A(s0,h1)          (0,1) reads A(s1,h0) + B(s1)
+//   (1,0) reads A(s1,h1) | vmcnt(0) + lgkmcnt(0), barrier, glds of tile t+2 into this buffer
+//   (1,1) reads A(s0,h0) + B(s0) of tile t+1 from the other buffer
+template <int NI>
+__device__ __forceinline__ void w8p_fa(const char* buf, int wr, int h, int s, int lr, int lk, s16x8 (&fa)[NI]) {
+#pragma unroll
+  for (int i = 0; i < NI; ++i) fa[i] = frag<false>(buf, wr * 128 + h * 64 + i * 16, s, lr, lk);
+}
+__device__ __forceinline__ void w8p_fb(const char* buf, int wc, int s, int lr, int lk, s16x8 (&fb)[4]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) fb[j] = frag<false>(buf + G_TILE_BYTES, wc * 64 + j * 16, s, lr, lk);
+}
+
+// 16 MFMAs of one stage (rows of half h) with NR fragment reads interleaved
+template <typename T, int NR>
+__device__ __forceinline__ void w8p_stage(const s16x8 (&fa)[4], const s16x8 (&fb)[4], f32x4 (&acc)[4][8], int h) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[j][4 * h + i] = mfma16<T>(fb[j], fa[i], acc[j][4 * h + i]);
+  constexpr int PER = NR > 0 ? 16 / NR : 16;
+#ifndef W8P_NOSCHED
+#pragma unroll
+  for (int g = 0; g < NR; ++g) {
+    __builtin_amdgcn_sched_group_barrier(0x008, PER, 0);  // MFMA
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);        // DS read
+  }
+#endif
+}
+
+template <typename T>
+__device__ __forceinline__ void mainloop_w8p(const T* __restrict__ A, const T* __restrict__ B, int M, int N, int K,
+                                             int64_t lda, int64_t ldb, int m0, int n0, char* smem, int wid, int wr,
+                                             int wc, int lane, f32x4 (&acc)[4][8]) {
+  constexpr int BKE = 64;
+  const int nt = K / BKE;
+  const int lr = lane & 15, lk = lane >> 4;
+  auto stage_tile = [&](int t, char* buf) {
+    stage_pieces<T, false>(A, lda, m0, M, t * BKE, buf, wid, lane, 0);
+    stage_pieces<T, false>(A, lda, m0, M, t * BKE, buf, wid, lane, 2);
+    stage_pieces<T, false>(B, ldb, n0, N, t * BKE, buf + G_TILE_BYTES, wid, lane, 0);
+    stage_pieces<T, false>(B, ldb, n0, N, t * BKE, buf + G_TILE_BYTES, wid, lane, 2);
+  };
+  stage_tile(0, smem);
+  if (nt > 1) {
+    stage_tile(1, smem + G_BUF_BYTES);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // tile 0's 8 pieces (tile 1's stay in flight)
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  bar();
+  s16x8 fa0[4], fa1[4], fb0[4], fb1[4];
+  w8p_fa<4>(smem, wr, 0, 0, lr, lk, fa0);
+  w8p_fb(smem, wc, 0, lr, lk, fb0);
+  // unrolled by two so each half's buffers are compile-time (no per-iteration buffer select; the
+  // fragment registers keep their places across the back edge)
+  auto iter = [&](const int t, char* cur, char* nxt) {
+    w8p_fa<4>(cur, wr, 1, 0, lr, lk, fa1);  // (0,0): reads A(s0,h1)
+    w8p_stage<T, 4>(fa0, fb0, acc, 0);
+    w8p_fa<4>(cur, wr, 0, 1, lr, lk, fa0);  // (0,1): reads A(s1,h0) + B(s1)
+    w8p_fb(cur, wc, 1, lr, lk, fb1);
+    w8p_stage<T, 8>(fa1, fb0, acc, 1);
+    w8p_fa<4>(cur, wr, 1, 1, lr, lk, fa1);  // (1,0): reads A(s1,h1)
+    w8p_stage<T, 4>(fa0, fb1, acc, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tile t+1 landed (this wave's pieces)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of tile t retired
+    bar();
+    if (t + 2 < nt) stage_tile(t + 2, cur);
+    if (t + 1 < nt) {  // (1,1): reads A(s0,h0) + B(s0) of tile t+1
+      w8p_fa<4>(nxt, wr, 0, 0, lr, lk, fa0);
+      w8p_fb(nxt, wc, 0, lr, lk, fb0);
+      w8p_stage<T, 8>(fa1, fb1, acc, 1);
+    } else {
+      w8p_stage<T, 0>(fa1, fb1, acc, 1);
+    }
+  };
+  for (int t = 0; t < nt; t += 2) {
+    iter(t, smem, smem + G_BUF_BYTES);
+    if (t + 1 < nt) iter(t + 1, smem + G_BUF_BYTES, smem);
+  }
+}
+
+template <typename T, int EPI, bool EDGE, int DBG = 0>
+__global__ void __launch_bounds__(G_THREADS) gemm_w8p_kernel(const T* __restrict__ A, const T* __restrict__ B,
+                                                             T* __restrict__ C, int M, int N, int K, int64_t lda,
+                                                             int64_t ldb, int64_t ldc, const T* __restrict__ bias,
+                                                             const T* __restrict__ aux, int64_t ldaux,
+                                                             T* __restrict__ aux_out, float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) char smem[G_LDS_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+  const int tiles_m = (M + GB_M - 1) / GB_M, tiles_n = (N + GB_N - 1) / GB_N;
+  const int nwg = tiles_m * tiles_n;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
+  const int wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  const int group = G_GROUP_M * tiles_n;
+  const int first_m = (wg / group) * G_GROUP_M;
+  const int gm = min(tiles_m - first_m, G_GROUP_M);
+  const int tm = first_m + (wg % group) % gm;
+  const int tn = (wg % group) / gm;
+  const int m0 = tm * GB_M, n0 = tn * GB_N;
+  f32x4 acc[4][8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  mainloop_w8p<T>(A, B, M, N, K, lda, ldb, m0, n0, smem, wid, wr, wc, lane, acc);
+  bar();  // every wave is past its last ds_read: LDS is free for the epilogue
+  if constexpr (DBG & 512) {
+    float t = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) t += acc[j][i][0] + acc[j][i][1] + acc[j][i][2] + acc[j][i][3];
+    if (t == 1.2345e-30f) C[0] = from_f<T>(t);
+    return;
+  }
+  epilogue<T, EPI, EDGE, 0, 4, false>(acc, smem + wid * 16384, C, M, N, ldc, bias, aux, ldaux, aux_out, part, m0, n0,
+                                      tm, wr, wc, lane);
+}
+
 // 2-D transpose out[C][R] = in[R][C] (16-bit elements). Each lane transposes an 8x8 block in
 // registers: 8 x 16-B row loads, 8 x 16-B row stores. A wave is 8 (along C) x 8 (along R) blocks,
 // so every load and every store instruction moves whole 128-B row runs. Edge blocks fall back to

@@ -91,17 +91,25 @@ void launch_m32(const Bufs& b, hipStream_t s) {
                      b.K, (int64_t)b.K, (int64_t)b.K, (int64_t)b.N, b.bias, b.aux, (int64_t)b.N, b.aux_out, b.part);
 }
 
+template <int EPI, int DBG = 0>
+void launch_w8p(const Bufs& b, hipStream_t s) {
+  const int tiles = ((b.M + 255) / 256) * ((b.N + 255) / 256);
+  hipLaunchKernelGGL((gemm_w8p_kernel<bf16, EPI, false, DBG>), dim3(tiles), dim3(512), 0, s, b.A, b.B, b.C, b.M, b.N,
+                     b.K, (int64_t)b.K, (int64_t)b.K, (int64_t)b.N, b.bias, b.aux, (int64_t)b.N, b.aux_out, b.part);
+}
+
 template <int EPI>
 void run_epi(Bufs& b, int rounds, int reps, hipStream_t s) {
   struct V {
     const char* name;
     void (*fn)(const Bufs&, hipStream_t);
   };
-  std::vector<V> vs = {{"w8", launch_old<EPI>}, {"w8m32", launch_m32<EPI>}};
+  std::vector<V> vs = {{"w8", launch_old<EPI>}, {"w8p", launch_w8p<EPI>}};
+  if (getenv("LAB_M32")) vs.push_back({"w8m32", launch_m32<EPI>});
   if (getenv("LAB_W2G")) vs.push_back({"w2g", launch_w2g<EPI>});
   if (getenv("LAB_NOEPI")) {
     vs.push_back({"w8_noepi", launch_old<EPI, 512>});
-    vs.push_back({"w8m32_noepi", launch_m32<EPI, 512>});
+    vs.push_back({"w8p_noepi", launch_w8p<EPI, 512>});
   }
   if (getenv("LAB_W4")) {
     vs.push_back({"w4", launch_w4<EPI>});
