@@ -1523,11 +1523,26 @@ __device__ __forceinline__ void mainloop_w8p(const T* __restrict__ A, const T* _
   constexpr int BKE = 64;
   const int nt = K / BKE;
   const int lr = lane & 15, lk = lane >> 4;
+  // glds through buffer resources (wave-uniform bases in SGPRs, one 32-bit voffset per piece and
+  // lane, the K-tile in soffset; rows past M / N read zero): 64-bit flat addresses per piece were
+  // spilled to scratch here, and every reload's vmcnt(0) then also waited for the copies in flight
+  const __amdgpu_buffer_rsrc_t rsa =
+      wave_rsrc(A + (int64_t)m0 * lda, (uint32_t)(min(M - m0, GB_M) * lda * (int64_t)sizeof(T)));
+  const __amdgpu_buffer_rsrc_t rsb =
+      wave_rsrc(B + (int64_t)n0 * ldb, (uint32_t)(min(N - n0, GB_N) * ldb * (int64_t)sizeof(T)));
+  uint32_t va[4], vb[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    va[j] = piece_voff<T, false>(wid * 4 + j, lane, lda);
+    vb[j] = piece_voff<T, false>(wid * 4 + j, lane, ldb);
+  }
   auto stage_tile = [&](int t, char* buf) {
-    stage_pieces<T, false>(A, lda, m0, M, t * BKE, buf, wid, lane, 0);
-    stage_pieces<T, false>(A, lda, m0, M, t * BKE, buf, wid, lane, 2);
-    stage_pieces<T, false>(B, ldb, n0, N, t * BKE, buf + G_TILE_BYTES, wid, lane, 0);
-    stage_pieces<T, false>(B, ldb, n0, N, t * BKE, buf + G_TILE_BYTES, wid, lane, 2);
+    const uint32_t so = (uint32_t)(t * BKE * (int)sizeof(T));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bglds16(rsa, buf + (wid * 4 + j) * 1024, va[j], so);
+      bglds16(rsb, buf + G_TILE_BYTES + (wid * 4 + j) * 1024, vb[j], so);
+    }
   };
   stage_tile(0, smem);
   if (nt > 1) {
