@@ -166,27 +166,42 @@ def _blk_bwd(do, q, k, v, o, lse, causal, scale, p, aux):
     return dq, dk, dv
 
 
-def _merge(acc_o, acc_lse, o, lse):
-    """Fold one block's (o, lse) into the running fp32 (acc_o [B, S, H, D], acc_lse [B, H, S]).
+def _merge(acc_o, acc_lse, o, lse, s0=0, S=None):
+    """Fold one block's (o [B, Sb, H, D], lse [B, H, Sb]) into rows s0 .. s0 + Sb of the running fp32
+    accumulator (acc_o [B, S, H, D], acc_lse [B, H, S]; None before the first block).
 
-    On the GPU one HIP pass (csrc/context_parallel.hip: reads the accumulator and the block once,
-    writes the accumulator once); the torch composition below is the CPU / reference path."""
+    On the GPU one HIP pass (csrc/context_parallel.hip: reads the accumulator rows and the block
+    once, writes the rows once, in place — a step that sees only this rank's late chunk merges into
+    that half without chunk copies); the torch composition below is the CPU / reference path."""
+    S = o.shape[1] if S is None else S
+    covers = s0 == 0 and o.shape[1] == S
     if _native_merge(o, lse):
         C = _ext.require()
-        first = acc_o is None
-        if first:
-            acc_o = torch.empty(o.shape, dtype=torch.float32, device=o.device)
-            acc_lse = torch.empty(lse.shape, dtype=torch.float32, device=o.device)
-        C.lse_merge(acc_o, acc_lse, o, lse.contiguous(), first)
+        first = acc_o is None and covers
+        if acc_o is None:
+            B, _, H, D = o.shape
+            if covers:
+                acc_o = torch.empty(B, S, H, D, dtype=torch.float32, device=o.device)
+                acc_lse = torch.empty(B, H, S, dtype=torch.float32, device=o.device)
+            else:  # rows no block has reached yet: weight 0 (lse = -inf) in the merge
+                acc_o = torch.zeros(B, S, H, D, dtype=torch.float32, device=o.device)
+                acc_lse = torch.full((B, H, S), float("-inf"), dtype=torch.float32, device=o.device)
+        C.lse_merge(acc_o, acc_lse, o, lse.contiguous(), first, s0)
         return acc_o, acc_lse
     lse = torch.where(torch.isposinf(lse), torch.full_like(lse, float("-inf")), lse)  # empty rows
     if acc_o is None:
-        return _f(o), lse.clone()
-    new = torch.logaddexp(acc_lse, lse)
+        B, _, H, D = o.shape
+        acc_o = torch.zeros(B, S, H, D, dtype=_acc_dtype(o), device=o.device)
+        acc_lse = torch.full((B, H, S), float("-inf"), dtype=lse.dtype, device=o.device)
+    rows = slice(s0, s0 + o.shape[1])
+    a_lse = acc_lse[:, :, rows]
+    new = torch.logaddexp(a_lse, lse)
     safe = torch.where(torch.isneginf(new), torch.zeros_like(new), new)
-    w_old = torch.exp(acc_lse - safe).transpose(1, 2).unsqueeze(-1)
+    w_old = torch.exp(a_lse - safe).transpose(1, 2).unsqueeze(-1)
     w_new = torch.exp(lse - safe).transpose(1, 2).unsqueeze(-1)
-    return acc_o * w_old + _f(o) * w_new, new
+    acc_o[:, rows] = acc_o[:, rows] * w_old + _f(o) * w_new
+    acc_lse[:, :, rows] = new
+    return acc_o, acc_lse
 
 
 def _native_merge(o, lse):
@@ -241,8 +256,13 @@ def _step_calls(r, src, W, layout, causal):
 
 
 def _rows(t, sel, n, dim):
-    """Chunk ``sel`` of ``t`` along ``dim`` (``t`` itself for sel None), contiguous."""
-    return t if sel is None else t.chunk(n, dim=dim)[sel].contiguous()
+    """Chunk ``sel`` of ``t`` along ``dim`` (``t`` itself for sel None). A view along the sequence
+    dim (the flash kernels take [B, S, H, D] views with any 16-byte-aligned row strides); copied
+    along other dims (the [B, H, S] log-sum-exp, read contiguous)."""
+    if sel is None:
+        return t
+    c = t.chunk(n, dim=dim)[sel]
+    return c if dim == 1 else c.contiguous()
 
 
 class _Ring:
@@ -274,7 +294,8 @@ class _RingAttention(torch.autograd.Function):
         ring = _Ring(group, ranks, r)
         q_ids, _ = chunk_ids(r, W, layout)
         nq = len(q_ids)
-        acc = [[None, None] for _ in range(nq)]
+        S = q.shape[1]
+        acc_o = acc_lse = None  # fp32 [B, S, H, D] / [B, H, S] over all local query rows
         aux = {}
         cur = [k.contiguous(), v.contiguous()]
         for step in range(W):
@@ -284,16 +305,13 @@ class _RingAttention(torch.autograd.Function):
             for q_sel, k_sel, diag in _step_calls(r, src, W, layout, causal):
                 o, lse, a = _blk_fwd(_rows(q, q_sel, nq, 1), _rows(cur[0], k_sel, nk, 1), _rows(cur[1], k_sel, nk, 1),
                                      diag, scale, p)
-                sel = range(nq) if q_sel is None else [q_sel]
-                os_ = o.chunk(len(sel), dim=1) if q_sel is None else [o]
-                ls_ = lse.chunk(len(sel), dim=2) if q_sel is None else [lse]
-                for qi, oo, ll in zip(sel, os_, ls_):
-                    acc[qi][0], acc[qi][1] = _merge(acc[qi][0], acc[qi][1], oo.contiguous(), ll.contiguous())
+                s0 = 0 if q_sel is None else q_sel * (S // nq)
+                acc_o, acc_lse = _merge(acc_o, acc_lse, o, lse, s0, S)
                 aux[(step, q_sel, k_sel)] = a
             if nxt is not None:
                 cur = _Ring.finish(nxt)
-        out = torch.cat([a[0] for a in acc], dim=1).to(q.dtype)
-        lse = torch.cat([a[1] for a in acc], dim=2)
+        out = acc_o.to(q.dtype)
+        lse = acc_lse
         ctx.save_for_backward(q, k, v, out, lse)
         ctx.cfg = (group, ranks, r, causal, scale, p, layout)
         ctx.aux = aux

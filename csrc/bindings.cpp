@@ -1030,17 +1030,22 @@ Tensor k_smx_bwd(Tensor dy, Tensor y, double scale) {
 }
 
 // context parallelism: fused log-sum-exp merge of one ring-attention block into the fp32 accumulator
-void k_lse_merge(Tensor acc_o, Tensor acc_lse, Tensor o, Tensor lse, bool first) {
+// acc_o [B, Sa, H, D] / acc_lse [B, H, Sa] fp32 contiguous; the block o [B, S, H, D] / lse [B, H, S]
+// merges into accumulator rows s0 .. s0 + S
+void k_lse_merge(Tensor acc_o, Tensor acc_lse, Tensor o, Tensor lse, bool first, int64_t s0) {
   TORCH_CHECK(acc_o.is_cuda() && acc_o.scalar_type() == at::kFloat && acc_o.is_contiguous() && acc_o.dim() == 4,
               "lse_merge: acc_o fp32 [B,S,H,D] contiguous");
   TORCH_CHECK(acc_lse.scalar_type() == at::kFloat && acc_lse.is_contiguous() && lse.scalar_type() == at::kFloat &&
                   lse.is_contiguous(),
               "lse_merge: fp32 contiguous lse");
-  TORCH_CHECK(o.is_contiguous() && o.sizes() == acc_o.sizes(), "lse_merge: o like acc_o, contiguous");
-  const int64_t B = acc_o.size(0), S = acc_o.size(1), H = acc_o.size(2), D = acc_o.size(3);
-  TORCH_CHECK(acc_lse.numel() == B * H * S && lse.numel() == B * H * S, "lse_merge: lse [B,H,S]");
+  TORCH_CHECK(o.is_contiguous() && o.dim() == 4 && o.size(0) == acc_o.size(0) && o.size(2) == acc_o.size(2) &&
+                  o.size(3) == acc_o.size(3) && s0 >= 0 && s0 + o.size(1) <= acc_o.size(1),
+              "lse_merge: o [B, S, H, D] contiguous, rows s0 .. s0 + S of acc_o");
+  const int64_t B = o.size(0), S = o.size(1), H = o.size(2), D = o.size(3), Sa = acc_o.size(1);
+  TORCH_CHECK(acc_lse.numel() == B * H * Sa && lse.numel() == B * H * S, "lse_merge: lse [B,H,S]");
   check(apex::lse_merge(acc_o.data_ptr<float>(), acc_lse.data_ptr<float>(), o.data_ptr(), lse.data_ptr<float>(), B,
-                        (int)S, (int)H, (int)D, first ? 1 : 0, dt_code(o.scalar_type()), cur_stream()),
+                        (int)S, (int)H, (int)D, first ? 1 : 0, dt_code(o.scalar_type()), cur_stream(), (int)Sa,
+                        (int)s0),
         "lse_merge");
 }
 
@@ -1453,7 +1458,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("partial_colsum", &k_partial_colsum, py::arg("part"), py::arg("out_dtype"), py::arg("out") = py::none());
   m.def("flash_dropout_mask", &flash_dropout_mask);
   m.def("lse_merge", &k_lse_merge, py::arg("acc_o"), py::arg("acc_lse"), py::arg("o"), py::arg("lse"),
-        py::arg("first"));
+        py::arg("first"), py::arg("s0") = 0);
   m.def("weight_norm_fwd", &k_wn_fwd);
   m.def("weight_norm_bwd", &k_wn_bwd);
   m.def("lstm_cell_fwd", &k_lstm_fwd);

@@ -134,7 +134,7 @@ int attn_bwd(const AttnArgs& a, const void* dout, float* delta_ws, void* dk, voi
 // context parallelism: acc (fp32 [B,S,H,D] + lse [B,H,S]) <- exact log-sum-exp merge with one block's
 // (o [B,S,H,D] in dt, lse [B,H,S]); first = 1 initialises the accumulator from the block
 int lse_merge(float* acc_o, float* acc_lse, const void* o, const float* lse, int64_t B, int S, int H, int D,
-              int first, int dt, hipStream_t s);
+              int first, int dt, hipStream_t s, int Sa = 0, int s0 = 0);
 int attn_dropout_mask(uint8_t* out, int64_t BH, int Sq, int Sk, uint64_t seed, uint64_t offset,
                       uint32_t thresh, hipStream_t s);
 

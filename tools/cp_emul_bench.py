@@ -56,22 +56,20 @@ def main():
         # step (_step_calls), the fused merges, the block backward and the partial adds
         for r in range(W):
             ql, _, _, dol = local[r]
-            acc = [[None, None], [None, None]]
+            acc_o = acc_l = None
             aux = {}
+            Sl = ql.shape[1]
             for step in range(W):
                 src = (r - step) % W
                 kl_, vl = local[src][1], local[src][2]
                 for q_sel, k_sel, diag in cp._step_calls(r, src, W, "zigzag", True):
                     o, lse, x = cp._blk_fwd(cp._rows(ql, q_sel, 2, 1), cp._rows(kl_, k_sel, 2, 1),
                                             cp._rows(vl, k_sel, 2, 1), diag, scale, 0.0)
-                    sel = range(2) if q_sel is None else [q_sel]
-                    os_ = o.chunk(2, dim=1) if q_sel is None else [o]
-                    ls_ = lse.chunk(2, dim=2) if q_sel is None else [lse]
-                    for qi, oo, ll in zip(sel, os_, ls_):
-                        acc[qi][0], acc[qi][1] = cp._merge(acc[qi][0], acc[qi][1], oo.contiguous(), ll.contiguous())
+                    s0 = 0 if q_sel is None else q_sel * (Sl // 2)
+                    acc_o, acc_l = cp._merge(acc_o, acc_l, o, lse, s0, Sl)
                     aux[(step, q_sel, k_sel)] = x
-            out = torch.cat([ac[0] for ac in acc], dim=1).to(q.dtype)
-            lse = torch.cat([ac[1] for ac in acc], dim=2).contiguous()
+            out = acc_o.to(q.dtype)
+            lse = acc_l
             dq = torch.zeros_like(ql, dtype=torch.float32)
             for step in range(W):
                 src = (r - step) % W
