@@ -141,3 +141,31 @@ def test_ring_attention_cp1_without_process_group(causal):
     want.backward(do)
     for a, b in zip(leaves, ref):
         torch.testing.assert_close(a.grad, b.grad)
+
+
+def test_merge_into_row_range_matches_whole_merge():
+    """_merge with a row offset (a zigzag step that reaches only the late chunk merges into that half
+    of the accumulator) equals merging the same block padded to all rows with -inf elsewhere."""
+    from apex.transformer import context_parallel as cp
+
+    g = torch.Generator().manual_seed(0)
+    B, S, H, D = 2, 8, 3, 16
+    o0 = torch.randn(B, S, H, D, generator=g, dtype=torch.float64)
+    l0 = torch.randn(B, H, S, generator=g, dtype=torch.float64)
+    o1 = torch.randn(B, S // 2, H, D, generator=g, dtype=torch.float64)
+    l1 = torch.randn(B, H, S // 2, generator=g, dtype=torch.float64)
+    l1[0, 1, 2] = float("inf")  # a row with no visible key in this block (flash marks it +inf)
+    acc_o, acc_l = cp._merge(None, None, o0, l0, 0, S)
+    acc_o, acc_l = cp._merge(acc_o, acc_l, o1, l1, S // 2, S)
+    # reference: the block padded to all rows, -inf (no contribution) on the early half
+    op = torch.cat([torch.zeros_like(o1), o1], dim=1)
+    lp = torch.cat([torch.full_like(l1, float("-inf")), torch.where(torch.isposinf(l1), torch.full_like(l1, float("-inf")), l1)], dim=2)
+    ref_l = torch.logaddexp(l0, lp)
+    w0 = torch.exp(l0 - ref_l).transpose(1, 2).unsqueeze(-1)
+    w1 = torch.exp(lp - ref_l).transpose(1, 2).unsqueeze(-1)
+    ref_o = o0 * w0 + op * w1
+    torch.testing.assert_close(acc_l, ref_l)
+    torch.testing.assert_close(acc_o, ref_o)
+    # first block covering only part of the rows: the rest stay empty (lse -inf, output 0)
+    a_o, a_l = cp._merge(None, None, o1, l1, S // 2, S)
+    assert torch.isneginf(a_l[:, :, : S // 2]).all() and float(a_o[:, : S // 2].abs().max()) == 0.0

@@ -118,3 +118,25 @@ def test_lse_merge_kernel_matches_torch_merge(dt):
     torch.testing.assert_close(acc_l, ref_l, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(acc_o, ref_o, rtol=1e-5, atol=1e-5)
     assert torch.isneginf(acc_l[1, 2, 40:45]).all() and (acc_o[1, 40:45, 2] == 0).all()
+
+
+@pytest.mark.gpu
+def test_lse_merge_kernel_row_range_matches_cpu_merge():
+    """The HIP merge into a row range of a larger accumulator (s0 > 0, first block not covering all
+    rows) against the torch composition on the CPU."""
+    from apex.transformer import context_parallel as cp
+
+    torch.manual_seed(3)
+    B, S, H, D = 2, 64, 3, 64
+    o0 = torch.randn(B, S // 2, H, D)
+    l0 = torch.randn(B, H, S // 2) * 2
+    o1 = torch.randn(B, S, H, D)
+    l1 = torch.randn(B, H, S) * 2
+    l1[1, 0, 3:6] = float("inf")
+    steps = [(o0, l0, S // 2), (o1, l1, 0), (o0 * 0.5, l0 - 1.0, 0)]
+    g_o = g_l = c_o = c_l = None
+    for o, l, s0 in steps:
+        g_o, g_l = cp._merge(g_o, g_l, o.cuda().bfloat16(), l.cuda(), s0, S)
+        c_o, c_l = cp._merge(c_o, c_l, o.bfloat16().float(), l, s0, S)
+    torch.testing.assert_close(g_l.cpu(), c_l, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(g_o.cpu(), c_o, rtol=1e-5, atol=1e-5)
