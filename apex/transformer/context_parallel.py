@@ -255,6 +255,75 @@ def _step_calls(r, src, W, layout, causal):
     return [(qi, ki, diag) for qi, ki, diag in _pairs(*(chunk_ids(x, W, layout)[0] for x in (r, src)), causal)]
 
 
+# A non-causal ring-step block with fewer query waves (B*H*Sq/32) than this runs its key range as
+# two halves on two streams: at B*H = 20, S = 8192 over 4 ranks a step block is 640-1280 waves
+# against the chip's 1024 SIMDs (profiles/README.md, round 4), one launch cannot fill it.
+_KV_SPLIT_WAVES = 2048
+_side = {}
+
+
+def _kv_parts(q, k, diag):
+    if diag or not _native(q) or os.environ.get("APEX_CP_KV_SPLIT", "1") == "0":
+        return 1
+    B, Sq, H, _ = q.shape
+    waves = B * H * ((Sq + 31) // 32)
+    return 2 if waves < _KV_SPLIT_WAVES and k.shape[1] >= 256 and k.shape[1] % 2 == 0 else 1
+
+
+def _side_streams(device):
+    key = (device.type, device.index)
+    if key not in _side:
+        _side[key] = [torch.cuda.Stream(device=device) for _ in range(2)]
+    return _side[key]
+
+
+def _on_side_streams(device, fns):
+    """Run fns[i]() on side stream i (after the current stream's work), join, and return the results
+    with every tensor marked as used by the current stream (the caching allocator must not hand
+    their memory to the side streams while the current stream still reads it)."""
+    cur = torch.cuda.current_stream(device)
+    ss = _side_streams(device)
+    outs = []
+    for s in ss[:len(fns)]:
+        s.wait_stream(cur)
+    for fn, s in zip(fns, ss):
+        with torch.cuda.stream(s):
+            outs.append(fn())
+    for s in ss[:len(fns)]:
+        cur.wait_stream(s)
+    for res in outs:
+        for t in (res if isinstance(res, (tuple, list)) else (res,)):
+            if isinstance(t, torch.Tensor) and t.is_cuda:
+                t.record_stream(cur)
+            elif isinstance(t, (tuple, list)):
+                for u in t:
+                    if isinstance(u, torch.Tensor) and u.is_cuda:
+                        u.record_stream(cur)
+    return outs
+
+
+def _step_fwd(q, k, v, diag, scale, p):
+    """[(o, lse, aux, part)] of one ring-step block: one flash call (part None), or the two key
+    halves (part 0, 1) run concurrently; every entry merges into the same accumulator rows."""
+    n = _kv_parts(q, k, diag)
+    if n == 1:
+        return [_blk_fwd(q, k, v, diag, scale, p) + (None,)]
+    ks, vs = k.chunk(2, dim=1), v.chunk(2, dim=1)
+    res = _on_side_streams(q.device, [lambda i=i: _blk_fwd(q, ks[i], vs[i], False, scale, p) for i in range(2)])
+    return [r + (i,) for i, r in enumerate(res)]
+
+
+def _step_bwd(do, q, k, v, o, lse, diag, scale, p, parts):
+    """[(dq, dk, dv, part)] of one ring-step block (``parts``: its _step_fwd entries' (aux, part))."""
+    if parts[0][1] is None:
+        return [_blk_bwd(do, q, k, v, o, lse, diag, scale, p, parts[0][0]) + (None,)]
+    ks, vs = k.chunk(2, dim=1), v.chunk(2, dim=1)
+    lse = lse.contiguous()
+    res = _on_side_streams(q.device, [lambda a=a, i=i: _blk_bwd(do, q, ks[i], vs[i], o, lse, False, scale, p, a)
+                                      for a, i in parts])
+    return [r + (i,) for r, (_, i) in zip(res, parts)]
+
+
 def _rows(t, sel, n, dim):
     """Chunk ``sel`` of ``t`` along ``dim`` (``t`` itself for sel None). A view along the sequence
     dim (the flash kernels take [B, S, H, D] views with any 16-byte-aligned row strides); copied
@@ -303,11 +372,12 @@ class _RingAttention(torch.autograd.Function):
             nxt = ring.start(cur) if step < W - 1 else None  # the transfer overlaps this step's blocks
             nk = len(chunk_ids(src, W, layout)[0])
             for q_sel, k_sel, diag in _step_calls(r, src, W, layout, causal):
-                o, lse, a = _blk_fwd(_rows(q, q_sel, nq, 1), _rows(cur[0], k_sel, nk, 1), _rows(cur[1], k_sel, nk, 1),
-                                     diag, scale, p)
+                blocks = _step_fwd(_rows(q, q_sel, nq, 1), _rows(cur[0], k_sel, nk, 1), _rows(cur[1], k_sel, nk, 1),
+                                   diag, scale, p)
                 s0 = 0 if q_sel is None else q_sel * (S // nq)
-                acc_o, acc_lse = _merge(acc_o, acc_lse, o, lse, s0, S)
-                aux[(step, q_sel, k_sel)] = a
+                for o, lse, _, _ in blocks:
+                    acc_o, acc_lse = _merge(acc_o, acc_lse, o, lse, s0, S)
+                aux[(step, q_sel, k_sel)] = [(a, part) for _, _, a, part in blocks]
             if nxt is not None:
                 cur = _Ring.finish(nxt)
         out = acc_o.to(q.dtype)
@@ -336,20 +406,25 @@ class _RingAttention(torch.autograd.Function):
             nk = len(chunk_ids(src, W, layout)[0])
             grads = []
             for q_sel, k_sel, diag in _step_calls(r, src, W, layout, causal):
-                g = _blk_bwd(_rows(do, q_sel, nq, 1), _rows(q, q_sel, nq, 1), _rows(cur[0], k_sel, nk, 1),
-                             _rows(cur[1], k_sel, nk, 1), _rows(out, q_sel, nq, 1), _rows(lse, q_sel, nq, 2), diag,
-                             scale, p, ctx.aux.get((step, q_sel, k_sel)))
-                (dq if q_sel is None else dq.chunk(nq, dim=1)[q_sel]).add_(g[0])
-                grads.append((k_sel, g[1], g[2]))
+                gs = _step_bwd(_rows(do, q_sel, nq, 1), _rows(q, q_sel, nq, 1), _rows(cur[0], k_sel, nk, 1),
+                               _rows(cur[1], k_sel, nk, 1), _rows(out, q_sel, nq, 1), _rows(lse, q_sel, nq, 2), diag,
+                               scale, p, ctx.aux[(step, q_sel, k_sel)])
+                for g in gs:
+                    (dq if q_sel is None else dq.chunk(nq, dim=1)[q_sel]).add_(g[0])
+                    grads.append((k_sel, g[3], g[1], g[2]))
             # the shard's dK/dV partial from the previous ranks (zero at step 0) + this rank's blocks
             if dkv_pending is None:
                 dk_t = torch.zeros(k.shape, dtype=_dkv_transport_dtype(k), device=k.device)
                 dv_t = torch.zeros(v.shape, dtype=_dkv_transport_dtype(v), device=v.device)
             else:
                 dk_t, dv_t = _Ring.finish(dkv_pending)
-            for k_sel, gk, gv in grads:
-                (dk_t if k_sel is None else dk_t.chunk(nk, dim=1)[k_sel]).add_(gk)
-                (dv_t if k_sel is None else dv_t.chunk(nk, dim=1)[k_sel]).add_(gv)
+            for k_sel, part, gk, gv in grads:
+                tk = dk_t if k_sel is None else dk_t.chunk(nk, dim=1)[k_sel]
+                tv = dv_t if k_sel is None else dv_t.chunk(nk, dim=1)[k_sel]
+                if part is not None:  # one key half of a split block
+                    tk, tv = tk.chunk(2, dim=1)[part], tv.chunk(2, dim=1)[part]
+                tk.add_(gk)
+                tv.add_(gv)
             if W == 1:  # no ring: the only shard is this rank's own (nothing to send to itself)
                 dkv_pending = ([], [dk_t, dv_t])
                 continue

@@ -140,3 +140,30 @@ def test_lse_merge_kernel_row_range_matches_cpu_merge():
         c_o, c_l = cp._merge(c_o, c_l, o.bfloat16().float(), l, s0, S)
     torch.testing.assert_close(g_l.cpu(), c_l, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(g_o.cpu(), c_o, rtol=1e-5, atol=1e-5)
+
+
+def test_ring_step_key_split_on_two_streams_matches_flash(monkeypatch):
+    """A small non-causal step block runs as two key halves on two streams (_step_fwd / _step_bwd):
+    forward merged through the log-sum-exp, dQ summed, dK / dV per half — equal to one flash call."""
+    from apex.contrib.multihead_attn.flash import flash_attention
+    from apex.transformer import context_parallel as cp
+
+    torch.manual_seed(4)
+    q, k, v = (torch.randn(1, 512, 4, 64, device="cuda", dtype=torch.bfloat16) for _ in range(3))
+    assert cp._kv_parts(q, k, False) == 2
+    do = torch.randn_like(q)
+    res = {}
+    for split in ("1", "0"):
+        monkeypatch.setenv("APEX_CP_KV_SPLIT", split)
+        qa, ka, va = (t.clone().requires_grad_() for t in (q, k, v))
+        out = cp._RingAttention.apply(qa, ka, va, None, [0], 0, False, 0.125, 0.0, "contiguous")
+        out.backward(do)
+        torch.cuda.synchronize()
+        res[split] = (out.float(), qa.grad.float(), ka.grad.float(), va.grad.float())
+    qb, kb, vb = (t.clone().requires_grad_() for t in (q, k, v))
+    ref = flash_attention(qb, kb, vb, causal=False, scale=0.125)
+    ref.backward(do)
+    for got in res.values():
+        torch.testing.assert_close(got[0], ref.float(), atol=2e-2, rtol=2e-2)
+        for g, b in zip(got[1:], (qb, kb, vb)):
+            torch.testing.assert_close(g, b.grad.float(), atol=2e-2, rtol=2e-2)

@@ -63,11 +63,12 @@ def main():
                 src = (r - step) % W
                 kl_, vl = local[src][1], local[src][2]
                 for q_sel, k_sel, diag in cp._step_calls(r, src, W, "zigzag", True):
-                    o, lse, x = cp._blk_fwd(cp._rows(ql, q_sel, 2, 1), cp._rows(kl_, k_sel, 2, 1),
-                                            cp._rows(vl, k_sel, 2, 1), diag, scale, 0.0)
+                    blocks = cp._step_fwd(cp._rows(ql, q_sel, 2, 1), cp._rows(kl_, k_sel, 2, 1),
+                                          cp._rows(vl, k_sel, 2, 1), diag, scale, 0.0)
                     s0 = 0 if q_sel is None else q_sel * (Sl // 2)
-                    acc_o, acc_l = cp._merge(acc_o, acc_l, o, lse, s0, Sl)
-                    aux[(step, q_sel, k_sel)] = x
+                    for o, lse, _, _ in blocks:
+                        acc_o, acc_l = cp._merge(acc_o, acc_l, o, lse, s0, Sl)
+                    aux[(step, q_sel, k_sel)] = [(x, part) for _, _, x, part in blocks]
             out = acc_o.to(q.dtype)
             lse = acc_l
             dq = torch.zeros_like(ql, dtype=torch.float32)
@@ -77,12 +78,17 @@ def main():
                 dk_t = torch.zeros(kl_.shape, dtype=cp._dkv_transport_dtype(k), device=q.device)
                 dv_t = torch.zeros_like(dk_t)
                 for q_sel, k_sel, diag in cp._step_calls(r, src, W, "zigzag", True):
-                    g = cp._blk_bwd(cp._rows(dol, q_sel, 2, 1), cp._rows(ql, q_sel, 2, 1), cp._rows(kl_, k_sel, 2, 1),
-                                    cp._rows(vl, k_sel, 2, 1), cp._rows(out, q_sel, 2, 1), cp._rows(lse, q_sel, 2, 2),
-                                    diag, scale, 0.0, aux[(step, q_sel, k_sel)])
-                    (dq if q_sel is None else dq.chunk(2, dim=1)[q_sel]).add_(g[0])
-                    (dk_t if k_sel is None else dk_t.chunk(2, dim=1)[k_sel]).add_(g[1])
-                    (dv_t if k_sel is None else dv_t.chunk(2, dim=1)[k_sel]).add_(g[2])
+                    gs = cp._step_bwd(cp._rows(dol, q_sel, 2, 1), cp._rows(ql, q_sel, 2, 1), cp._rows(kl_, k_sel, 2, 1),
+                                      cp._rows(vl, k_sel, 2, 1), cp._rows(out, q_sel, 2, 1), cp._rows(lse, q_sel, 2, 2),
+                                      diag, scale, 0.0, aux[(step, q_sel, k_sel)])
+                    for g in gs:
+                        (dq if q_sel is None else dq.chunk(2, dim=1)[q_sel]).add_(g[0])
+                        tk = dk_t if k_sel is None else dk_t.chunk(2, dim=1)[k_sel]
+                        tv = dv_t if k_sel is None else dv_t.chunk(2, dim=1)[k_sel]
+                        if g[3] is not None:
+                            tk, tv = tk.chunk(2, dim=1)[g[3]], tv.chunk(2, dim=1)[g[3]]
+                        tk.add_(g[1])
+                        tv.add_(g[2])
 
     def bench(fn):
         for _ in range(2):
@@ -101,7 +107,8 @@ def main():
     print(json.dumps({"S": S, "W": W, "H": H, "D": D, "B": B, "full_flash_fwd_bwd_ms": round(t_full, 3),
                       "ring_all_ranks_ms": round(t_emul, 3), "overhead": round(t_emul / t_full - 1.0, 4),
                       "merge": "hip" if cp._native_merge(q, torch.empty(1, device=q.device)) else "torch",
-                      "dkv_transport": str(cp._dkv_transport_dtype(k)).replace("torch.", "")}), flush=True)
+                      "dkv_transport": str(cp._dkv_transport_dtype(k)).replace("torch.", ""),
+                      "kv_split": os.environ.get("APEX_CP_KV_SPLIT", "1")}), flush=True)
 
 
 if __name__ == "__main__":
