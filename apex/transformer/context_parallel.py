@@ -255,15 +255,18 @@ def _step_calls(r, src, W, layout, causal):
     return [(qi, ki, diag) for qi, ki, diag in _pairs(*(chunk_ids(x, W, layout)[0] for x in (r, src)), causal)]
 
 
-# A non-causal ring-step block with fewer query waves (B*H*Sq/32) than this runs its key range as
-# two halves on two streams: at B*H = 20, S = 8192 over 4 ranks a step block is 640-1280 waves
-# against the chip's 1024 SIMDs (profiles/README.md, round 4), one launch cannot fill it.
+# APEX_CP_KV_SPLIT=1: a non-causal ring-step block with fewer query waves (B*H*Sq/32) than this runs
+# its key range as two halves on two streams (at B*H = 20, S = 8192 over 4 ranks a step block is
+# 640-1280 waves against the chip's 1024 SIMDs). Off by default: measured SLOWER
+# (profiles/r4_cp_ring_emulation.jsonl: CP4 at S = 8192 144 % over one flash call with the split,
+# 84 % without) — the halves' launches did not overlap enough to pay for the extra merges, dQ adds
+# and stream joins of ~50-90 us blocks.
 _KV_SPLIT_WAVES = 2048
 _side = {}
 
 
 def _kv_parts(q, k, diag):
-    if diag or not _native(q) or os.environ.get("APEX_CP_KV_SPLIT", "1") == "0":
+    if diag or not _native(q) or os.environ.get("APEX_CP_KV_SPLIT", "0") != "1":
         return 1
     B, Sq, H, _ = q.shape
     waves = B * H * ((Sq + 31) // 32)

@@ -108,7 +108,7 @@ def main():
                       "ring_all_ranks_ms": round(t_emul, 3), "overhead": round(t_emul / t_full - 1.0, 4),
                       "merge": "hip" if cp._native_merge(q, torch.empty(1, device=q.device)) else "torch",
                       "dkv_transport": str(cp._dkv_transport_dtype(k)).replace("torch.", ""),
-                      "kv_split": os.environ.get("APEX_CP_KV_SPLIT", "1")}), flush=True)
+                      "kv_split": os.environ.get("APEX_CP_KV_SPLIT", "0")}), flush=True)
 
 
 if __name__ == "__main__":
