@@ -156,3 +156,22 @@ def test_f32_attention_dispatch_uses_kernel_and_is_memory_lean():
     assert peak < 0.5 * B * H * S * S * 4, peak
     o_ref = att.attention_reference(q.detach(), k.detach(), v.detach(), causal=True)
     torch.testing.assert_close(o.detach(), o_ref, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_f32_kernel_bias_dropout_causal_klens_together():
+    """Every option at once: additive bias, dropout, causal mask and per-batch key lengths."""
+    from apex.contrib.multihead_attn.attention import prepare_bias
+
+    B, Sq, Sk, H, D = 2, 150, 150, 2, 64
+    q, k, v, do = _inputs(B, Sq, Sk, H, D, seed=7)
+    g = torch.Generator(device="cpu").manual_seed(8)
+    bias = (torch.randn(1, H, Sq, Sk, generator=g) * 0.5).to(DEV)
+    k_lens = torch.tensor([150, 97], dtype=torch.int32, device=DEV)
+    p, seed, offset = 0.2, 77, 5
+    kb = prepare_bias(bias, B, H, Sq, Sk, torch.float32)
+    got = _run(q, k, v, do, 0.125, True, p=p, k_lens=k_lens, bias=kb, seed=seed, offset=offset)
+    thresh = min(255, max(1, int(p * 256 + 0.5)))
+    keep = _keep_from_words(got[5], B, H, Sq, Sk)
+    ref = _ref(q, k, v, do, 0.125, True, k_lens=k_lens, bias=bias, keep=keep, drop_scale=256.0 / (256 - thresh))
+    _check(got[:5], ref, "all options")
