@@ -265,8 +265,8 @@ constexpr int kFwdKB = 64;              // keys per tile
 // tile kt's math, right after the S products, and tile kt + 2's global loads are issued then
 // (cdna_hip_programming.md T14 "async-STAGE split"); the single-buffer loop pays two barriers per
 // tile (previous tile consumed / this tile staged).
-template <typename T, int D, bool CAUSAL, bool DROPOUT, bool SHORT, bool BIAS, bool DB = false>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SHORT ? (DROPOUT ? 3 : 4) : (D > 128 ? 1 : (DB && D <= 64 && !DROPOUT ? 3 : 2)))))
+template <typename T, int D, bool CAUSAL, bool DROPOUT, bool SHORT, bool BIAS, bool DB = false, bool W4 = false>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SHORT ? (DROPOUT ? (W4 ? 4 : 3) : 4) : (D > 128 ? 1 : (DB && D <= 64 && !DROPOUT ? 3 : 2)))))
 attn_fwd_kernel(AttnArgs a) {
   static_assert(!SHORT || D == 64, "SHORT is the D = 64 single-pass variant");
   static_assert(!(SHORT && DB), "SHORT stages the whole key range once");
@@ -1351,6 +1351,14 @@ int attn_fwd_impl(const AttnArgs& a, int dt, hipStream_t s) {
   // vs 74.0-75.7 us — the same; p = 0 at 56 us is within ~10 % of its HBM floor (276 MB moved).
   if constexpr (D == 64) {
     if (a.Sk <= 2 * kFwdKB && (!drop || attn_fwd_short_drop()) && !a.bias) {
+      // W4: the dropout variant at 128 VGPRs / 4 workgroups per CU (APEX_ATTN_SHORT_W4, A/B knob):
+      // 4 VGPRs spill there and it measured slower, b768 p = 0.1 245-247 -> 272-273 us
+      // (profiles/r4_attn_short_w4_ab.jsonl, same box), so 3 workgroups per CU stays the default
+      if (drop && attn_env_on("APEX_ATTN_SHORT_W4", false)) {
+        ATTN_DISPATCH(dt, T, ATTN_DISPATCH_B(a.causal, C,
+            hipLaunchKernelGGL((attn_fwd_kernel<T, 64, C, true, true, false, false, true>), grid, dim3(256), 0, s, a)));
+        return (int)hipGetLastError();
+      }
       ATTN_DISPATCH(dt, T, ATTN_DISPATCH_B(a.causal, C, ATTN_DISPATCH_B(drop, DR,
           hipLaunchKernelGGL((attn_fwd_kernel<T, 64, C, DR, true, false>), grid, dim3(256), 0, s, a))));
       return (int)hipGetLastError();
