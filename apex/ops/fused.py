@@ -78,6 +78,28 @@ def _wgrad_splits(M, N, K):
     return s
 
 
+_WGRAD_TT = os.environ.get("APEX_WGRAD_TT", "auto")
+
+
+def _wgrad_tt_splits(M, N, K):
+    """K-slices for the weight gradient on the transposed-read MFMA kernel (csrc/gemm.hip gemm_tt,
+    fp32 slabs + the same splitk_reduce), or 0 to keep the library split-K.
+    ``APEX_WGRAD_TT``: auto, 0 (library only), or a slice count. auto: the 256x256-tile counts of
+    BERT-Large's FFN weights (64 tiles: 4 slices = one wave of 256 workgroups), where the kernel
+    beats hipBLASLt since the balanced main loop (tools/wgrad_tt_bench.py, M = 98304,
+    profiles/r4_wgrad_tt_vs_lib.jsonl); the QKV (48 tiles) and output-projection (16) shapes stay on
+    the library, which is as fast or faster there."""
+    if _WGRAD_TT == "0" or N % 256 or K % 256:
+        return 0
+    if _WGRAD_TT not in ("auto", ""):
+        s = int(_WGRAD_TT)
+        return s if M % (64 * s) == 0 else 0
+    tiles = (N // 256) * (K // 256)
+    if M < 16384 or tiles < 64 or M % 256:
+        return 0
+    return max(1, 256 // tiles)
+
+
 def _gt(p):
     """The parameter's DDP bucket slot to write its gradient into, or None
     (apex.parallel.distributed.grad_target)."""
@@ -166,14 +188,15 @@ def _wgrad(dy2, x2, out=None, param=None):
     s = _wgrad_splits(M, N, K) if dy2.dtype in (torch.bfloat16, torch.float16) else 1
     from . import gemm as G
 
-    if G.mode() == "mfma" and dy2.is_cuda:
+    if dy2.is_cuda and dy2.dtype in (torch.bfloat16, torch.float16):
         C = _ext.require()
-        st = max(s, 4 if M >= 16384 else 1)
-        if C.gemm_tt_supported(dy2, x2, st):
-            # hand-written transposed-read MFMA GEMM (csrc/gemm.hip, TR main loop); at parity with
-            # the library here (profiles/r1_gemm_policy.jsonl), so only in the all-MFMA mode
-            r = C.gemm_tt(dy2, x2, st, dy2.dtype)
-            return out.copy_(r) if out is not None else r
+        st = _wgrad_tt_splits(M, N, K)
+        if G.mode() == "mfma" and not st:
+            st = max(s, 4 if M >= 16384 else 1)
+        if st and C.gemm_tt_supported(dy2, x2, st) and (out is None or out.is_contiguous()):
+            # hand-written transposed-read MFMA GEMM (csrc/gemm.hip); the split-K reduction writes
+            # the gradient-bucket slot directly when one is given
+            return C.gemm_tt(dy2, x2, st, dy2.dtype, out=out)
     if s == 1 or not (dy2.is_contiguous() and x2.is_contiguous()):
         return torch.mm(dy2.t(), x2, out=out) if out is not None else torch.mm(dy2.t(), x2)
     slabs = torch.bmm(dy2.view(s, M // s, N).transpose(1, 2), x2.view(s, M // s, K), out_dtype=torch.float32)

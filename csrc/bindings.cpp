@@ -1331,7 +1331,7 @@ bool k_gemm_tt_supported(Tensor a, Tensor b, int64_t splits) {
          apex::gemm_tt_supported((int)a.size(1), (int)b.size(1), (int)a.size(0), (int)splits, a.size(1), b.size(1));
 }
 
-Tensor k_gemm_tt(Tensor a, Tensor b, int64_t splits, at::ScalarType out_dtype) {
+Tensor k_gemm_tt(Tensor a, Tensor b, int64_t splits, at::ScalarType out_dtype, const c10::optional<Tensor>& out_opt) {
   TORCH_CHECK(k_gemm_tt_supported(a, b, splits), "gemm_tt: unsupported operands");
   const int64_t R = a.size(0), P = a.size(1), Q = b.size(1);
   apex::GemmArgs g{};
@@ -1345,7 +1345,7 @@ Tensor k_gemm_tt(Tensor a, Tensor b, int64_t splits, at::ScalarType out_dtype) {
   g.ldc = Q;
   g.splits = (int)splits;
   Tensor out;
-  if (splits == 1 && out_dtype == a.scalar_type()) {
+  if (splits == 1 && out_dtype == a.scalar_type() && !out_opt) {
     out = at::empty({P, Q}, a.options());
     g.C = out.data_ptr();
     g.epi = apex::EPI_NONE;
@@ -1356,7 +1356,8 @@ Tensor k_gemm_tt(Tensor a, Tensor b, int64_t splits, at::ScalarType out_dtype) {
   g.part = slabs.data_ptr<float>();
   g.epi = apex::EPI_F32;
   check(apex::gemm_tt(g, dt_code(a.scalar_type()), cur_stream()), "gemm_tt");
-  return k_splitk_reduce(slabs, out_dtype, c10::nullopt);
+  // (out given: the reduction writes the parameter's gradient-bucket slot directly)
+  return k_splitk_reduce(slabs, out_dtype, out_opt);
 }
 
 // out[P, Q] += a^T b in fp32 (a [R, P], b [R, Q] 16-bit, out fp32 contiguous): the weight gradient
@@ -1511,7 +1512,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("aux") = py::none(), py::arg("bias_grad_dtype") = py::none(), py::arg("bias_grad_out") = py::none());
   m.def("transpose", &k_transpose);
   m.def("gemm_tt_supported", &k_gemm_tt_supported);
-  m.def("gemm_tt", &k_gemm_tt);
+  m.def("gemm_tt", &k_gemm_tt, py::arg("a"), py::arg("b"), py::arg("splits"), py::arg("out_dtype"),
+        py::arg("out") = py::none());
   m.def("gemm_tt_acc", &k_gemm_tt_acc);
   m.attr("EPI_NONE") = (int)apex::EPI_NONE;
   m.attr("EPI_BIAS") = (int)apex::EPI_BIAS;

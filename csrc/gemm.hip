@@ -4,7 +4,8 @@
 //
 // Both operands are K-contiguous ("NT"): the forward projections (X . W^T) directly, and the
 // input-gradient GEMMs (dY . W) through a transposed copy of W (transpose_2d below).
-// Weight gradients (contraction over tokens) stay on hipBLASLt with split-K (fused.py).
+// Weight gradients (contraction over tokens): the transposed-read instantiation (gemm_tt, split-K
+// fp32 slabs) for the shapes where it beats hipBLASLt, the library split-K otherwise (fused.py).
 //
 // Epilogues (fused into the tile write, so the activation never makes an extra HBM round
 // trip — the separate bias/GELU/residual kernels they replace each read+wrote [M,N]):
@@ -388,6 +389,143 @@ __device__ __forceinline__ void mainloop_bk64(const T* __restrict__ A, const T* 
   }
 }
 
+// ---- "balanced" variant of the same schedule: the production main loop (DBG bit 1024 selects the
+// one above, for lab A/B) ----------------------------------------------------------------------------
+// The loop above reads 12 fragments in p1, 4 in p2, 8 in p3 and none in p4; p1's read section is the
+// long pole of the ping-pong (the other group's 16-MFMA section has to cover it). Here the quadrant
+// order alternates per K-tile — even tiles (0,0) (0,1) (1,1) (1,0), odd tiles (0,1) (0,0) (1,0) (1,1)
+// — so the B half a tile starts with is the one its predecessor ended without, and p4 reads it from
+// the other buffer for the next tile: 8 / 4 / 8 / 4 fragments per phase. That needs B(t+1) landed
+// one phase earlier: p3 waits for it (vmcnt(6): only A(t+1) and B(t+2)'s first pieces stay in
+// flight), and the barriers after p3 make it visible. WAR is unchanged: B(t+1) is last read in
+// tile t+1's p2, before B(t+3) is staged over it in p3. Measured against the loop above
+// (profiles/r4_gemm_balanced_loop.jsonl, same box, interleaved, outputs bit-identical): NT 8192^3
+// 1.49 -> 1.53 PF/s, BERT M = 98304 shapes 1-5 % faster (FFN2 dgrad + residual 642 -> 618 us);
+// transposed-read weight gradients 2-8 % (two ds_read_b64_tr_b16 per fragment: the read sections
+// are longer there, so evening them out pays more).
+template <bool TR>
+__device__ __forceinline__ void read_fa(s16x8 (&fa)[4][2], const char* ta, int rb, int lr, int lk) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) fa[i][s] = frag<TR>(ta, rb + i * 16, s, lr, lk);
+}
+template <bool TR>
+__device__ __forceinline__ void read_fb(s16x8 (&fb)[2][2], const char* tb, int cb, int lr, int lk) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) fb[j][s] = frag<TR>(tb, cb + j * 16, s, lr, lk);
+}
+template <typename T, int FA, int FB, int MH, int NH>
+__device__ __forceinline__ void quad_mma(f32x4 (&acc)[4][8], const s16x8 (&fa)[4][2], const s16x8 (&fb)[2][2]) {
+  __builtin_amdgcn_s_setprio(1);
+  if constexpr (FA >= 0) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        acc[2 * NH + j][4 * MH + i] = mfma_f8<FB, FA>(fb[j][0], fb[j][1], fa[i][0], fa[i][1], acc[2 * NH + j][4 * MH + i]);
+  } else {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[2 * NH + j][4 * MH + i] = mfma16<T>(fb[j][s], fa[i][s], acc[2 * NH + j][4 * MH + i]);
+  }
+  __builtin_amdgcn_s_setprio(0);
+}
+
+template <typename T, bool TR, int FA, int FB, int DBG, int PAR>
+__device__ __forceinline__ void bal_tile(int t, int nt, const T* __restrict__ A, const T* __restrict__ B, int M, int N,
+                                         int64_t lda, int64_t ldb, int m0, int n0, char* smem, int wid, int wr, int wc,
+                                         int lane, f32x4 (&acc)[4][8], s16x8 (&fa)[4][2], s16x8 (&fb)[2][2][2]) {
+  constexpr int BKE = 128 / (int)sizeof(T);
+  constexpr int OP = 1 - PAR;
+  const int lr = lane & 15, lk = lane >> 4;
+  // t & 1 == PAR, but kept opaque (an SGPR the compiler cannot fold): with a constant buffer base
+  // per parity hipcc keeps separate fragment-address registers for both buffers and spills
+  int pb = t & 1;
+  asm("" : "+s"(pb));
+  char* cur = smem + pb * G_BUF_BYTES;
+  char* oth = smem + (pb ^ 1) * G_BUF_BYTES;
+  const char* ta = cur;
+  const char* tb = cur + G_TILE_BYTES;
+  const bool ld_a = t + 1 < nt, ld_b = t + 2 < nt;
+  constexpr bool RD = !(DBG & 128), GL = !(DBG & 32), BR = !(DBG & 64);
+  // p1: A rows mh=0; stage A(t+1) pieces 0,1
+  if constexpr (RD) read_fa<TR>(fa, ta, wr * 128, lr, lk);
+  if (GL && ld_a) stage_pieces<T, TR>(A, lda, m0, M, (t + 1) * BKE, oth, wid, lane, 0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if constexpr (BR) bar();
+  quad_mma<T, FA, FB, 0, PAR>(acc, fa, fb[PAR]);
+  if constexpr (BR) bar();
+  // p2: B half OP; stage A(t+1) pieces 2,3
+  if constexpr (RD) read_fb<TR>(fb[OP], tb, wc * 64 + OP * 32, lr, lk);
+  if (GL && ld_a) stage_pieces<T, TR>(A, lda, m0, M, (t + 1) * BKE, oth, wid, lane, 2);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if constexpr (BR) bar();
+  quad_mma<T, FA, FB, 0, OP>(acc, fa, fb[OP]);
+  if constexpr (BR) bar();
+  // p3: A rows mh=1; stage B(t+2) pieces 0,1 into this buffer; retire B(t+1) for p4
+  if constexpr (RD) read_fa<TR>(fa, ta, wr * 128 + 64, lr, lk);
+  if (ld_b) {
+    if constexpr (GL) stage_pieces<T, TR>(B, ldb, n0, N, (t + 2) * BKE, cur + G_TILE_BYTES, wid, lane, 0);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  } else if (ld_a) {
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if constexpr (BR) bar();
+  quad_mma<T, FA, FB, 1, OP>(acc, fa, fb[OP]);
+  if constexpr (BR) bar();
+  // p4: next tile's first B half (OP) from the other buffer; stage B(t+2) pieces 2,3; retire A(t+1).
+  // (Unconditional: after the last tile it reads stale LDS that nothing uses — a conditional load
+  // would keep the old fragment live across the phase and cost registers.)
+  if constexpr (RD) read_fb<TR>(fb[OP], oth + G_TILE_BYTES, wc * 64 + OP * 32, lr, lk);
+  if (ld_b) {
+    if constexpr (GL) stage_pieces<T, TR>(B, ldb, n0, N, (t + 2) * BKE, cur + G_TILE_BYTES, wid, lane, 2);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if constexpr (BR) bar();
+  quad_mma<T, FA, FB, 1, PAR>(acc, fa, fb[PAR]);
+  if constexpr (BR) bar();
+}
+
+template <typename T, bool TR, int FA = -1, int FB = -1, int DBG = 0>
+__device__ __forceinline__ void mainloop_bal(const T* __restrict__ A, const T* __restrict__ B, int M, int N, int K,
+                                             int64_t lda, int64_t ldb, int m0, int n0, char* smem, int wid, int wr,
+                                             int wc, int lane, f32x4 (&acc)[4][8]) {
+  constexpr int BKE = 128 / (int)sizeof(T);
+  const int nt = K / BKE;
+  stage_pieces<T, TR>(A, lda, m0, M, 0, smem, wid, lane, 0);
+  stage_pieces<T, TR>(A, lda, m0, M, 0, smem, wid, lane, 2);
+  stage_pieces<T, TR>(B, ldb, n0, N, 0, smem + G_TILE_BYTES, wid, lane, 0);
+  stage_pieces<T, TR>(B, ldb, n0, N, 0, smem + G_TILE_BYTES, wid, lane, 2);
+  if (nt > 1) {
+    stage_pieces<T, TR>(B, ldb, n0, N, BKE, smem + G_BUF_BYTES + G_TILE_BYTES, wid, lane, 0);
+    stage_pieces<T, TR>(B, ldb, n0, N, BKE, smem + G_BUF_BYTES + G_TILE_BYTES, wid, lane, 2);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  bar();
+  if (wr == 1) bar();  // stagger group 1 by one barrier
+  s16x8 fa[4][2], fb[2][2][2];
+  const int lr = lane & 15, lk = lane >> 4;
+  if constexpr (!(DBG & 128)) read_fb<TR>(fb[0], smem + G_TILE_BYTES, wc * 64, lr, lk);  // tile 0's first B half
+  int t = 0;
+  for (; t + 1 < nt; t += 2) {
+    bal_tile<T, TR, FA, FB, DBG, 0>(t, nt, A, B, M, N, lda, ldb, m0, n0, smem, wid, wr, wc, lane, acc, fa, fb);
+    bal_tile<T, TR, FA, FB, DBG, 1>(t + 1, nt, A, B, M, N, lda, ldb, m0, n0, smem, wid, wr, wc, lane, acc, fa, fb);
+  }
+  if (t < nt) bal_tile<T, TR, FA, FB, DBG, 0>(t, nt, A, B, M, N, lda, ldb, m0, n0, smem, wid, wr, wc, lane, acc, fa, fb);
+}
+
 // Buffer resource for a wave-uniform base address (the epilogue's full-tile path): every lane
 // addresses rows through ONE 32-bit voffset plus an SGPR soffset per row slot, instead of a 64-bit
 // VGPR address pair per access (32 pairs per lane for a load+store epilogue, which the scheduler
@@ -736,7 +874,13 @@ __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(const TI* __restrict
     A += (int64_t)blockIdx.y * K * lda;
     B += (int64_t)blockIdx.y * K * ldb;
   }
-  mainloop_bk64<TI, TR, FA, FB, DBG>(A, B, M, N, K, lda, ldb, m0, n0, smem, wid, wr, wc, lane, acc);
+  // mainloop_bal for the full-tile 16-bit kernels; the fp8 and edge-tile instantiations keep the
+  // previous schedule (their epilogues hold more registers: the balanced loop's extra live
+  // fragment spilled 50-240 VGPRs there). DBG bit 1024 forces the previous one (lab A/B).
+  if constexpr ((DBG & 1024) || FA >= 0 || EDGE)
+    mainloop_bk64<TI, TR, FA, FB, DBG>(A, B, M, N, K, lda, ldb, m0, n0, smem, wid, wr, wc, lane, acc);
+  else
+    mainloop_bal<TI, TR, FA, FB, DBG>(A, B, M, N, K, lda, ldb, m0, n0, smem, wid, wr, wc, lane, acc);
   if (wr == 0) bar();  // re-align the groups
   bar();               // every wave is past its last ds_read: LDS is free for the epilogue
   if constexpr (EPI == EPI_F32) {

@@ -179,7 +179,7 @@ def test_gemm_supported_rejects():
 
 
 @pytest.mark.parametrize("R,P,Q,splits", [(256, 256, 256, 1), (1024, 256, 512, 2), (2048, 512, 256, 4),
-                                          (8192, 1024, 1024, 8)])
+                                          (8192, 1024, 1024, 8), (64, 256, 256, 1), (576, 256, 512, 3)])
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 def test_gemm_tt_weight_grad(R, P, Q, splits, dt):
     """dW = dY^T X through the transposed-read (ds_read_b64_tr_b16) main loop, split-K slabs."""
@@ -194,6 +194,31 @@ def test_gemm_tt_weight_grad(R, P, Q, splits, dt):
     _close(out, ref, 1e-2)
     out32 = C.gemm_tt(dy, x, splits, torch.float32)
     _close(out32, ref, 1e-4)
+
+
+@pytest.mark.parametrize("N,K", [(1024, 4096), (4096, 1024)])
+def test_wgrad_tt_policy_writes_slot(N, K, monkeypatch):
+    """apex.ops.fused._wgrad on the FFN weight shapes (>= 64 output tiles, >= 16k tokens): the
+    transposed-read kernel in 4 slices, the split-K reduction writing straight into a gradient
+    slot (a view inside a larger bucket), equal to the library path and the fp32 reference."""
+    from apex.ops import fused
+
+    torch.manual_seed(N)
+    M = 16384
+    dy = torch.randn(M, N, device=DEV).bfloat16()
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    monkeypatch.setattr(fused, "_WGRAD_TT", "auto")
+    assert fused._wgrad_tt_splits(M, N, K) == 4
+    bucket = torch.full((N * K + 64,), 7.0, device=DEV, dtype=torch.bfloat16)
+    slot = bucket[32:32 + N * K].view(N, K)
+    r = fused._wgrad(dy, x, out=slot)
+    assert r.data_ptr() == slot.data_ptr()
+    assert (bucket[:32] == 7).all() and (bucket[32 + N * K:] == 7).all()
+    ref = dy.float().t() @ x.float()
+    _close(slot, ref, 1e-2)
+    monkeypatch.setattr(fused, "_WGRAD_TT", "0")
+    lib = fused._wgrad(dy, x)
+    _close(slot, lib.float(), 1e-2)
 
 
 def test_gemm_tt_asymmetric_identity():

@@ -104,7 +104,8 @@ void run_epi(Bufs& b, int rounds, int reps, hipStream_t s) {
     const char* name;
     void (*fn)(const Bufs&, hipStream_t);
   };
-  std::vector<V> vs = {{"w8", launch_old<EPI>}, {"w8p", launch_w8p<EPI>}};
+  std::vector<V> vs = {{"w8", launch_old<EPI>}, {"w8old", launch_old<EPI, 1024>}};
+  if (getenv("LAB_W8P")) vs.push_back({"w8p", launch_w8p<EPI>});
   if (getenv("LAB_M32")) vs.push_back({"w8m32", launch_m32<EPI>});
   if (getenv("LAB_W2G")) vs.push_back({"w2g", launch_w2g<EPI>});
   if (getenv("LAB_NOEPI")) {
