@@ -25,6 +25,9 @@ def main():
     import apex._ext as e
     from apex.ops.fused import _wgrad
 
+    from apex.ops import fused
+
+    fused._WGRAD_TT = "0"  # "lib" below = the library split-K path
     C = e.require()
     M = int(os.environ.get("PB_M", 32768))
     H, F = 1024, 4096
