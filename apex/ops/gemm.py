@@ -10,8 +10,9 @@
 
 The kernel takes both operands K-contiguous (A[M,K], B[N,K]); the input-gradient GEMMs use a
 transposed copy of W made by a HIP transpose kernel (cheap next to the GEMM: 2 bytes/weight
-each way). Weight gradients (contraction over tokens) stay on hipBLASLt with split-K
-(apex.ops.fused._wgrad).
+each way). Weight gradients (contraction over tokens) go through apex.ops.fused._wgrad: the
+transposed-read MFMA kernel for the shapes where it wins (BERT-Large's FFN weights), hipBLASLt
+split-K otherwise.
 
 Policy (``APEX_GEMM``):
   auto (default)  the MFMA kernel where its fused epilogue removes a separate [M, N] pass
@@ -24,6 +25,14 @@ Policy (``APEX_GEMM``):
                     MFMA wins      FFN1 fwd+bias+GELU 299 vs 328 (mm + bias_act), FFN2 dgrad+dGELU
                                    318 vs 402 (mm + bias_act_bwd), QKV dgrad+residual 171 vs 199
                                    (addmm), FFN1 dgrad+residual 221 vs 242
+                  Re-measured in round 4 with the balanced main loop at the bench's M = 98304
+                  (profiles/r4_gemm_policy_m98304.jsonl): the library still wins the plain
+                  products (qkv fwd 476 vs 532 us, attn-out fwd 168 vs 192, FFN2 fwd 551 vs 599);
+                  the fused ones are MFMA by 16-24 % (QKV dgrad+residual 482 vs 570, FFN1
+                  dgrad+residual 613 vs 717, FFN2 dgrad+dGELU 927 vs 1222, FFN1 fwd+GELU 874 vs 990).
+                  What the plain products lose to is the epilogue: the 256-tile rounds store their
+                  outputs all at once with the matrix cores idle (19-28 % of the kernel at K = 1024,
+                  profiles/r4_gemmlab_ablation_m98304.jsonl).
   mfma            every supported GEMM on the MFMA kernels, including the weight gradients on
                   the transposed-read variant (C.gemm_tt: 266-273 us vs the library's 267-272
                   for the FFN shapes with 4 K-slices; slower for QKV) — A/B and coverage runs
