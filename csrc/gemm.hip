@@ -874,10 +874,12 @@ __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(const TI* __restrict
     A += (int64_t)blockIdx.y * K * lda;
     B += (int64_t)blockIdx.y * K * ldb;
   }
-  // mainloop_bal for the full-tile 16-bit kernels; the fp8 and edge-tile instantiations keep the
-  // previous schedule (their epilogues hold more registers: the balanced loop's extra live
-  // fragment spilled 50-240 VGPRs there). DBG bit 1024 forces the previous one (lab A/B).
-  if constexpr ((DBG & 1024) || FA >= 0 || EDGE)
+  // mainloop_bal for the 16-bit kernels; the fp8 instantiations and the edge-tile dGELU / multiply
+  // epilogues keep the previous schedule (their epilogues hold more registers: the balanced loop's
+  // extra live fragment spilled 50-240 VGPRs in fp8, 2 -> 52 in edge EPI_MUL). DBG bit 1024 forces
+  // the previous one (lab A/B).
+  constexpr bool EDGE_HEAVY = EDGE && (EPI == EPI_MUL || EPI == EPI_DGELU || EPI == EPI_DGELU_TANH);
+  if constexpr ((DBG & 1024) || FA >= 0 || EDGE_HEAVY)
     mainloop_bk64<TI, TR, FA, FB, DBG>(A, B, M, N, K, lda, ldb, m0, n0, smem, wid, wr, wc, lane, acc);
   else
     mainloop_bal<TI, TR, FA, FB, DBG>(A, B, M, N, K, lda, ldb, m0, n0, smem, wid, wr, wc, lane, acc);

@@ -66,9 +66,14 @@ typedef void (*Launch)(const Bufs&, int epi, hipStream_t);
 template <int EPI, int DBG = 0, int STAGGER = 0>
 void launch_old(const Bufs& b, hipStream_t s) {
   const int tiles = ((b.M + 255) / 256) * ((b.N + 255) / 256);
-  hipLaunchKernelGGL((gemm_nt_kernel<bf16, EPI, false, false, bf16, -1, -1, DBG>), dim3(tiles), dim3(512), 0, s, b.A, b.B, b.C, b.M, b.N,
-                     b.K, (int64_t)b.K, (int64_t)b.K, (int64_t)b.N, b.bias, b.aux, (int64_t)b.N, b.aux_out, b.part, STAGGER,
-                     nullptr, nullptr);
+  if (b.M % 256 || b.N % 256)  // partial tiles: the bounds-checked instantiation (as launch_gemm)
+    hipLaunchKernelGGL((gemm_nt_kernel<bf16, EPI, false, true, bf16, -1, -1, DBG>), dim3(tiles), dim3(512), 0, s, b.A, b.B, b.C,
+                       b.M, b.N, b.K, (int64_t)b.K, (int64_t)b.K, (int64_t)b.N, b.bias, b.aux, (int64_t)b.N, b.aux_out, b.part,
+                       STAGGER, nullptr, nullptr);
+  else
+    hipLaunchKernelGGL((gemm_nt_kernel<bf16, EPI, false, false, bf16, -1, -1, DBG>), dim3(tiles), dim3(512), 0, s, b.A, b.B, b.C,
+                       b.M, b.N, b.K, (int64_t)b.K, (int64_t)b.K, (int64_t)b.N, b.bias, b.aux, (int64_t)b.N, b.aux_out, b.part,
+                       STAGGER, nullptr, nullptr);
 }
 template <int EPI, int DBG = 0>
 void launch_w4(const Bufs& b, hipStream_t s) {
@@ -105,25 +110,27 @@ void run_epi(Bufs& b, int rounds, int reps, hipStream_t s) {
     void (*fn)(const Bufs&, hipStream_t);
   };
   std::vector<V> vs = {{"w8", launch_old<EPI>}, {"w8old", launch_old<EPI, 1024>}};
-  if (getenv("LAB_W8P")) vs.push_back({"w8p", launch_w8p<EPI>});
-  if (getenv("LAB_M32")) vs.push_back({"w8m32", launch_m32<EPI>});
-  if (getenv("LAB_W2G")) vs.push_back({"w2g", launch_w2g<EPI>});
-  if (getenv("LAB_NOEPI")) {
+  // the other variants have no bounds-checked form: full tiles only
+  const bool full = b.M % 256 == 0 && b.N % 256 == 0;
+  if (full && getenv("LAB_W8P")) vs.push_back({"w8p", launch_w8p<EPI>});
+  if (full && getenv("LAB_M32")) vs.push_back({"w8m32", launch_m32<EPI>});
+  if (full && getenv("LAB_W2G")) vs.push_back({"w2g", launch_w2g<EPI>});
+  if (full && getenv("LAB_NOEPI")) {
     vs.push_back({"w8_noepi", launch_old<EPI, 512>});
     vs.push_back({"w8p_noepi", launch_w8p<EPI, 512>});
   }
-  if (getenv("LAB_W4")) {
+  if (full && getenv("LAB_W4")) {
     vs.push_back({"w4", launch_w4<EPI>});
     vs.push_back({"w4r", launch_w4<EPI, 256>});
   }
-  if (getenv("LAB_DBG")) {
+  if (full && getenv("LAB_DBG")) {
     vs.push_back({"w8_noglds", launch_old<EPI, 32>});
     vs.push_back({"w8_nobar", launch_old<EPI, 64>});
     vs.push_back({"w8_nodsread", launch_old<EPI, 128>});
     vs.push_back({"w8_nomem", launch_old<EPI, 32 + 64 + 128>});
     vs.push_back({"w8_noepi", launch_old<EPI, 512>});
   }
-  if (getenv("LAB_STAGGER")) {
+  if (full && getenv("LAB_STAGGER")) {
     vs.push_back({"w8_st1", launch_old<EPI, 0, 1>});
     vs.push_back({"w8_st2", launch_old<EPI, 0, 2>});
     vs.push_back({"w8_st3", launch_old<EPI, 0, 3>});
@@ -201,6 +208,10 @@ int main(int argc, char** argv) {
   b.M = atoi(argv[1]);
   b.N = atoi(argv[2]);
   b.K = atoi(argv[3]);
+  if (b.K % 64 || b.N % 8 || b.M <= 0) {  // what gemm_supported() requires of every launch
+    fprintf(stderr, "K must be a multiple of 64 and N of 8\n");
+    return 1;
+  }
   const int epi = argc > 4 ? atoi(argv[4]) : 0;
   const int rounds = argc > 5 ? atoi(argv[5]) : 5;
   const int reps = argc > 6 ? atoi(argv[6]) : 10;
