@@ -1,0 +1,32 @@
+"""Weight-gradient routing (apex.ops.fused): which shapes go to the transposed-read MFMA kernel
+(_wgrad_tt_splits) and how the library split-K slices (_wgrad_splits) are chosen. Pure host logic."""
+from apex.ops import fused
+
+
+def test_tt_auto_takes_the_ffn_shapes_only(monkeypatch):
+    monkeypatch.setattr(fused, "_WGRAD_TT", "auto")
+    M = 98304
+    assert fused._wgrad_tt_splits(M, 4096, 1024) == 4  # FFN1: 64 tiles -> one wave of 256 workgroups
+    assert fused._wgrad_tt_splits(M, 1024, 4096) == 4  # FFN2
+    assert fused._wgrad_tt_splits(M, 3072, 1024) == 0  # QKV (48 tiles): library
+    assert fused._wgrad_tt_splits(M, 1024, 1024) == 0  # attention out (16 tiles): library
+    assert fused._wgrad_tt_splits(8192, 4096, 1024) == 0  # too few tokens
+    assert fused._wgrad_tt_splits(M, 1600, 6400) == 0  # not tile multiples
+
+
+def test_tt_overrides(monkeypatch):
+    monkeypatch.setattr(fused, "_WGRAD_TT", "0")
+    assert fused._wgrad_tt_splits(98304, 4096, 1024) == 0
+    monkeypatch.setattr(fused, "_WGRAD_TT", "8")
+    assert fused._wgrad_tt_splits(98304, 3072, 1024) == 8
+    assert fused._wgrad_tt_splits(98304 + 64, 3072, 1024) == 0  # slices must divide into K-tiles
+
+
+def test_library_split_k_fills_the_chip(monkeypatch):
+    monkeypatch.setattr(fused, "_WGRAD_SPLITK", "auto")
+    M = 98304
+    for n, k in ((3072, 1024), (1024, 1024), (4096, 1024), (1024, 4096)):
+        s = fused._wgrad_splits(M, n, k)
+        tiles = ((n + 255) // 256) * ((k + 255) // 256)
+        assert M % s == 0 and s * tiles <= 256 and (s == 16 or 2 * s * tiles > 256)
+    assert fused._wgrad_splits(4096, 1024, 1024) == 1
