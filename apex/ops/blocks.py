@@ -37,17 +37,67 @@ _STORE_DERIV = os.environ.get("APEX_MLP_STORE", "deriv") != "h"
 
 # Memory-efficient post-LN: the bias+dropout+residual+LN forward does not store its LN input s; the
 # backward rebuilds x-hat = (y - beta) / gamma from the LN output y, which is saved anyway as the next
-# sublayer's GEMM input — one [tokens, hidden] write less per sublayer (and that much less activation
-# memory bandwidth). As with any output-based LayerNorm backward, a gamma entry of exactly 0 makes its
-# column's x-hat unrecoverable: the forward kernel therefore also gets an (untouched) s buffer and
-# writes it only when it sees a zero in gamma, and the backward kernel makes the same test and reads
-# that s instead (csrc/fused_ops.hip, s_cond / s_alt) — exact gradients in every case, the extra
-# [tokens, hidden] write only in the degenerate one. APEX_LN_MEM=0 always stores s.
+# sublayer's GEMM input — one [tokens, hidden] write and one saved [tokens, hidden] activation less per
+# sublayer (BERT-Large b768: 80.3 -> 71 GB peak). As with any output-based LayerNorm backward, a gamma
+# entry of exactly 0 makes its column's x-hat unrecoverable: a host-side check (_GammaZeroCheck, one
+# batched reduction + one read per step) then has the forward allocate s too, the kernel writes it (it
+# makes the same test, csrc/fused_ops.hip s_cond) and the backward reads it instead (s_alt) — exact
+# gradients in every case, the extra buffer only in the degenerate one. APEX_LN_MEM=0 always stores s.
 _LN_MEM = os.environ.get("APEX_LN_MEM", "1") != "0"
 
 
 def _ln_mem(C, cols):
     return _LN_MEM and C.bdaln_supported(cols)
+
+
+class _GammaZeroCheck:
+    """Does an LN gamma hold an exact 0? Decided on the host, once per training step for all gammas.
+
+    The s buffer of the memory-efficient mode is only needed when a gamma entry is exactly 0, and
+    holding it for every sublayer until backward costs a [tokens, hidden] activation per sublayer
+    (9 GB at BERT-Large b768). So the forward allocates and saves it only when this check says a
+    zero is present. The check runs as ONE batched device reduction over every gamma seen so far
+    plus ONE host read, the first time a sublayer runs after a backward pass, i.e. once per step
+    (the optimizer, our fused kernels included, writes gammas only between a backward and the next
+    forward), or when a gamma's version counter / storage changed (in-place writes through autograd-
+    visible ops). Writes through `.data` between two forwards with no backward in between are not
+    seen: that is the one case this check misses.
+    """
+
+    def __init__(self):
+        self._known = {}  # id(gamma) -> (weakref, version, data_ptr, has_zero)
+        self._dirty = True
+
+    def mark_dirty(self):
+        self._dirty = True
+
+    def has_zero(self, gamma):
+        import weakref
+        ent = self._known.get(id(gamma))
+        if (not self._dirty and ent is not None and ent[0]() is gamma and ent[1] == gamma._version
+                and ent[2] == gamma.data_ptr()):
+            return ent[3]
+        live = [gamma] + [e[0]() for k, e in self._known.items() if k != id(gamma)]
+        live = [g for g in live if g is not None and g.device == gamma.device]
+        with torch.no_grad():
+            flags = torch.stack([(g == 0).any() for g in live]).cpu()
+        self._known = {id(g): (weakref.ref(g), g._version, g.data_ptr(), bool(f)) for g, f in zip(live, flags)}
+        self._dirty = False
+        return self._known[id(gamma)][3]
+
+
+_GZ = _GammaZeroCheck()
+
+
+def _ln_plan(C, gamma, cols, needs_grad):
+    """(mem, store_s) for a bias+dropout+residual+LN forward: mem = rebuild x-hat from y in the
+    backward; store_s = also keep the LN input s (mem mode: only when gamma has an exact 0)."""
+    mem = _ln_mem(C, cols)
+    if not mem:
+        return False, True
+    if not needs_grad:
+        return True, False  # no backward will read it
+    return True, _GZ.has_zero(gamma)
 
 
 # fp8 codes written by the bias+dropout+residual+LayerNorm kernels themselves (apex.fp8 "producer-side
@@ -100,15 +150,15 @@ class _AttnSublayer(torch.autograd.Function):
             _q8_file(f8, o2, None if q8o is None else (q8o[0].view(B * S, E),) + tuple(q8o[1:]), okey, f8._fwd)
         t = G.linear(o2, wo, f8=f8)
         sh, oh = _seed(x.device) if p_hidden > 0 else (0, 0)
-        mem = _ln_mem(C, E)
+        mem, store_s = _ln_plan(C, gamma, E, any(ctx.needs_input_grad))
         ykey = (f8.key_of(gamma), "y") if f8 is not None else None
         q8 = _q8(f8, ykey, f8._fwd, t) if f8 is not None else None
         y, s, mean, rstd = C.bdaln_fwd(t, bo, x2.contiguous(), gamma, beta, float(eps), float(p_hidden), sh, oh,
-                                       s_cond=mem, **_q8_kw(q8))
+                                       store_s=store_s, s_cond=mem, **_q8_kw(q8))
         if f8 is not None:
             _q8_file(f8, y, q8, ykey, f8._fwd)
         ctx.save_for_backward(x2, wqkv, qkv, o, lse, k_lens, dmask, wo, y if mem else s, gamma, mean, rstd,
-                              s if mem else None)
+                              s if mem and store_s else None)
         ctx.ln_beta = beta if mem else None
         ctx.f8 = f8
         ctx.params = (wqkv, bqkv, wo, bo, gamma, beta)
@@ -119,6 +169,7 @@ class _AttnSublayer(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         C = _ext.require()
+        _GZ.mark_dirty()  # an optimizer step may follow: re-check the gammas at the next forward
         x2, wqkv, qkv, o, lse, k_lens, dmask, wo, s, gamma, mean, rstd, s_alt = ctx.saved_tensors
         B, S, E, heads, d, scale, causal, p_attn, sa, oa, p_hidden, sh, oh, has_bqkv, has_bo, bdt = ctx.cfg
         pqkv, pbqkv, pwo, pbo, pg, pb = ctx.params
@@ -181,14 +232,15 @@ class _FFNSublayer(torch.autograd.Function):
             hb = b1
         t = G.linear(g, w2, f8=f8)
         seed, off = _seed(x.device) if p > 0 else (0, 0)
-        mem = _ln_mem(C, x2.shape[1])
+        mem, store_s = _ln_plan(C, gamma, x2.shape[1], any(ctx.needs_input_grad))
         ykey = (f8.key_of(gamma), "y") if f8 is not None else None
         q8 = _q8(f8, ykey, f8._fwd, t) if f8 is not None else None
         y, s, mean, rstd = C.bdaln_fwd(t, b2, x2.contiguous(), gamma, beta, float(eps), float(p), seed, off,
-                                       s_cond=mem, **_q8_kw(q8))
+                                       store_s=store_s, s_cond=mem, **_q8_kw(q8))
         if f8 is not None:
             _q8_file(f8, y, q8, ykey, f8._fwd)
-        ctx.save_for_backward(x2, w1, hb, h, g, w2, y if mem else s, gamma, mean, rstd, s if mem else None)
+        ctx.save_for_backward(x2, w1, hb, h, g, w2, y if mem else s, gamma, mean, rstd,
+                              s if mem and store_s else None)
         ctx.ln_beta = beta if mem else None
         ctx.cfg = (p, seed, off, act, b2 is not None, b1.dtype if b1 is not None else None)
         ctx.params = (w1, b1, w2, b2, gamma, beta)
@@ -197,6 +249,7 @@ class _FFNSublayer(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         C = _ext.require()
+        _GZ.mark_dirty()
         x2, w1, hb, h, g, w2, s, gamma, mean, rstd, s_alt = ctx.saved_tensors
         p, seed, off, act, has_b2, b1dt = ctx.cfg
         f8 = ctx.f8

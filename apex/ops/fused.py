@@ -88,14 +88,16 @@ def _wgrad_tt_splits(M, N, K):
     BERT-Large's FFN weights (64 tiles: 4 slices = one wave of 256 workgroups), where the kernel
     beats hipBLASLt since the balanced main loop (tools/wgrad_tt_bench.py, M = 98304,
     profiles/r4_wgrad_tt_vs_lib.jsonl); the QKV (48 tiles) and output-projection (16) shapes stay on
-    the library, which is as fast or faster there."""
+    the library, which is as fast or faster there. Auto is limited to the measured tile range
+    (64 <= tiles < 128); larger weights (hundreds of tiles, e.g. Megatron / GPT MLPs) stay on the
+    library until measured."""
     if _WGRAD_TT == "0" or N % 256 or K % 256:
         return 0
     if _WGRAD_TT not in ("auto", ""):
         s = int(_WGRAD_TT)
         return s if M % (64 * s) == 0 else 0
     tiles = (N // 256) * (K // 256)
-    if M < 16384 or tiles < 64 or M % 256:
+    if M < 16384 or tiles < 64 or tiles >= 128 or M % 256:
         return 0
     return max(1, 256 // tiles)
 

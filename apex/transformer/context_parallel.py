@@ -214,8 +214,10 @@ def _native_merge(o, lse):
 
 def _dkv_transport_dtype(k):
     """dtype of the dK/dV partials travelling the ring: the input dtype for 16-bit inputs (each hop
-    adds its contribution in fp32 and rounds once: half the P2P bytes of an fp32 partial), fp32 /
-    fp64 accumulation for wider inputs. APEX_CP_DKV_FP32=1 keeps 16-bit inputs' partials in fp32."""
+    adds its fp32 block gradients into the 16-bit partial, i.e. the running sum is rounded once per
+    hop — W roundings over a W-rank ring; half the P2P bytes of an fp32 partial), fp32 / fp64
+    accumulation for wider inputs. APEX_CP_DKV_FP32=1 keeps 16-bit inputs' partials in fp32
+    (tests/test_cp_ring_native_gpu.py bounds both against one flash call)."""
     if k.dtype in (torch.bfloat16, torch.float16) and os.environ.get("APEX_CP_DKV_FP32", "0") != "1":
         return k.dtype
     return _acc_dtype(k)

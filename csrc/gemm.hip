@@ -863,6 +863,11 @@ __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(const TI* __restrict
   for (int j = 0; j < 4; ++j)
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // DBG bit 2048 (lab timeline trace, bf16 kernels only): per workgroup the 100 MHz real-time clock at
+  // start, after the main loop and after the epilogue's stores completed, plus HW_ID / XCC_ID, into
+  // the uint64 buffer passed as alpha_a (unused by the 16-bit kernels)
+  uint64_t tr0 = 0, tr1 = 0;
+  if constexpr (DBG & 2048) tr0 = __builtin_amdgcn_s_memrealtime();
 
   {
     const int st = ctl & 0xffff;
@@ -885,6 +890,7 @@ __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(const TI* __restrict
     mainloop_bal<TI, TR, FA, FB, DBG>(A, B, M, N, K, lda, ldb, m0, n0, smem, wid, wr, wc, lane, acc);
   if (wr == 0) bar();  // re-align the groups
   bar();               // every wave is past its last ds_read: LDS is free for the epilogue
+  if constexpr (DBG & 2048) tr1 = __builtin_amdgcn_s_memrealtime();
   if constexpr (EPI == EPI_F32) {
     // fp32 slab (split-K partials): each lane stores its 4 consecutive columns per fragment
     float* out = part + (int64_t)blockIdx.y * M * ldc;
@@ -940,6 +946,21 @@ __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(const TI* __restrict
   if constexpr (FA >= 0) alpha = alpha_a[0] * alpha_b[0];
   epilogue<T, EPI, EDGE, 0, 4, false, Q8>(acc, smem + wid * 16384, C, M, N, ldc, bias, aux, ldaux, aux_out, part, m0,
                                          n0, tm, wr, wc, lane, alpha, q8);
+  if constexpr ((DBG & 2048) && FA < 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+    const uint64_t tr2 = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0) {
+      uint32_t hw, xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      uint64_t* tp = (uint64_t*)alpha_a + (int64_t)bid * 4;
+      tp[0] = tr0;
+      tp[1] = tr1;
+      tp[2] = tr2;
+      tp[3] = (uint64_t)hw | ((uint64_t)xcc << 32);
+    }
+  }
 }
 
 

@@ -12,6 +12,7 @@ def test_tt_auto_takes_the_ffn_shapes_only(monkeypatch):
     assert fused._wgrad_tt_splits(M, 1024, 1024) == 0  # attention out (16 tiles): library
     assert fused._wgrad_tt_splits(8192, 4096, 1024) == 0  # too few tokens
     assert fused._wgrad_tt_splits(M, 1600, 6400) == 0  # not tile multiples
+    assert fused._wgrad_tt_splits(M, 10240, 2560) == 0  # 400 tiles: unmeasured range, library
 
 
 def test_tt_overrides(monkeypatch):

@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <map>
 #include <vector>
 
 using namespace apex;
@@ -75,6 +76,82 @@ void launch_old(const Bufs& b, hipStream_t s) {
                        b.M, b.N, b.K, (int64_t)b.K, (int64_t)b.K, (int64_t)b.N, b.bias, b.aux, (int64_t)b.N, b.aux_out, b.part,
                        STAGGER, nullptr, nullptr);
 }
+// timeline trace (LAB_TRACE): the production kernel with DBG bit 2048, 4 x uint64 per workgroup
+uint64_t* g_trace = nullptr;
+template <int EPI>
+void launch_trace(const Bufs& b, hipStream_t s) {
+  const int tiles = ((b.M + 255) / 256) * ((b.N + 255) / 256);
+  hipLaunchKernelGGL((gemm_nt_kernel<bf16, EPI, false, false, bf16, -1, -1, 2048>), dim3(tiles), dim3(512), 0, s, b.A, b.B,
+                     b.C, b.M, b.N, b.K, (int64_t)b.K, (int64_t)b.K, (int64_t)b.N, b.bias, b.aux, (int64_t)b.N, b.aux_out,
+                     b.part, 0, (const float*)g_trace, nullptr);
+}
+
+// Summary of one traced launch: per-phase durations, the gap between a workgroup's end and the next
+// start on the same CU, and how many workgroups sit in their epilogue at the same time (lockstep).
+void trace_summary(const Bufs& b, int epi, hipStream_t s, void (*fn)(const Bufs&, hipStream_t)) {
+  const int tiles = ((b.M + 255) / 256) * ((b.N + 255) / 256);
+  CK(hipMalloc(&g_trace, (size_t)tiles * 32));
+  fn(b, s);
+  CK(hipMemsetAsync(g_trace, 0, (size_t)tiles * 32, s));
+  fn(b, s);
+  std::vector<uint64_t> h((size_t)tiles * 4);
+  CK(hipMemcpyAsync(h.data(), g_trace, (size_t)tiles * 32, hipMemcpyDeviceToHost, s));
+  CK(hipStreamSynchronize(s));
+  CK(hipFree(g_trace));
+  g_trace = nullptr;
+  uint64_t t0 = ~0ull, tend = 0;
+  for (int i = 0; i < tiles; ++i) {
+    t0 = std::min(t0, h[i * 4]);
+    tend = std::max(tend, h[i * 4 + 2]);
+  }
+  std::vector<double> ml, ep, gaps;
+  std::vector<std::pair<uint64_t, int>> ev;  // (time, +1 epilogue start / -1 end)
+  std::map<uint64_t, std::vector<std::pair<uint64_t, uint64_t>>> percu;
+  for (int i = 0; i < tiles; ++i) {
+    const uint64_t a = h[i * 4], m = h[i * 4 + 1], e = h[i * 4 + 2], id = h[i * 4 + 3];
+    ml.push_back((m - a) * 0.01);
+    ep.push_back((e - m) * 0.01);
+    const uint64_t hw = id & 0xffffffffull, xcc = id >> 32;
+    const uint64_t cu = ((xcc & 0xf) << 16) | (((hw >> 13) & 7) << 8) | (((hw >> 12) & 1) << 4) | ((hw >> 8) & 0xf);
+    percu[cu].push_back({a, e});
+    ev.push_back({m, +1});
+    ev.push_back({e, -1});
+  }
+  for (auto& kv : percu) {
+    auto v = kv.second;
+    std::sort(v.begin(), v.end());
+    for (size_t j = 1; j < v.size(); ++j) gaps.push_back(((double)v[j].first - (double)v[j - 1].second) * 0.01);
+  }
+  std::sort(ev.begin(), ev.end());
+  // time-weighted histogram of the number of workgroups in their epilogue
+  int cur = 0, peak = 0;
+  double w[5] = {0, 0, 0, 0, 0};  // 0, 1-63, 64-127, 128-191, 192+
+  for (size_t j = 0; j + 1 < ev.size(); ++j) {
+    cur += ev[j].second;
+    peak = std::max(peak, cur);
+    const double dt = (double)(ev[j + 1].first - ev[j].first) * 0.01;
+    w[cur == 0 ? 0 : 1 + std::min(3, cur / 64)] += dt;
+  }
+  auto med = [](std::vector<double> v) {
+    if (v.empty()) return 0.0;
+    std::sort(v.begin(), v.end());
+    return v[v.size() / 2];
+  };
+  auto mean = [](const std::vector<double>& v) {
+    double t = 0;
+    for (double x : v) t += x;
+    return v.empty() ? 0.0 : t / v.size();
+  };
+  const double span = (tend - t0) * 0.01;
+  printf("{\"trace\": true, \"M\": %d, \"N\": %d, \"K\": %d, \"epi\": %d, \"span_us\": %.1f, \"cus\": %zu, "
+         "\"mainloop_us_med\": %.2f, \"mainloop_us_mean\": %.2f, \"epi_us_med\": %.2f, \"epi_us_mean\": %.2f, "
+         "\"gap_us_med\": %.2f, \"gap_us_mean\": %.2f, \"epi_concurrency_peak\": %d, "
+         "\"time_frac_epi_wgs\": {\"0\": %.3f, \"1-63\": %.3f, \"64-127\": %.3f, \"128-191\": %.3f, \"192+\": %.3f}}\n",
+         b.M, b.N, b.K, epi, span, percu.size(), med(ml), mean(ml), med(ep), mean(ep), med(gaps), mean(gaps), peak,
+         w[0] / span, w[1] / span, w[2] / span, w[3] / span, w[4] / span);
+  fflush(stdout);
+}
+
 template <int EPI, int DBG = 0>
 void launch_w4(const Bufs& b, hipStream_t s) {
   const int tiles = ((b.M + 255) / 256) * ((b.N + 255) / 256);
@@ -136,6 +213,7 @@ void run_epi(Bufs& b, int rounds, int reps, hipStream_t s) {
     vs.push_back({"w8_st3", launch_old<EPI, 0, 3>});
     vs.push_back({"w8_st5", launch_old<EPI, 0, 5>});
   }
+  if (full && getenv("LAB_TRACE")) trace_summary(b, EPI, s, launch_trace<EPI>);
   const int64_t MN = (int64_t)b.M * b.N;
   float* dmax;
   CK(hipMalloc(&dmax, 4));
