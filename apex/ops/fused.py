@@ -91,15 +91,32 @@ def _wgrad_tt_splits(M, N, K):
     the library, which is as fast or faster there. Auto is limited to the measured tile range
     (64 <= tiles < 128); larger weights (hundreds of tiles, e.g. Megatron / GPT MLPs) stay on the
     library until measured."""
-    if _WGRAD_TT == "0" or N % 256 or K % 256:
+    if _WGRAD_TT == "0" or N % 8 or K % 8:
         return 0
     if _WGRAD_TT not in ("auto", ""):
         s = int(_WGRAD_TT)
         return s if M % (64 * s) == 0 else 0
+    hit = _WGRAD_TT_MEASURED.get((N, K))
+    if hit is not None:
+        m_min, s = hit
+        return s if M >= m_min and M % (64 * s) == 0 else 0
+    if N % 256 or K % 256:
+        return 0  # partial tiles run on the kernel (forced counts above); auto keeps measured shapes only
     tiles = (N // 256) * (K // 256)
     if M < 16384 or tiles < 64 or tiles >= 128 or M % 256:
         return 0
     return max(1, 256 // tiles)
+
+
+# (N, K) -> (min tokens, slices): weight-gradient shapes routed to the transposed-read kernel by
+# measurement. Empty: in isolation (tools/wgrad_tt_bench.py, profiles/r5_wgrad_tt_gpt2_megatron.jsonl)
+# the kernel beat the library on GPT-2 1.5B's attention-out / FFN shapes (123 vs 142, 379 vs 458, 378 vs
+# 490 us at 16384 tokens, partial 256-tiles) and Megatron H2560's (122 vs 136, 437 vs 512 us), but the
+# GPT-2 model step with those shapes routed was 1.3 % SLOWER (84.2k vs 85.3k tokens/s, same box,
+# profiles/r5_gpt2_wgrad_tt_ab.jsonl; a likely cause, unverified: the isolated loop re-reads the same
+# ~260 MB of operands, mostly served from the 256 MB Infinity Cache) — so the library keeps them (forced APEX_WGRAD_TT=<slices>
+# still runs any multiple-of-8 shape on the kernel).
+_WGRAD_TT_MEASURED = {}
 
 
 def _gt(p):

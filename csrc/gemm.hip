@@ -193,7 +193,12 @@ __device__ __forceinline__ void stage_pieces(const T* __restrict__ g, int64_t ld
     if constexpr (TR) {
       const int r = piece * 2 + (lane >> 5);
       const int chunk = (lane & 31) ^ ftr(r);
-      glds16(g + (int64_t)(k0 + r) * ld + row0 + chunk * (16 / (int)sizeof(T)), lds_tile + piece * 1024);
+      // partial tiles (rows % 256, e.g. GPT-2's 1600 / 4800): chunks past the last row read the
+      // last full chunk instead (rows % 8 == 0) — they only feed output rows / columns the
+      // bounds-checked epilogue does not store, and the last K-row never reads past the tensor
+      int col = row0 + chunk * (16 / (int)sizeof(T));
+      col = col < rows ? col : rows - 16 / (int)sizeof(T);
+      glds16(g + (int64_t)(k0 + r) * ld + col, lds_tile + piece * 1024);
     } else {
       const int r = piece * 8 + (lane >> 3);
       const int chunk = (lane & 7) ^ ((r >> 1) & 7);
@@ -542,14 +547,17 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const void* p, uint3
 // Epilogue shared by both kernels (wave tile 128 x 64 at rows m0 + wr*128, cols n0 + wc*64).
 // Rounds the accumulators of a 128 x 64 wave tile (acc[J0 .. J0+3][*]) to T and writes them into the
 // wave's 16 KB LDS region in the layout the epilogue reads back (see epilogue()).
-template <typename T, int J0, int NJ>
+// I0 / NI: the fragment rows staged (NI = 4: one 64-row half of the wave tile into an 8 KB region,
+// local rows 0..63; the row's XOR pattern only depends on row & 15, so it is the same either way)
+template <typename T, int J0, int NJ, int I0 = 0, int NI = 8>
 __device__ __forceinline__ void stage_acc(const f32x4 (&acc)[NJ][8], char* reg, int lane, float alpha) {
   const int lr = lane & 15, lk = lane >> 4;
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int row = i * 16 + lr;
+    for (int ii = 0; ii < NI; ++ii) {
+      const int i = I0 + ii;
+      const int row = ii * 16 + lr;
       const int chunk = (2 * j + (lk >> 1)) ^ (row & 7);
       const int half = (lk & 1) ^ ((row >> 3) & 1);
       Pack<T, 4> pk;
@@ -563,12 +571,55 @@ __device__ __forceinline__ void stage_acc(const f32x4 (&acc)[NJ][8], char* reg, 
 // Q8 (1 + fp8 format, 0 = off): the C output's fp8 codes are written too (q8.y, ldc bytes per row,
 // scaled by q8.scale[0], max|C| into q8.amax) — the next GEMM's fp8 operand without a standalone
 // quantise pass over C
-template <typename T, int EPI, bool EDGE, int J0 = 0, int NJ = 4, bool STAGED = false, int Q8 = 0>
+// Loads the compiler does not see (the persistent kernel's epilogue): with LDS-DMA pieces of the next
+// tile in flight, hipcc waits vmcnt(0) before the first use of any load it issued itself, i.e. the
+// epilogue would stall on the next tile's prologue. These load through a descriptor held in SGPRs
+// (built from wave-uniform values: s_nop 4 covers the SGPR-write -> buffer-read hazard) and are
+// retired by explicit counted waits (asm_wait8 / asm_wait16) that name every destination register.
+typedef unsigned u32x4g __attribute__((ext_vector_type(4)));
+typedef int i32x4s __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ i32x4s sgpr_rsrc(const void* p, uint32_t bytes) {
+  const uint64_t a = (uint64_t)p;
+  return i32x4s{(int)__builtin_amdgcn_readfirstlane((uint32_t)a),
+                (int)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) & 0xffff,
+                (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000};
+}
+__device__ __forceinline__ u32x4g asm_load16(const i32x4s& rs, uint32_t voff, int soff) {
+  u32x4g d;
+  asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(d) : "v"(voff), "s"(rs), "s"(soff) : "memory");
+  return d;
+}
+template <int N>
+__device__ __forceinline__ void asm_wait(u32x4g (&r)[8]) {
+  asm volatile("s_waitcnt vmcnt(%8)"
+               : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), "+v"(r[6]), "+v"(r[7])
+               : "n"(N)
+               : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+template <int N>
+__device__ __forceinline__ void asm_wait1(u32x4g& r) {
+  asm volatile("s_waitcnt vmcnt(%1)" : "+v"(r) : "n"(N) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+struct NoHook {
+  __device__ __forceinline__ void operator()() const {}
+};
+
+// HALVES (the persistent kernel): `reg` is an 8 KB region; each 64-row half of the wave tile is staged
+// into it right before its 8 row slots are read back (the other 64 KB of LDS hold the next tile's
+// first K-tile meanwhile)
+// With HALVES the epilogue's own loads (bias, [M, N] input) are asm loads issued BEFORE `pre()` (the
+// caller's hook: the next tile's LDS-DMA pieces, exactly 8 per wave) and retired by counted waits that
+// leave those pieces (and this epilogue's stores) in flight.
+template <typename T, int EPI, bool EDGE, int J0 = 0, int NJ = 4, bool STAGED = false, int Q8 = 0,
+          bool HALVES = false, typename Hook = NoHook>
 __device__ __forceinline__ void epilogue(const f32x4 (&acc)[NJ][8], char* reg, T* __restrict__ C, int M, int N,
                                          int64_t ldc, const T* __restrict__ bias, const T* __restrict__ aux,
                                          int64_t ldaux, T* __restrict__ aux_out, float* __restrict__ part, int m0,
                                          int n0, int tm, int wr, int wc, int lane, float alpha = 1.f,
-                                         const Q8Out& q8 = Q8Out{}) {
+                                         const Q8Out& q8 = Q8Out{}, const Hook& pre = Hook{}) {
+  static_assert(!HALVES || (Q8 == 0 && !STAGED && !EDGE), "halved staging: full tiles, no fp8 codes, accumulators in registers");
   const int lr = lane & 15, lk = lane >> 4;
   // acc[j][i] holds rows wr*128 + i*16 + lr, cols wc*64 + j*16 + 4*lk .. +3 of the tile. The fp32
   // accumulators are rounded to T and transposed through the wave's own 16 KB LDS region
@@ -654,32 +705,71 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[NJ][8], char* reg, T
     // first half of the input operand in flight (sched_barriers pin the phase order: left alone,
     // the scheduler hoists both halves' loads above the transposition and spills around them)
     u32x4 ra[8];
-    if constexpr (AUX_IN) {
+    constexpr bool HAS_BIAS = EPI == EPI_BIAS || GELU_FWD;
+    u32x4g braw = u32x4g{0u, 0u, 0u, 0u};
+    i32x4s rsx_s = i32x4s{0, 0, 0, 0};
+    if constexpr (HALVES) {
+      if constexpr (AUX_IN) {
+        rsx_s = sgpr_rsrc(aux + (int64_t)wrow0 * ldaux + wcol0, (uint32_t)(128 * ldaux * (int64_t)sizeof(T)));
+#pragma unroll
+        for (int it = 0; it < 8; ++it) ra[it] = asm_load16(rsx_s, voff(ldaux, it), soff(ldaux, it));
+        pre();
+        __builtin_amdgcn_sched_barrier(0);
+        stage_acc<T, J0, NJ, 0, 4>(acc, reg, lane, alpha);
+        __builtin_amdgcn_sched_barrier(0);
+        asm_wait<8>(ra);  // the 8 pieces of pre() are younger
+      } else {
+        if constexpr (HAS_BIAS) braw = asm_load16(sgpr_rsrc(bias + n0 + wc * 64, 128), (uint32_t)((lane & 7) * 16), 0);
+        pre();
+        __builtin_amdgcn_sched_barrier(0);
+        stage_acc<T, J0, NJ, 0, 4>(acc, reg, lane, alpha);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (HAS_BIAS) asm_wait1<8>(braw);
+      }
+    } else if constexpr (AUX_IN) {
 #pragma unroll
       for (int it = 0; it < 8; ++it) ra[it] = __builtin_amdgcn_raw_buffer_load_b128(rs_x, voff(ldaux, it), soff(ldaux, it), 0);
     }
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (!STAGED) stage_acc<T, J0, NJ>(acc, reg, lane, alpha);
+    if constexpr (!STAGED && !HALVES) stage_acc<T, J0, NJ>(acc, reg, lane, alpha);
     __builtin_amdgcn_sched_barrier(0);
     float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if constexpr (EPI == EPI_BIAS || GELU_FWD) {
-      const int nc = ncol < N ? ncol : N - 8;  // (N % 8 == 0: edge lanes read a valid chunk, unused)
-      unpack(*reinterpret_cast<const u32x4*>(bias + nc), bv);
+    if constexpr (HAS_BIAS) {
+      if constexpr (HALVES) {
+        unpack(*reinterpret_cast<const u32x4*>(&braw), bv);
+      } else {
+        const int nc = ncol < N ? ncol : N - 8;  // (N % 8 == 0: edge lanes read a valid chunk, unused)
+        unpack(*reinterpret_cast<const u32x4*>(bias + nc), bv);
+      }
     }
     float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     u32x4 rb[8];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       u32x4 rc[8];
+      if constexpr (HALVES) {
+        if (h == 1) {  // (half 0 was staged before the first wait; LDS ops of one wave run in order)
+          stage_acc<T, J0, NJ, 4, 4>(acc, reg, lane, alpha);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
 #pragma unroll
       for (int it = 0; it < 8; ++it) {
-        const int row = (8 * h + it) * 8 + lrow, c = lane & 7;
+        const int row = ((HALVES ? 0 : 8 * h) + it) * 8 + lrow, c = lane & 7;
         u32x4 x = *reinterpret_cast<const u32x4*>(reg + row * 128 + ((c ^ (row & 7)) << 4));
         if ((row >> 3) & 1) x = u32x4{x[2], x[3], x[0], x[1]};
         rc[it] = x;
       }
       if constexpr (AUX_IN) {
-        if (h == 0) {
+        if constexpr (HALVES) {
+          // second half of the input: issued now, retired at h = 1 behind the 8 stores of h = 0
+          if (h == 0) {
+#pragma unroll
+            for (int it = 0; it < 8; ++it) rb[it] = asm_load16(rsx_s, voff(ldaux, 8 + it), soff(ldaux, 8 + it));
+          } else {
+            asm_wait<8>(rb);
+          }
+        } else if (h == 0) {
 #pragma unroll
           for (int it = 0; it < 8; ++it)
             rb[it] = __builtin_amdgcn_raw_buffer_load_b128(rs_x, voff(ldaux, 8 + it), soff(ldaux, 8 + it), 0);
@@ -963,6 +1053,165 @@ __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(const TI* __restrict
   }
 }
 
+
+// ============================================================================================
+// Persistent kernel: one workgroup per CU walks the tile list; the next tile's first K-tile is
+// loaded while this tile's epilogue runs.
+//
+// The timeline trace of the one-tile-per-workgroup kernel (tools/gemmlab LAB_TRACE,
+// profiles/r5_gemm_trace_m98304.jsonl) puts 3.2-11.4 us of epilogue and ~0.5 us of dispatch gap
+// after each 25-28 us main loop at K = 1024, and the main loop itself includes the prologue: the
+// first K-tile's 64 KB arriving while every CU's new workgroup asks for its own at once. Here the
+// workgroup, after its last main-loop read of LDS:
+//   1. issues the NEXT tile's A(0) and B(0) (buffer 0, 64 KB) — they load during the epilogue;
+//   2. runs the epilogue with its accumulators staged through buffer 1 in two 64-row halves (8 KB per
+//      wave instead of 16 KB);
+//   3. barrier (buffer 1 free), issues B(1) into it, and waits for A(0) / B(0) with a COUNTED vmcnt
+//      that leaves this epilogue's stores (and B(1)) in flight: loads, stores and LDS-DMA retire in
+//      issue order, so vmcnt(stores + 4) retires exactly the 8 older pieces;
+//   4. re-staggers the wave groups and enters the next tile's main loop (mainloop_bal's body).
+// Tiles: workgroup b takes virtual block ids b, b + G, b + 2G, ... (G = grid, a multiple of 8) through
+// the same bijective XCD remap + GROUP_M order as gemm_nt_kernel, so the tiles an XCD runs at once
+// are the same adjacent ones. Full tiles only (M, N multiples of 256), 16-bit NT, no fp8 codes.
+__device__ __forceinline__ void tile_coords(int v, int tiles_m, int tiles_n, int& m0, int& n0, int& tm) {
+  const int nwg = tiles_m * tiles_n;
+  const int xcd = v & 7, q = nwg >> 3, rr = nwg & 7;
+  const int wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (v >> 3);
+  const int group = G_GROUP_M * tiles_n;
+  const int first_m = (wg / group) * G_GROUP_M;
+  const int gm = min(tiles_m - first_m, G_GROUP_M);
+  tm = first_m + (wg % group) % gm;
+  const int tn = (wg % group) / gm;
+  m0 = tm * GB_M;
+  n0 = tn * GB_N;
+}
+
+// vector-memory instructions one wave's epilogue issues after the next tile's A(0) / B(0) pieces,
+// counting only those that can still be in flight at the wait: the stores (its loads are consumed
+// inside the epilogue, so they have retired). Must not exceed the true count (a larger vmcnt would
+// let A(0) / B(0) through unretired): C 16, + pre-activation or gelu' 16, + the bias-grad partial row
+// 2 (lanes 0..7).
+template <int EPI> constexpr int epi_stores() {
+  constexpr bool GELU_FWD = EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_TANH || EPI == EPI_BIAS_GELU_D ||
+                            EPI == EPI_BIAS_GELU_TANH_D;
+  constexpr bool COLSUM = EPI == EPI_DGELU || EPI == EPI_DGELU_TANH || EPI == EPI_MUL;
+  return 16 + (GELU_FWD ? 16 : 0) + (COLSUM ? 2 : 0);
+}
+
+template <typename T, int EPI, int DBG = 0>
+__global__ void __launch_bounds__(G_THREADS) gemm_persist_kernel(const T* __restrict__ A, const T* __restrict__ B,
+                                                                 T* __restrict__ C, int M, int N, int K, int64_t lda,
+                                                                 int64_t ldb, int64_t ldc, const T* __restrict__ bias,
+                                                                 const T* __restrict__ aux, int64_t ldaux,
+                                                                 T* __restrict__ aux_out, float* __restrict__ part,
+                                                                 uint64_t* __restrict__ trace) {
+  __shared__ __attribute__((aligned(16))) char smem[G_LDS_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+  const int tiles_m = M / GB_M, tiles_n = N / GB_N, nwg = tiles_m * tiles_n;
+  const int G = gridDim.x;
+  constexpr int BKE = 64;
+  const int nt = K / BKE;
+  int v = blockIdx.x;
+  if (v >= nwg) return;  // (the host sizes the grid to at most the tile count)
+  int m0, n0, tm;
+  tile_coords(v, tiles_m, tiles_n, m0, n0, tm);
+  // first tile's prologue (mainloop_bal's): A(0), B(0) -> buffer 0, B(1) -> buffer 1
+  stage_pieces<T, false>(A, lda, m0, M, 0, smem, wid, lane, 0);
+  stage_pieces<T, false>(A, lda, m0, M, 0, smem, wid, lane, 2);
+  stage_pieces<T, false>(B, ldb, n0, N, 0, smem + G_TILE_BYTES, wid, lane, 0);
+  stage_pieces<T, false>(B, ldb, n0, N, 0, smem + G_TILE_BYTES, wid, lane, 2);
+  if (nt > 1) {
+    stage_pieces<T, false>(B, ldb, n0, N, BKE, smem + G_BUF_BYTES + G_TILE_BYTES, wid, lane, 0);
+    stage_pieces<T, false>(B, ldb, n0, N, BKE, smem + G_BUF_BYTES + G_TILE_BYTES, wid, lane, 2);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  bar();
+  for (;;) {
+    uint64_t tr0 = 0, tr1 = 0;
+    if constexpr (DBG & 2048) tr0 = __builtin_amdgcn_s_memrealtime();
+    f32x4 acc[4][8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (wr == 1) bar();  // stagger group 1 by one barrier
+    // the K loop's per-lane addresses from an opaque lane copy: recomputed per tile rather than kept
+    // live through the epilogue (where they spilled, and a scratch reload at the next tile's start
+    // waits, in vmcnt order, for every epilogue store still in flight)
+    int lane_k = lane;
+    asm volatile("" : "+v"(lane_k));
+    const int lrk = lane_k & 15, lkk = lane_k >> 4;
+    s16x8 fa[4][2], fb[2][2][2];
+    read_fb<false>(fb[0], smem + G_TILE_BYTES, wc * 64, lrk, lkk);  // tile 0's first B half
+    int t = 0;
+    for (; t + 1 < nt; t += 2) {
+      bal_tile<T, false, -1, -1, 0, 0>(t, nt, A, B, M, N, lda, ldb, m0, n0, smem, wid, wr, wc, lane_k, acc, fa, fb);
+      bal_tile<T, false, -1, -1, 0, 1>(t + 1, nt, A, B, M, N, lda, ldb, m0, n0, smem, wid, wr, wc, lane_k, acc, fa, fb);
+    }
+    if (t < nt) bal_tile<T, false, -1, -1, 0, 0>(t, nt, A, B, M, N, lda, ldb, m0, n0, smem, wid, wr, wc, lane_k, acc, fa, fb);
+    if (wr == 0) bar();  // re-align the groups
+    bar();               // every wave is past its last ds_read of this tile
+    if constexpr (DBG & 2048) tr1 = __builtin_amdgcn_s_memrealtime();
+    const int vn = v + G;
+    const bool more = vn < nwg;
+    int m1 = 0, n1 = 0, tm1 = 0;
+    // an opaque copy of the lane id: everything the epilogue and the next tile's staging derive from
+    // it is computed here, not hoisted above the K loop (where it stayed live and spilled ~55 VGPRs)
+    int lane_e = lane;
+    asm volatile("" : "+v"(lane_e));
+    if (more) {
+      tile_coords(vn, tiles_m, tiles_n, m1, n1, tm1);
+    } else {  // the last tile re-loads its own first K-tile (unused): the epilogue's counted waits
+      m1 = m0;  // assume exactly 8 pieces behind its first loads
+      n1 = n0;
+    }
+    // the next tile's A(0), B(0): issued by the epilogue after its own first loads (hook)
+    auto next_k0 = [&]() {
+      stage_pieces<T, false>(A, lda, m1, M, 0, smem, wid, lane_e, 0);
+      stage_pieces<T, false>(A, lda, m1, M, 0, smem, wid, lane_e, 2);
+      stage_pieces<T, false>(B, ldb, n1, N, 0, smem + G_TILE_BYTES, wid, lane_e, 0);
+      stage_pieces<T, false>(B, ldb, n1, N, 0, smem + G_TILE_BYTES, wid, lane_e, 2);
+    };
+    __builtin_amdgcn_sched_barrier(0);
+    epilogue<T, EPI, false, 0, 4, false, 0, true>(acc, smem + G_BUF_BYTES + wid * 8192, C, M, N, ldc, bias, aux,
+                                                   ldaux, aux_out, part, m0, n0, tm, wr, wc, lane_e, 1.f, Q8Out{},
+                                                   next_k0);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (DBG & 2048) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      bar();
+      const uint64_t tr2 = __builtin_amdgcn_s_memrealtime();
+      if (tid == 0) {
+        uint32_t hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        uint64_t* tp = trace + (int64_t)v * 4;
+        tp[0] = tr0;
+        tp[1] = tr1;
+        tp[2] = tr2;
+        tp[3] = (uint64_t)hw | ((uint64_t)xcc << 32);
+      }
+    }
+    if (!more) break;
+    bar();  // every wave is done with its epilogue region: buffer 1 is free
+    if (nt > 1) {
+      stage_pieces<T, false>(B, ldb, n1, N, BKE, smem + G_BUF_BYTES + G_TILE_BYTES, wid, lane_e, 0);
+      stage_pieces<T, false>(B, ldb, n1, N, BKE, smem + G_BUF_BYTES + G_TILE_BYTES, wid, lane_e, 2);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(epi_stores<EPI>() + 4) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(epi_stores<EPI>()) : "memory");
+    }
+    bar();  // A(0), B(0) of the next tile visible to every wave
+    v = vn;
+    m0 = m1;
+    n0 = n1;
+    tm = tm1;
+  }
+}
 
 // ============================================================================================
 // Four-wave kernel ("w4"): the same 256 x 256 x 64 output tile and LDS image, but 256 threads =
@@ -1863,9 +2112,43 @@ inline bool host_m32(int epi) {
   return (mask >> epi) & 1;
 }
 
+// Persistent kernel (gemm_persist_kernel) for full-tile 16-bit NT launches: APEX_GEMM_PERSIST=0 turns it
+// off (A/B). Measured against the one-tile-per-workgroup kernel at the BERT shapes, same process,
+// interleaved, bit-identical outputs (profiles/r5_gemm_persist_m98304.jsonl): 0.7-3.6 % faster on
+// every shape (plain / bias 3.6 %, residual 1-3 %, GELU_D 1.9 %, multiply 0.7 %).
+inline bool host_persist() {
+  static int on = -1;
+  if (on == -1) {
+    const char* e = getenv("APEX_GEMM_PERSIST");
+    on = (e && e[0] == '0') ? 0 : 1;
+  }
+  return on == 1;
+}
+inline int host_cus() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    cus = n;
+  }
+  return cus;
+}
+
 template <typename T, int EPI, bool TR = false>
 void launch_gemm(const GemmArgs& g, hipStream_t s) {
   const int tiles = ((g.M + GB_M - 1) / GB_M) * ((g.N + GB_N - 1) / GB_N);
+  if constexpr (!TR && EPI != EPI_F32 && EPI != EPI_F32_ACC) {
+    if (g.M % GB_M == 0 && g.N % GB_N == 0 && tiles > host_cus() && host_persist() && h_gemm_dbg == 0 &&
+        h_gemm_stagger <= 0 && !host_m32(EPI)) {
+      // more tiles than CUs: one workgroup per CU walks them (the grid stays a multiple of 8)
+      const int grid = (host_cus() / 8) * 8;
+      hipLaunchKernelGGL((gemm_persist_kernel<T, EPI>), dim3(grid), dim3(G_THREADS), 0, s, (const T*)g.A, (const T*)g.B,
+                         (T*)g.C, g.M, g.N, g.K, g.lda, g.ldb, g.ldc, (const T*)g.bias, (const T*)g.aux, g.ldaux,
+                         (T*)g.aux_out, g.part, (uint64_t*)nullptr);
+      return;
+    }
+  }
   if constexpr (!TR && std::is_same<T, bf16>::value && EPI != EPI_F32 && EPI != EPI_F32_ACC) {
     if (host_m32(EPI)) {
       if (g.M % GB_M != 0 || g.N % GB_N != 0)
@@ -1881,9 +2164,9 @@ void launch_gemm(const GemmArgs& g, hipStream_t s) {
   }
   const int units = h_gemm_stagger > 0 ? h_gemm_stagger : h_gemm_stagger < 0 ? 0 : host_stagger(EPI);
   const int stagger = (units & 0xffff) | (h_gemm_dbg << 16);  // the kernel's ctl word
-  const bool edge = !TR && (g.M % GB_M != 0 || g.N % GB_N != 0);  // (gemm_tt shapes are tile multiples)
-  if (!TR && edge)
-    hipLaunchKernelGGL((gemm_nt_kernel<T, EPI, TR, !TR>), dim3(tiles, TR ? g.splits : 1), dim3(G_THREADS), 0, s,
+  const bool edge = g.M % GB_M != 0 || g.N % GB_N != 0;
+  if (edge)  // (the transposed-read weight-gradient kernels too: partial tiles since round 5)
+    hipLaunchKernelGGL((gemm_nt_kernel<T, EPI, TR, true>), dim3(tiles, TR ? g.splits : 1), dim3(G_THREADS), 0, s,
                        (const T*)g.A, (const T*)g.B, (T*)g.C, g.M, g.N, g.K, g.lda, g.ldb, g.ldc, (const T*)g.bias,
                        (const T*)g.aux, g.ldaux, (T*)g.aux_out, g.part, stagger);
   else
@@ -2014,7 +2297,8 @@ int gemm_nt_f8(const GemmArgs& g, int fmt_a, int fmt_b, int out_dt, hipStream_t 
 }
 
 bool gemm_tt_supported(int P, int Q, int R, int splits, int64_t lda, int64_t ldb) {
-  return P > 0 && Q > 0 && splits > 0 && P % GB_M == 0 && Q % GB_N == 0 && R % (splits * GB_K) == 0 &&
+  // P, Q: any multiple of 8 (partial 256-tiles: clamped staging + bounds-checked epilogues)
+  return P > 0 && Q > 0 && splits > 0 && P % 8 == 0 && Q % 8 == 0 && R % (splits * GB_K) == 0 &&
          lda % 8 == 0 && ldb % 8 == 0;
 }
 

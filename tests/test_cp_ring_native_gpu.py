@@ -81,13 +81,19 @@ def test_ring_threads_match_full_attention(W, causal, dkv_fp32, monkeypatch):
     monkeypatch.setattr(cp, "_Ring", _fake_ring(mail))
     res, errs = [None] * W, []
 
+    class Ctx:  # the Function's forward / backward called directly in each rank's thread: autograd
+        def save_for_backward(self, *t):  # would run every rank's backward on its one device thread
+            self.saved_tensors = t
+
     def rank(r):
         try:
-            ql, kl, vl = (shard(t, r).requires_grad_(True) for t in (q, k, v))
-            o = cp._RingAttention.apply(ql, kl, vl, None, list(range(W)), r, causal, scale, 0.0, "zigzag")
-            o.backward(shard(do, r))
+            ql, kl, vl = (shard(t, r) for t in (q, k, v))
+            ctx = Ctx()
+            with torch.no_grad():
+                o = cp._RingAttention.forward(ctx, ql, kl, vl, None, list(range(W)), r, causal, scale, 0.0, "zigzag")
+                dq, dk, dv = cp._RingAttention.backward(ctx, shard(do, r))[:3]
             torch.cuda.synchronize()
-            res[r] = (o.detach(), ql.grad, kl.grad, vl.grad)
+            res[r] = (o, dq, dk, dv)
         except Exception as e:  # surfaced below
             errs.append(e)
 

@@ -179,7 +179,10 @@ def test_gemm_supported_rejects():
 
 
 @pytest.mark.parametrize("R,P,Q,splits", [(256, 256, 256, 1), (1024, 256, 512, 2), (2048, 512, 256, 4),
-                                          (8192, 1024, 1024, 8), (64, 256, 256, 1), (576, 256, 512, 3)])
+                                          (8192, 1024, 1024, 8), (64, 256, 256, 1), (576, 256, 512, 3),
+                                          # partial 256-tiles (GPT-2's 1600 / 4800): clamped staging
+                                          (1024, 1600, 480, 2), (512, 200, 264, 1), (2048, 4800, 1600, 4),
+                                          (128, 8, 1608, 1)])
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 def test_gemm_tt_weight_grad(R, P, Q, splits, dt):
     """dW = dY^T X through the transposed-read (ds_read_b64_tr_b16) main loop, split-K slabs."""
@@ -219,6 +222,24 @@ def test_wgrad_tt_policy_writes_slot(N, K, monkeypatch):
     monkeypatch.setattr(fused, "_WGRAD_TT", "0")
     lib = fused._wgrad(dy, x)
     _close(slot, lib.float(), 1e-2)
+
+
+def test_gemm_tt_acc_partial_tiles():
+    """main_grad accumulation (EPI_F32_ACC read-modify-write) on a partial-tile shape: only [P, Q] is
+    touched (a guard band after the accumulator stays), the sum adds onto the previous contents."""
+    C = _C()
+    torch.manual_seed(3)
+    R, P, Q = 1024, 1600, 488
+    dy = torch.randn(R, P, device=DEV).bfloat16()
+    x = torch.randn(R, Q, device=DEV).bfloat16()
+    buf = torch.full((P * Q + 256,), 5.0, device=DEV)
+    mg = buf[:P * Q].view(P, Q)
+    mg.copy_(torch.randn(P, Q, device=DEV))
+    before = mg.clone()
+    C.gemm_tt_acc(dy, x, mg)
+    ref = before + dy.float().t() @ x.float()
+    _close(mg, ref, 1e-4)
+    assert (buf[P * Q:] == 5.0).all()
 
 
 def test_gemm_tt_asymmetric_identity():

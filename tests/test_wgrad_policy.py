@@ -11,8 +11,8 @@ def test_tt_auto_takes_the_ffn_shapes_only(monkeypatch):
     assert fused._wgrad_tt_splits(M, 3072, 1024) == 0  # QKV (48 tiles): library
     assert fused._wgrad_tt_splits(M, 1024, 1024) == 0  # attention out (16 tiles): library
     assert fused._wgrad_tt_splits(8192, 4096, 1024) == 0  # too few tokens
-    assert fused._wgrad_tt_splits(M, 1600, 6400) == 0  # not tile multiples
-    assert fused._wgrad_tt_splits(M, 10240, 2560) == 0  # 400 tiles: unmeasured range, library
+    assert fused._wgrad_tt_splits(M, 1600, 4800) == 0  # partial tiles, unmeasured: library
+    assert fused._wgrad_tt_splits(M, 2560, 7680) == 0  # 300 tiles: unmeasured, library
 
 
 def test_tt_overrides(monkeypatch):
@@ -21,6 +21,13 @@ def test_tt_overrides(monkeypatch):
     monkeypatch.setattr(fused, "_WGRAD_TT", "8")
     assert fused._wgrad_tt_splits(98304, 3072, 1024) == 8
     assert fused._wgrad_tt_splits(98304 + 64, 3072, 1024) == 0  # slices must divide into K-tiles
+    assert fused._wgrad_tt_splits(16384, 4800, 1600) == 8  # partial tiles: the forced count applies
+    monkeypatch.setattr(fused, "_WGRAD_TT", "auto")
+    assert fused._wgrad_tt_splits(16384, 4800, 1600) == 0  # GPT-2 QKV: the library wins it
+    assert fused._wgrad_tt_splits(16384, 6400, 1600) == 0  # GPT-2 FFN: faster alone, slower in the model
+    monkeypatch.setattr(fused, "_WGRAD_TT_MEASURED", {(6400, 1600): (16384, 4)})
+    assert fused._wgrad_tt_splits(16384, 6400, 1600) == 4  # a measured entry routes its shape
+    assert fused._wgrad_tt_splits(8192, 6400, 1600) == 0  # ... from its token count up
 
 
 def test_library_split_k_fills_the_chip(monkeypatch):

@@ -86,10 +86,21 @@ void launch_trace(const Bufs& b, hipStream_t s) {
                      b.part, 0, (const float*)g_trace, nullptr);
 }
 
+int g_cus = 0;
+template <int EPI, int DBG = 0>
+void launch_persist(const Bufs& b, hipStream_t s) {
+  const int tiles = (b.M / 256) * (b.N / 256);
+  const int grid = std::min(tiles, g_cus);
+  hipLaunchKernelGGL((gemm_persist_kernel<bf16, EPI, DBG>), dim3(grid), dim3(512), 0, s, b.A, b.B, b.C, b.M, b.N, b.K,
+                     (int64_t)b.K, (int64_t)b.K, (int64_t)b.N, b.bias, b.aux, (int64_t)b.N, b.aux_out, b.part, g_trace);
+}
+
 // Summary of one traced launch: per-phase durations, the gap between a workgroup's end and the next
 // start on the same CU, and how many workgroups sit in their epilogue at the same time (lockstep).
 void trace_summary(const Bufs& b, int epi, hipStream_t s, void (*fn)(const Bufs&, hipStream_t)) {
   const int tiles = ((b.M + 255) / 256) * ((b.N + 255) / 256);
+  static int call = 0;
+  const char* tname = (call++ % 2) ? "persist" : "w8";
   CK(hipMalloc(&g_trace, (size_t)tiles * 32));
   fn(b, s);
   CK(hipMemsetAsync(g_trace, 0, (size_t)tiles * 32, s));
@@ -143,11 +154,11 @@ void trace_summary(const Bufs& b, int epi, hipStream_t s, void (*fn)(const Bufs&
     return v.empty() ? 0.0 : t / v.size();
   };
   const double span = (tend - t0) * 0.01;
-  printf("{\"trace\": true, \"M\": %d, \"N\": %d, \"K\": %d, \"epi\": %d, \"span_us\": %.1f, \"cus\": %zu, "
+  printf("{\"trace\": \"%s\", \"M\": %d, \"N\": %d, \"K\": %d, \"epi\": %d, \"span_us\": %.1f, \"cus\": %zu, "
          "\"mainloop_us_med\": %.2f, \"mainloop_us_mean\": %.2f, \"epi_us_med\": %.2f, \"epi_us_mean\": %.2f, "
          "\"gap_us_med\": %.2f, \"gap_us_mean\": %.2f, \"epi_concurrency_peak\": %d, "
          "\"time_frac_epi_wgs\": {\"0\": %.3f, \"1-63\": %.3f, \"64-127\": %.3f, \"128-191\": %.3f, \"192+\": %.3f}}\n",
-         b.M, b.N, b.K, epi, span, percu.size(), med(ml), mean(ml), med(ep), mean(ep), med(gaps), mean(gaps), peak,
+         tname, b.M, b.N, b.K, epi, span, percu.size(), med(ml), mean(ml), med(ep), mean(ep), med(gaps), mean(gaps), peak,
          w[0] / span, w[1] / span, w[2] / span, w[3] / span, w[4] / span);
   fflush(stdout);
 }
@@ -213,7 +224,11 @@ void run_epi(Bufs& b, int rounds, int reps, hipStream_t s) {
     vs.push_back({"w8_st3", launch_old<EPI, 0, 3>});
     vs.push_back({"w8_st5", launch_old<EPI, 0, 5>});
   }
-  if (full && getenv("LAB_TRACE")) trace_summary(b, EPI, s, launch_trace<EPI>);
+  if (full && getenv("LAB_TRACE")) {
+    trace_summary(b, EPI, s, launch_trace<EPI>);
+    trace_summary(b, EPI, s, launch_persist<EPI, 2048>);
+  }
+  if (full && !getenv("LAB_NOPERSIST")) vs.push_back({"w8pers", launch_persist<EPI>});
   const int64_t MN = (int64_t)b.M * b.N;
   float* dmax;
   CK(hipMalloc(&dmax, 4));
@@ -305,6 +320,7 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&b.part, (int64_t)((b.M + 255) / 256) * 2 * b.N * 4));
   hipStream_t s;
   CK(hipStreamCreate(&s));
+  CK(hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, 0));
   hipLaunchKernelGGL(fill_kernel, dim3(2048), dim3(256), 0, s, b.A, MK, 1u, 1.f);
   hipLaunchKernelGGL(fill_kernel, dim3(2048), dim3(256), 0, s, b.B, NK, 2u, 1.f / sqrtf((float)b.K));
   hipLaunchKernelGGL(fill_kernel, dim3(64), dim3(256), 0, s, b.bias, (int64_t)b.N, 3u, 0.1f);

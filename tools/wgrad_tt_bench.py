@@ -18,17 +18,30 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():
+    import argparse
+
     from apex.ops import fused
 
-    M = 98304
-    shapes = {"qkv": (3072, 1024), "attn_out": (1024, 1024), "ffn1": (4096, 1024), "ffn2": (1024, 4096)}
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--M", type=int, default=98304)
+    ap.add_argument("--shapes", default="qkv:3072x1024,attn_out:1024x1024,ffn1:4096x1024,ffn2:1024x4096",
+                    help="name:NxK,... (GPT-2 1.5B at M = 16384: qkv:4800x1600,attn_out:1600x1600,"
+                         "ffn1:6400x1600,ffn2:1600x6400)")
+    ap.add_argument("--splits", default="2,4,8,16")
+    args = ap.parse_args()
+    M = args.M
+    shapes = {}
+    for item in args.shapes.split(","):
+        name, nk = item.split(":")
+        n, k = nk.split("x")
+        shapes[name] = (int(n), int(k))
     torch.manual_seed(0)
     for name, (n, k) in shapes.items():
         dy = torch.randn(M, n, device="cuda", dtype=torch.bfloat16)
         x = torch.randn(M, k, device="cuda", dtype=torch.bfloat16)
         out = torch.empty(n, k, device="cuda", dtype=torch.bfloat16)
         paths = {"lib": "0"}
-        for s in (2, 4, 8, 16):
+        for s in (int(x) for x in args.splits.split(",")):
             if M % (64 * s) == 0:
                 paths[f"tt_s{s}"] = str(s)
         paths["auto"] = "auto"
