@@ -151,9 +151,13 @@ class Fp8State:
             s = st.slots.pop((key, role), None)
             if s is not None:
                 st._fresh.discard(s)
-                # reusable only from the next step() on, in sorted order: finalizers run when the
-                # garbage collector gets to them, which need not be the same point on every rank
-                # of the amax reduction group — slot i must name the same role on all of them
+                # reusable only from the next step() on, in sorted order. That makes the ORDER of
+                # reuse the same on every rank of the amax reduction group, not its TIMING: a tensor
+                # freed by refcounting dies at the same point of the step everywhere, but one caught
+                # in a reference cycle dies when the cyclic GC runs, which can fall on different
+                # sides of a step() boundary on different ranks — the slot is then recycled a step
+                # apart and, for that step, the reduced amax mixes two roles (a one-step scale error,
+                # not a crash). Keep fp8 weights out of reference cycles to stay exact.
                 st._dying.append(s)
         st._wcache.pop(key, None)
 

@@ -103,8 +103,9 @@ def test_slot_keys_survive_id_reuse_and_recycle():
     """Slots are keyed by a counter stored on the tensor, not id(): a tensor re-created every
     step (an O1 cast) reuses the freed slot instead of growing the buffers, and a new tensor never
     inherits a dead one's scale history. A freed slot is reusable only after the next step()
-    boundary (_recycle_slots), in sorted order, so every rank of the amax reduction group agrees
-    on slot numbers whatever order its garbage collector ran the finalizers in."""
+    boundary (_recycle_slots), in sorted order, so every rank of the amax reduction group reuses
+    slots in the same order (the timing still depends on when each rank frees the tensor: see
+    Fp8State._release)."""
     st = fp8.Fp8State(device="cpu")
     for step in range(50):
         w = torch.randn(4, 4)  # a fresh per-step weight copy

@@ -67,6 +67,17 @@ void tr(const Prob& p, hipStream_t s) {
                      (int64_t)0, nullptr, p.part, 0);
 }
 
+// the four-wave kernel (one wave per SIMD, 128 x 128 wave tiles: half the fragment reads per FLOP
+// of the 8-wave 128 x 64 tile, which matters most for the transposed reads' doubled LDS instruction
+// count); DBG 256 = its register-staged loop
+template <int EPI, int DBG>
+void tr_w4(const Prob& p, hipStream_t s) {
+  const int tiles = (p.P / GB_M) * (p.Q / GB_N);
+  hipLaunchKernelGGL((gemm_w4_kernel<bf16, EPI, true, false, DBG>), dim3(tiles, p.S), dim3(W_THREADS), 0, s, p.A, p.B,
+                     p.C, p.P, p.Q, p.R / p.S, (int64_t)p.P, (int64_t)p.Q, (int64_t)p.Q, nullptr, nullptr, (int64_t)0,
+                     nullptr, p.part);
+}
+
 template <int EPI, int DBG>
 void nt(const Prob& p, hipStream_t s) {
   const int Kc = p.R / p.S, M = p.P * p.S;
@@ -107,6 +118,8 @@ int main(int argc, char** argv) {
     void (*fn)(const Prob&, hipStream_t);
   };
   std::vector<V> vs = {{"tr_f32", tr<EPI_F32, 0>},
+                       {"tr_w4_f32", tr_w4<EPI_F32, 0>},
+                       {"tr_w4r_f32", tr_w4<EPI_F32, 256>},
                        {"tr_f32_old", tr<EPI_F32, 1024>},
                        {"tr_noepi", tr<EPI_NONE, 512>},
                        {"tr_noepi_old", tr<EPI_NONE, 512 + 1024>},
@@ -127,7 +140,7 @@ int main(int argc, char** argv) {
     if (nm == "tr_f32" || nm == "nt_f32") {
       vs[v].fn(p, s);
       CK(hipMemcpyAsync(ref, p.part, nP * 4, hipMemcpyDeviceToDevice, s));
-    } else if (nm == "tr_f32_old" || nm == "nt_f32_old") {
+    } else if (nm == "tr_f32_old" || nm == "nt_f32_old" || nm == "tr_w4_f32" || nm == "tr_w4r_f32") {
       CK(hipMemsetAsync(p.part, 0, nP * 4, s));
       vs[v].fn(p, s);
       CK(hipMemsetAsync(dmax, 0, 4, s));
