@@ -7,9 +7,13 @@ The reference (apex) has no fp8 path; this is an MI355X-first extension of its a
 What runs in fp8
   forward   y = x W^T (+ bias / GELU / residual epilogue)    x: e4m3, W: e4m3
   backward  dx = dy W (+ dGELU / residual epilogue)          dy: e5m2 ("hybrid"), W^T: e4m3
-  weight gradients stay in the activation dtype (bf16 via hipBLASLt split-K), as do attention,
-  normalisation and the optimizer. Outputs are bf16 / fp16, produced by the same fused
-  epilogues as the bf16 path.
+  weight    dW = dy^T x                                        dy: e5m2, x: e4m3 (the SAME codes the
+            two GEMMs above consumed, kept from the forward; csrc/gemm.hip gemm_tt_f8, a
+            ds_read_b64_tr_b8 transposed-read main loop over the token-major codes, fp32 split-K
+            slabs rounded once into the gradient slot). Recipe ``fp8_wgrad`` / APEX_FP8_WGRAD=0:
+            bf16 weight gradients instead.
+  Attention, normalisation and the optimizer stay in the activation dtype. Outputs are bf16 /
+  fp16, produced by the same fused epilogues as the bf16 path.
 
 Scaling
   * weights: current scaling — quantised (and transposed for the backward) once per optimizer
@@ -42,6 +46,7 @@ from __future__ import annotations
 
 import contextlib
 import dataclasses
+import os
 import weakref
 from typing import Optional
 
@@ -66,6 +71,7 @@ class Fp8Recipe:
     bwd_format: str = "e5m2"
     amax_reduction_group: Optional[object] = None
     reduce_amax: bool = True
+    fp8_wgrad: bool = True
 
     def fmt(self, which):
         name = self.fwd_format if which == "fwd" else self.bwd_format
@@ -78,6 +84,32 @@ def _C():
     from .. import _ext
 
     return _ext.require()
+
+
+# fp8 weight gradients: "auto" (slice policy below), "0" (bf16 weight gradients), or a slice count
+_FP8_WGRAD = os.environ.get("APEX_FP8_WGRAD", "auto")
+
+
+def _f8_wgrad_splits(R, P, Q, cus=256):
+    """Split-K slices for the fp8 weight gradient dW [P, Q] over R tokens. With t 256x256 output
+    tiles and s slices the kernel runs ceil(t s / CUs) workgroup rounds of R / s tokens each, so
+    pick the s in {1, 2, 4, 8, 16} minimising ceil(t s / CUs) / s (ties: fewer slices, less fp32
+    slab traffic), each slice a whole number of 128-token K-tiles and >= 1024 tokens long.
+    Measured at BERT-Large's 98304 tokens (tools/wgrad_f8_bench.py, profiles/r5_wgrad_f8.jsonl):
+    QKV (48 tiles) 381 us at 16 slices vs 402 / 414 at 4 / 8; out-projection (16) 130 at 16 vs 202
+    at 8; FFN (64) 442 / 431 at 4 vs 465-532 at 8 / 16 — the model's picks."""
+    if _FP8_WGRAD not in ("auto", "", "0"):
+        s = int(_FP8_WGRAD)
+        return s if R % (128 * s) == 0 else 0
+    tiles = -(-P // 256) * -(-Q // 256)
+    best, best_cost = 1, None
+    for s in (1, 2, 4, 8, 16):
+        if R % (128 * s) or (s > 1 and R // s < 1024):
+            break
+        cost = -(-tiles * s // cus) / s
+        if best_cost is None or cost < best_cost - 1e-12:
+            best, best_cost = s, cost
+    return best
 
 
 class Fp8State:
@@ -111,6 +143,7 @@ class Fp8State:
         self._pre: dict = {}
         self._pre_bytes = 0
         self.prequant_hits = 0
+        self._last = None  # (data_ptr, shape, codes, scale_inv) of the last fp8 GEMM's activation operand
         self._grow(128)
 
     # ------------------------------------------------------------------ slots
@@ -316,6 +349,7 @@ class Fp8State:
             return None
         pre = self._take(a, self._fwd) if self._pre else None
         a8, ia = pre if pre is not None else self.quantize(a, (self.key_of(w), "x"), self._fwd)
+        self._last = (a.data_ptr(), tuple(a.shape), a8, ia)
         w8, iw = self.weight(w)
         kw = {}
         if q8 is not None:
@@ -335,12 +369,41 @@ class Fp8State:
             return None
         pre = self._take(dy, self._bwd) if self._pre else None
         d8, id_ = pre if pre is not None else self.quantize(dy, (self.key_of(w), "dy"), self._bwd)
+        self._last = (dy.data_ptr(), tuple(dy.shape), d8, id_)
         wt8, iw = self.weight_t(w)
         kw = {}
         if q8 is not None:  # (dGELU / MUL epilogues: the hidden gradient's codes for the W1 dgrad)
             kw = dict(q8_out=q8[0], q8_scale=q8[1], q8_amax=q8[2], q8_fmt=q8[3])
             self._q8_last = q8[0]
         return _C().gemm_f8(d8, wt8, id_, iw, self._bwd, epi, None, aux, bias_grad_dtype, dy.dtype, **kw)
+
+    # ------------------------------------------------------------------ weight gradients
+    def operand_codes(self, a):
+        """(codes, scale_inv) of ``a`` if the last ``forward_gemm`` / ``backward_gemm`` consumed it
+        in fp8, else None. The fused blocks keep them for the weight gradient (``wgrad``): the
+        layer input's codes from the forward, the output gradient's from the input-gradient GEMM
+        — no second quantisation of either tensor. scale_inv is a view of the slot, which only
+        ``step()`` rewrites, i.e. after every backward of the step."""
+        e, self._last = self._last, None
+        if e is None or e[0] != a.data_ptr() or e[1] != tuple(a.shape) or not self.wgrad_enabled():
+            return None
+        return e[2], e[3]
+
+    def wgrad_enabled(self):
+        return self.recipe.fp8_wgrad and _FP8_WGRAD != "0" and self._fwd == E4M3
+
+    def wgrad(self, d, x, out_dtype, out=None):
+        """dW [P, Q] = dy^T x from the codes ``d`` (dy [R, P], backward format) and ``x`` (x [R, Q],
+        e4m3) on the fp8 transposed-read kernel (csrc/gemm.hip gemm_tt_f8) -> out_dtype (written
+        into ``out`` when given), or None when the recipe or the shape rules it out."""
+        if not self.wgrad_enabled() or d is None or x is None:
+            return None
+        (d8, sd), (x8, sx) = d, x
+        s = _f8_wgrad_splits(d8.shape[0], d8.shape[1], x8.shape[1])
+        C = _C()
+        if not s or not C.gemm_tt_f8_supported(d8, x8, s):
+            return None
+        return C.gemm_tt_f8(d8, x8, sd, sx, self._bwd, self._fwd, s, out_dtype, out=out)
 
     # ------------------------------------------------------------------ step
     def step(self):
@@ -349,6 +412,7 @@ class Fp8State:
         all-reduce); no host synchronisation."""
         self.gen += 1
         self.steps += 1
+        self._last = None
         self._wcache.clear()
         self._pre.clear()
         self._pre_bytes = 0

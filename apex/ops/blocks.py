@@ -143,6 +143,8 @@ class _AttnSublayer(torch.autograd.Function):
         x2 = _2d(x)
         f8 = G.fp8_state()
         qkv = G.linear(x2, wqkv, bqkv, f8=f8)
+        # fp8: the GEMMs' activation codes are kept for the weight gradients (apex.fp8 operand_codes)
+        x8 = f8.operand_codes(x2) if f8 is not None else None
         q, k, v = qkv.view(B, S, 3, heads, d).unbind(2)
         sa, oa = _seed(x.device) if p_attn > 0 else (0, 0)
         # fp8: the flash forward also writes the e4m3 codes of its output, the attention-out GEMM's
@@ -156,6 +158,7 @@ class _AttnSublayer(torch.autograd.Function):
         if f8 is not None:
             _q8_file(f8, o2, None if q8o is None else (q8o[0].view(B * S, E),) + tuple(q8o[1:]), okey, f8._fwd)
         t = G.linear(o2, wo, f8=f8)
+        ctx.f8codes = (x8, f8.operand_codes(o2) if f8 is not None else None)
         sh, oh = _seed(x.device) if p_hidden > 0 else (0, 0)
         mem, store_s = _ln_plan(C, gamma, E, any(ctx.needs_input_grad))
         ykey = (f8.key_of(gamma), "y") if f8 is not None else None
@@ -190,7 +193,9 @@ class _AttnSublayer(torch.autograd.Function):
         if q8 is not None:
             f8.register(dt, q8[0], q8[4], q8[3])
         dctx = G.dgrad(dt, wo, f8=f8).view(B, S, heads, d)
-        dwo = _wgrad(dt, o.view(B * S, E), param=pwo)
+        x8, o8 = ctx.f8codes
+        dwo = _wgrad(dt, o.view(B * S, E), param=pwo,
+                     f8=(f8, f8.operand_codes(dt) if f8 is not None else None, o8))
         q, k, v = qkv.view(B, S, 3, heads, d).unbind(2)
         dqkv = torch.empty_like(qkv)
         dq, dk, dv = dqkv.view(B, S, 3, heads, d).unbind(2)
@@ -211,7 +216,7 @@ class _AttnSublayer(torch.autograd.Function):
             f8.register(dqkv, q8d[0], q8d[4], q8d[3])
         dbqkv = C.partial_colsum(dsum, bdt, _gt(pbqkv)) if has_bqkv else None
         dx = G.dgrad_resid(dqkv, wqkv, dres, f8=f8)  # residual grad accumulated in the GEMM epilogue
-        dwqkv = _wgrad(dqkv, x2, param=pqkv)
+        dwqkv = _wgrad(dqkv, x2, param=pqkv, f8=(f8, f8.operand_codes(dqkv) if f8 is not None else None, x8))
         return (dx.view(B, S, E), dwqkv, dbqkv, dwo, dbo if has_bo else None, dgamma, dbeta,
                 None, None, None, None, None, None)
 
@@ -230,6 +235,7 @@ class _FFNSublayer(torch.autograd.Function):
             q8 = _q8(f8, gkey, f8._fwd, x2, shape=(x2.shape[0], w1.shape[0])) if f8 is not None else None
             g, h = G.linear_gelu_d(x2, w1, b1, f8=f8, q8=q8) if _STORE_DERIV else \
                 G.linear_gelu(x2, w1, b1, f8=f8, q8=q8)
+            x8 = f8.operand_codes(x2) if f8 is not None else None
             if f8 is not None:
                 _q8_file(f8, g, q8 if f8.q8_written(q8) else None, gkey, f8._fwd)
             hb = None
@@ -237,7 +243,9 @@ class _FFNSublayer(torch.autograd.Function):
             h = torch.mm(x2, w1.t())
             g = C.bias_act_fwd(h, b1, act)
             hb = b1
+            x8 = None
         t = G.linear(g, w2, f8=f8)
+        ctx.f8codes = (x8, f8.operand_codes(g) if f8 is not None else None)
         seed, off = _seed(x.device) if p > 0 else (0, 0)
         mem, store_s = _ln_plan(C, gamma, x2.shape[1], any(ctx.needs_input_grad))
         ykey = (f8.key_of(gamma), "y") if f8 is not None else None
@@ -279,15 +287,18 @@ class _FFNSublayer(torch.autograd.Function):
                 dh, db1 = G.dgrad_mul(dt, w2, h, b1dt, f8=f8, bias_grad_out=tb1, q8=q8h)
             else:
                 dh, db1 = G.dgrad_dgelu(dt, w2, h, b1dt, f8=f8, bias_grad_out=tb1, q8=q8h)  # (dt W2) * gelu'(h) from h
+            dt8 = f8.operand_codes(dt) if f8 is not None else None
             if q8h is not None and f8.q8_written(q8h):
                 f8.register(dh, q8h[0], q8h[4], q8h[3])
             if tb1 is not None and db1 is not None and db1.data_ptr() != tb1.data_ptr():
                 db1 = tb1.copy_(db1)  # a path that could not write the slot: keep the handed-out view valid
         else:
             dh, db1 = C.bias_act_bwd(G.dgrad(dt, w2, f8=f8), h, hb, act)
-        dw2 = _wgrad(dt, g, param=pw2)
+            dt8 = f8.operand_codes(dt) if f8 is not None else None
+        x8, g8 = ctx.f8codes
+        dw2 = _wgrad(dt, g, param=pw2, f8=(f8, dt8, g8))
         dx = G.dgrad_resid(dh, w1, dres, f8=f8)  # residual grad accumulated in the GEMM epilogue
-        dw1 = _wgrad(dh, x2, param=pw1)
+        dw1 = _wgrad(dh, x2, param=pw1, f8=(f8, f8.operand_codes(dh) if f8 is not None else None, x8))
         return (dx.view_as(dy), dw1, db1 if b1dt is not None else None, dw2, db2 if has_b2 else None, dgamma,
                 dbeta, None, None, None)
 
@@ -306,7 +317,9 @@ class _MLP(torch.autograd.Function):
             g, gd = G.linear_gelu_d(x2, w1, b1, act, f8=f8)  # gelu(h) and gelu'(h)
         else:
             g, gd = G.linear_gelu(x2, w1, b1, act, f8=f8)  # gelu(h) and h
+        x8 = f8.operand_codes(x2) if f8 is not None else None
         t = G.linear(g, w2, f8=f8)
+        ctx.f8codes = (x8, f8.operand_codes(g) if f8 is not None else None)
         ctx.save_for_backward(x2, w1, gd, g, w2)
         ctx.params = (w1, b1, w2)
         ctx.act = act
@@ -323,11 +336,14 @@ class _MLP(torch.autograd.Function):
             dh, db1 = G.dgrad_mul(dt2, w2, gd, ctx.b1dt, f8=ctx.f8, bias_grad_out=tb1)
         else:
             dh, db1 = G.dgrad_dgelu(dt2, w2, gd, ctx.b1dt, act=ctx.act, f8=ctx.f8, bias_grad_out=tb1)
+        f8 = ctx.f8
+        dt8 = f8.operand_codes(dt2) if f8 is not None else None
         if tb1 is not None and db1 is not None and db1.data_ptr() != tb1.data_ptr():
             db1 = tb1.copy_(db1)
-        dw2 = _wgrad(dt2, g, param=pw2)
-        dx = G.dgrad(dh, w1, f8=ctx.f8).view(*dt.shape[:-1], w1.shape[1])
-        dw1 = _wgrad(dh, x2, param=pw1)
+        x8, g8 = ctx.f8codes
+        dw2 = _wgrad(dt2, g, param=pw2, f8=(f8, dt8, g8))
+        dx = G.dgrad(dh, w1, f8=f8).view(*dt.shape[:-1], w1.shape[1])
+        dw1 = _wgrad(dh, x2, param=pw1, f8=(f8, f8.operand_codes(dh) if f8 is not None else None, x8))
         return dx, dw1, db1, dw2, None
 
 

@@ -189,12 +189,13 @@ def main_grad_placeholder(param):
     return torch._efficientzerotensor(param.shape, dtype=param.dtype, device=param.device)
 
 
-def _wgrad(dy2, x2, out=None, param=None):
+def _wgrad(dy2, x2, out=None, param=None, f8=None):
     """Weight gradient dy2^T @ x2 in dy2's dtype (split-K batched GEMM when it pays), written into
     ``out`` when given (a gradient-bucket slot), or into ``param``'s bucket slot
     (apex.parallel.grad_target). When ``param`` carries an fp32 ``main_grad`` (DDP
     fp32_main_grad mode) the gradient is accumulated there instead and a placeholder is returned
-    for autograd (main_grad_placeholder: the DDP hook drops it)."""
+    for autograd (main_grad_placeholder: the DDP hook drops it). ``f8`` = (Fp8State, dy2 codes,
+    x2 codes) (apex.fp8 ``operand_codes``): the product runs on those fp8 codes instead."""
     if param is not None:
         mg = getattr(param, "main_grad", None)
         if mg is not None:
@@ -202,6 +203,10 @@ def _wgrad(dy2, x2, out=None, param=None):
             return main_grad_placeholder(param)
         if out is None:
             out = _gt(param)
+    if f8 is not None and f8[0] is not None and (out is None or out.is_contiguous()):
+        r = f8[0].wgrad(f8[1], f8[2], dy2.dtype, out=out)
+        if r is not None:
+            return r
     M, N = dy2.shape
     K = x2.shape[1]
     s = _wgrad_splits(M, N, K) if dy2.dtype in (torch.bfloat16, torch.float16) else 1

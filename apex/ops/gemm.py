@@ -55,6 +55,8 @@ import torch
 from .. import _ext
 
 _MODE = os.environ.get("APEX_GEMM", "auto")
+# plain / bias-only products in auto mode: "lib" (hipBLASLt) or "own" (the persistent MFMA kernel)
+_PLAIN = os.environ.get("APEX_GEMM_PLAIN", "lib")
 
 
 def _C():
@@ -71,7 +73,7 @@ def mode() -> str:
 
 def use_mfma(a, w, fused=True) -> bool:
     """MFMA kernel for this call? ``fused``: the call carries an epilogue the library lacks."""
-    if _MODE == "blas" or not a.is_cuda or (_MODE == "auto" and not fused):
+    if _MODE == "blas" or not a.is_cuda or (_MODE == "auto" and not fused and _PLAIN != "own"):
         return False
     return _C().gemm_supported(a, w)
 
@@ -176,7 +178,7 @@ def dgrad(dy, w, wT=None, f8=None):
         r = f8.backward_gemm(a, w, _C().EPI_NONE)
         if r is not None:
             return r[0].view(*dy.shape[:-1], w.shape[1])
-    if _MODE == "mfma" and a.is_cuda:
+    if (_MODE == "mfma" or (_MODE == "auto" and _PLAIN == "own")) and a.is_cuda:
         wT = transpose(w) if wT is None else wT
         if use_mfma(a, wT, fused=False):
             C = _C()

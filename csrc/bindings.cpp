@@ -1360,6 +1360,44 @@ Tensor k_gemm_tt(Tensor a, Tensor b, int64_t splits, at::ScalarType out_dtype, c
   return k_splitk_reduce(slabs, out_dtype, out_opt);
 }
 
+// fp8 weight gradient: out[P, Q] = alpha_a alpha_b a^T b over uint8 codes a [R, P] (format fmt_a),
+// b [R, Q] (fmt_b) — the codes the forward / backward GEMMs already consumed — split into `splits`
+// slices of fp32 partials, combined (and rounded to out_dtype) by splitk_reduce
+bool k_gemm_tt_f8_supported(Tensor a, Tensor b, int64_t splits) {
+  if (!a.is_cuda() || a.dim() != 2 || b.dim() != 2 || a.scalar_type() != at::kByte || b.scalar_type() != at::kByte)
+    return false;
+  if (!a.is_contiguous() || !b.is_contiguous() || a.size(0) != b.size(0)) return false;
+  auto al = [](const Tensor& t) { return reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0; };
+  return al(a) && al(b) && splits >= 1 &&
+         apex::gemm_tt_f8_supported((int)a.size(1), (int)b.size(1), (int)a.size(0), (int)splits, a.size(1), b.size(1));
+}
+
+Tensor k_gemm_tt_f8(Tensor a, Tensor b, Tensor alpha_a, Tensor alpha_b, int64_t fmt_a, int64_t fmt_b, int64_t splits,
+                    at::ScalarType out_dtype, const c10::optional<Tensor>& out_opt) {
+  TORCH_CHECK(k_gemm_tt_f8_supported(a, b, splits), "gemm_tt_f8: unsupported operands");
+  TORCH_CHECK(alpha_a.is_cuda() && alpha_a.scalar_type() == at::kFloat && alpha_a.numel() >= 1 && alpha_b.is_cuda() &&
+                  alpha_b.scalar_type() == at::kFloat && alpha_b.numel() >= 1,
+              "gemm_tt_f8: alpha_a / alpha_b must be fp32 device scalars");
+  const int64_t R = a.size(0), P = a.size(1), Q = b.size(1);
+  apex::GemmArgs g{};
+  g.A = a.data_ptr();
+  g.B = b.data_ptr();
+  g.M = (int)P;
+  g.N = (int)Q;
+  g.K = (int)(R / splits);
+  g.lda = P;
+  g.ldb = Q;
+  g.ldc = Q;
+  g.splits = (int)splits;
+  g.alpha_a = alpha_a.data_ptr<float>();
+  g.alpha_b = alpha_b.data_ptr<float>();
+  Tensor slabs = at::empty({splits, P, Q}, a.options().dtype(at::kFloat));
+  g.part = slabs.data_ptr<float>();
+  g.epi = apex::EPI_F32;
+  check(apex::gemm_tt_f8(g, (int)fmt_a, (int)fmt_b, cur_stream()), "gemm_tt_f8");
+  return k_splitk_reduce(slabs, out_dtype, out_opt);
+}
+
 // out[P, Q] += a^T b in fp32 (a [R, P], b [R, Q] 16-bit, out fp32 contiguous): the weight gradient
 // accumulated straight into an fp32 main_grad by the transposed-read MFMA kernel's
 // read-modify-write epilogue — one launch, no slab, no 16-bit rounding of the micro-batch dW
@@ -1515,6 +1553,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_tt", &k_gemm_tt, py::arg("a"), py::arg("b"), py::arg("splits"), py::arg("out_dtype"),
         py::arg("out") = py::none());
   m.def("gemm_tt_acc", &k_gemm_tt_acc);
+  m.def("gemm_tt_f8_supported", &k_gemm_tt_f8_supported);
+  m.def("gemm_tt_f8", &k_gemm_tt_f8, py::arg("a"), py::arg("b"), py::arg("alpha_a"), py::arg("alpha_b"),
+        py::arg("fmt_a"), py::arg("fmt_b"), py::arg("splits"), py::arg("out_dtype"), py::arg("out") = py::none());
   m.attr("EPI_NONE") = (int)apex::EPI_NONE;
   m.attr("EPI_BIAS") = (int)apex::EPI_BIAS;
   m.attr("EPI_BIAS_GELU") = (int)apex::EPI_BIAS_GELU;

@@ -182,7 +182,12 @@ __device__ __forceinline__ void bar() {
 //  TR = true (operand stored [K][rows], rows contiguous — the weight-gradient GEMM, where the
 //    contraction runs over tokens): piece = 2 K-rows x 512 B; image [64 K][256 rows], chunk c of
 //    K-row r at c ^ ftr(r); fragments are gathered with ds_read_b64_tr_b16 (hardware transpose).
+//    fp8 (the fp8 weight gradient): K-tile = 128 K-rows of 256 B, piece = 4 K-rows, chunk c of
+//    K-row r at c ^ ftr8(r); fragments from ds_read_b64_tr_b8.
 __device__ __forceinline__ int ftr(int r) { return 2 * (r & 3) + 8 * ((r >> 3) & 1); }
+// A tr_b8 read's 32-lane half covers K-rows r0 + q and r0 + 16 + q (q = 0..7, r0 % 8 == 0), 8 bytes
+// each of one 16-byte chunk: (r & 7) | bit 4 of r puts those 16 rows on 16 distinct slots (64 banks)
+__device__ __forceinline__ int ftr8(int r) { return (r & 7) | (((r >> 4) & 1) << 3); }
 
 template <typename T, bool TR>
 __device__ __forceinline__ void stage_pieces(const T* __restrict__ g, int64_t ld, int row0, int rows, int k0,
@@ -191,8 +196,9 @@ __device__ __forceinline__ void stage_pieces(const T* __restrict__ g, int64_t ld
   for (int j = p0; j < p0 + 2; ++j) {
     const int piece = wid * 4 + j;
     if constexpr (TR) {
-      const int r = piece * 2 + (lane >> 5);
-      const int chunk = (lane & 31) ^ ftr(r);
+      constexpr int LPR = 16 * (int)sizeof(T);  // lanes (16-byte chunks) per K-row: 32 (16-bit), 16 (fp8)
+      const int r = piece * (64 / LPR) + lane / LPR;
+      const int chunk = (lane % LPR) ^ (sizeof(T) == 1 ? ftr8(r) : ftr(r));
       // partial tiles (rows % 256, e.g. GPT-2's 1600 / 4800): chunks past the last row read the
       // last full chunk instead (rows % 8 == 0) — they only feed output rows / columns the
       // bounds-checked epilogue does not store, and the last K-row never reads past the tensor
@@ -213,12 +219,26 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ s16x4 lds_tr16(const char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
 }
+typedef int i32x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ i32x2v lds_tr8(const char* p) {
+  return __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) i32x2v*)(p));
+}
 
 // MFMA fragment for tile rows rb .. rb+15, K step s (32 wide): lane holds rows rb + lr,
-// K = 32s + 8 lk .. +7.
-template <bool TR>
+// K = 32s + 8 lk .. +7. ES = operand element bytes (1: fp8, where the 16 bytes are K = 64s + 16lk ..
+// +15, the chunk 4s + lk the NT image's lds_frag reads — see mfma_f8).
+template <bool TR, int ES = 2>
 __device__ __forceinline__ s16x8 frag(const char* tile, int rb, int s, int lr, int lk) {
-  if constexpr (TR) {
+  if constexpr (TR && ES == 1) {
+    // two 8(K) x 16(rows) byte blocks (ds_read_b64_tr_b8): lane 2q+p of a 16-lane group addresses
+    // K-row 64s + 16lk + 8h + q, rows rb + 8p .. +7; it receives row rb + lr, K-rows 8h .. 8h+7
+    const int q = lr >> 1, pp = lr & 1;
+    const int cl = rb >> 4;
+    const int r0 = s * 64 + 16 * lk + q, r1 = r0 + 8;
+    const i32x2v lo = lds_tr8(tile + r0 * 256 + ((cl ^ ftr8(r0)) << 4) + pp * 8);
+    const i32x2v hi = lds_tr8(tile + r1 * 256 + ((cl ^ ftr8(r1)) << 4) + pp * 8);
+    return __builtin_bit_cast(s16x8, i32x4{lo[0], lo[1], hi[0], hi[1]});
+  } else if constexpr (TR) {
     // two 4(K) x 16(rows) transposed blocks: lane 4q+p of a 16-lane group addresses K-row
     // 32s + 8lk + 4h + q, rows rb + 4p .. +3; it receives row rb + lr, K 4h .. 4h+3
     const int q = lr >> 2, pp = lr & 3;
@@ -269,7 +289,7 @@ __device__ __forceinline__ void mainloop_bk64(const T* __restrict__ A, const T* 
                                               int wc, int lane, f32x4 (&acc)[4][8]) {
   // one K-tile = 128 bytes of every row: 64 bf16/f16 elements or 128 fp8 ones
   constexpr bool F8 = FA >= 0;
-  static_assert(!F8 || (!TR && sizeof(T) == 1), "fp8: NT operands only");
+  static_assert(!F8 || sizeof(T) == 1, "fp8: uint8 codes");
   constexpr int BKE = 128 / (int)sizeof(T);
   const int nt = K / BKE;
   const int lr = lane & 15, lk = lane >> 4;
@@ -298,10 +318,10 @@ __device__ __forceinline__ void mainloop_bk64(const T* __restrict__ A, const T* 
     // ---------------- p1: A mh=0, B nh=0; stage A(t+1) pieces 0,1 ----------------
 #pragma unroll
     for (int j = 0; j < 2; ++j)
-      if constexpr (!(DBG & 128)) for (int s = 0; s < 2; ++s) fb0[j][s] = frag<TR>(tb, wc * 64 + j * 16, s, lr, lk);
+      if constexpr (!(DBG & 128)) for (int s = 0; s < 2; ++s) fb0[j][s] = frag<TR, sizeof(T)>(tb, wc * 64 + j * 16, s, lr, lk);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      if constexpr (!(DBG & 128)) for (int s = 0; s < 2; ++s) fa[i][s] = frag<TR>(ta, wr * 128 + i * 16, s, lr, lk);
+      if constexpr (!(DBG & 128)) for (int s = 0; s < 2; ++s) fa[i][s] = frag<TR, sizeof(T)>(ta, wr * 128 + i * 16, s, lr, lk);
     if (ld_a && !(DBG & 32)) stage_pieces<T, TR>(A, lda, m0, M, (t + 1) * BKE, oth, wid, lane, 0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if constexpr (!(DBG & 64)) bar();
@@ -324,7 +344,7 @@ __device__ __forceinline__ void mainloop_bk64(const T* __restrict__ A, const T* 
     // ---------------- p2: B nh=1; stage A(t+1) pieces 2,3 ----------------
 #pragma unroll
     for (int j = 0; j < 2; ++j)
-      if constexpr (!(DBG & 128)) for (int s = 0; s < 2; ++s) fb1[j][s] = frag<TR>(tb, wc * 64 + 32 + j * 16, s, lr, lk);
+      if constexpr (!(DBG & 128)) for (int s = 0; s < 2; ++s) fb1[j][s] = frag<TR, sizeof(T)>(tb, wc * 64 + 32 + j * 16, s, lr, lk);
     if (ld_a && !(DBG & 32)) stage_pieces<T, TR>(A, lda, m0, M, (t + 1) * BKE, oth, wid, lane, 2);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if constexpr (!(DBG & 64)) bar();
@@ -347,7 +367,7 @@ __device__ __forceinline__ void mainloop_bk64(const T* __restrict__ A, const T* 
     // ---------------- p3: A mh=1; stage B(t+2) pieces 0,1 into this buffer ----------------
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      if constexpr (!(DBG & 128)) for (int s = 0; s < 2; ++s) fa[i][s] = frag<TR>(ta, wr * 128 + 64 + i * 16, s, lr, lk);
+      if constexpr (!(DBG & 128)) for (int s = 0; s < 2; ++s) fa[i][s] = frag<TR, sizeof(T)>(ta, wr * 128 + 64 + i * 16, s, lr, lk);
     if (ld_b && !(DBG & 32)) stage_pieces<T, TR>(B, ldb, n0, N, (t + 2) * BKE, cur + G_TILE_BYTES, wid, lane, 0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if constexpr (!(DBG & 64)) bar();
@@ -408,19 +428,19 @@ __device__ __forceinline__ void mainloop_bk64(const T* __restrict__ A, const T* 
 // 1.49 -> 1.53 PF/s, BERT M = 98304 shapes 1-5 % faster (FFN2 dgrad + residual 642 -> 618 us);
 // transposed-read weight gradients 2-8 % (two ds_read_b64_tr_b16 per fragment: the read sections
 // are longer there, so evening them out pays more).
-template <bool TR>
+template <bool TR, int ES = 2>
 __device__ __forceinline__ void read_fa(s16x8 (&fa)[4][2], const char* ta, int rb, int lr, int lk) {
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int s = 0; s < 2; ++s) fa[i][s] = frag<TR>(ta, rb + i * 16, s, lr, lk);
+    for (int s = 0; s < 2; ++s) fa[i][s] = frag<TR, ES>(ta, rb + i * 16, s, lr, lk);
 }
-template <bool TR>
+template <bool TR, int ES = 2>
 __device__ __forceinline__ void read_fb(s16x8 (&fb)[2][2], const char* tb, int cb, int lr, int lk) {
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
-    for (int s = 0; s < 2; ++s) fb[j][s] = frag<TR>(tb, cb + j * 16, s, lr, lk);
+    for (int s = 0; s < 2; ++s) fb[j][s] = frag<TR, ES>(tb, cb + j * 16, s, lr, lk);
 }
 template <typename T, int FA, int FB, int MH, int NH>
 __device__ __forceinline__ void quad_mma(f32x4 (&acc)[4][8], const s16x8 (&fa)[4][2], const s16x8 (&fb)[2][2]) {
@@ -460,21 +480,21 @@ __device__ __forceinline__ void bal_tile(int t, int nt, const T* __restrict__ A,
   const bool ld_a = t + 1 < nt, ld_b = t + 2 < nt;
   constexpr bool RD = !(DBG & 128), GL = !(DBG & 32), BR = !(DBG & 64);
   // p1: A rows mh=0; stage A(t+1) pieces 0,1
-  if constexpr (RD) read_fa<TR>(fa, ta, wr * 128, lr, lk);
+  if constexpr (RD) read_fa<TR, sizeof(T)>(fa, ta, wr * 128, lr, lk);
   if (GL && ld_a) stage_pieces<T, TR>(A, lda, m0, M, (t + 1) * BKE, oth, wid, lane, 0);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   if constexpr (BR) bar();
   quad_mma<T, FA, FB, 0, PAR>(acc, fa, fb[PAR]);
   if constexpr (BR) bar();
   // p2: B half OP; stage A(t+1) pieces 2,3
-  if constexpr (RD) read_fb<TR>(fb[OP], tb, wc * 64 + OP * 32, lr, lk);
+  if constexpr (RD) read_fb<TR, sizeof(T)>(fb[OP], tb, wc * 64 + OP * 32, lr, lk);
   if (GL && ld_a) stage_pieces<T, TR>(A, lda, m0, M, (t + 1) * BKE, oth, wid, lane, 2);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   if constexpr (BR) bar();
   quad_mma<T, FA, FB, 0, OP>(acc, fa, fb[OP]);
   if constexpr (BR) bar();
   // p3: A rows mh=1; stage B(t+2) pieces 0,1 into this buffer; retire B(t+1) for p4
-  if constexpr (RD) read_fa<TR>(fa, ta, wr * 128 + 64, lr, lk);
+  if constexpr (RD) read_fa<TR, sizeof(T)>(fa, ta, wr * 128 + 64, lr, lk);
   if (ld_b) {
     if constexpr (GL) stage_pieces<T, TR>(B, ldb, n0, N, (t + 2) * BKE, cur + G_TILE_BYTES, wid, lane, 0);
     asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
@@ -488,7 +508,7 @@ __device__ __forceinline__ void bal_tile(int t, int nt, const T* __restrict__ A,
   // p4: next tile's first B half (OP) from the other buffer; stage B(t+2) pieces 2,3; retire A(t+1).
   // (Unconditional: after the last tile it reads stale LDS that nothing uses — a conditional load
   // would keep the old fragment live across the phase and cost registers.)
-  if constexpr (RD) read_fb<TR>(fb[OP], oth + G_TILE_BYTES, wc * 64 + OP * 32, lr, lk);
+  if constexpr (RD) read_fb<TR, sizeof(T)>(fb[OP], oth + G_TILE_BYTES, wc * 64 + OP * 32, lr, lk);
   if (ld_b) {
     if constexpr (GL) stage_pieces<T, TR>(B, ldb, n0, N, (t + 2) * BKE, cur + G_TILE_BYTES, wid, lane, 2);
     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
@@ -522,7 +542,7 @@ __device__ __forceinline__ void mainloop_bal(const T* __restrict__ A, const T* _
   if (wr == 1) bar();  // stagger group 1 by one barrier
   s16x8 fa[4][2], fb[2][2][2];
   const int lr = lane & 15, lk = lane >> 4;
-  if constexpr (!(DBG & 128)) read_fb<TR>(fb[0], smem + G_TILE_BYTES, wc * 64, lr, lk);  // tile 0's first B half
+  if constexpr (!(DBG & 128)) read_fb<TR, sizeof(T)>(fb[0], smem + G_TILE_BYTES, wc * 64, lr, lk);  // tile 0's first B half
   int t = 0;
   for (; t + 1 < nt; t += 2) {
     bal_tile<T, TR, FA, FB, DBG, 0>(t, nt, A, B, M, N, lda, ldb, m0, n0, smem, wid, wr, wc, lane, acc, fa, fb);
@@ -983,14 +1003,17 @@ __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(const TI* __restrict
   if constexpr (DBG & 2048) tr1 = __builtin_amdgcn_s_memrealtime();
   if constexpr (EPI == EPI_F32) {
     // fp32 slab (split-K partials): each lane stores its 4 consecutive columns per fragment
+    // (fp8 operands: dequantised here, alpha = the two per-tensor inverse scales)
     float* out = part + (int64_t)blockIdx.y * M * ldc;
+    float sc = 1.f;
+    if constexpr (FA >= 0) sc = alpha_a[0] * alpha_b[0];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int n = n0 + wc * 64 + j * 16 + 4 * lk;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const int m = m0 + wr * 128 + i * 16 + lr;
-        if (m < M && n < N) *reinterpret_cast<f32x4*>(out + (int64_t)m * ldc + n) = acc[j][i];
+        if (m < M && n < N) *reinterpret_cast<f32x4*>(out + (int64_t)m * ldc + n) = acc[j][i] * sc;
       }
     }
     return;
@@ -2319,6 +2342,40 @@ int gemm_tt(const GemmArgs& g, int dt, hipStream_t s) {
   } else {
     return -1;
   }
+  return (int)hipGetLastError();
+}
+
+bool gemm_tt_f8_supported(int P, int Q, int R, int splits, int64_t lda, int64_t ldb) {
+  // fp8 codes: 16-byte chunks of 16 columns (partial 256-tiles clamp to the last full chunk)
+  return P > 0 && Q > 0 && splits > 0 && P % 16 == 0 && Q % 16 == 0 && R % (splits * 128) == 0 && lda % 16 == 0 &&
+         ldb % 16 == 0;
+}
+
+// fp8 weight gradient: fp32 slabs [splits, P, Q] of alpha_a alpha_b sum_r A[r, p] B[r, q] over the
+// uint8 codes A (format fmt_a: the output gradient, e5m2 in the hybrid recipe) and B (fmt_b: the
+// layer input, e4m3); the transposed-read main loop with ds_read_b64_tr_b8 fragments
+template <int FA, int FB>
+void launch_gemm_tt_f8(const GemmArgs& g, hipStream_t s) {
+  const int tiles = ((g.M + GB_M - 1) / GB_M) * ((g.N + GB_N - 1) / GB_N);
+  if (g.M % GB_M != 0 || g.N % GB_N != 0)
+    hipLaunchKernelGGL((gemm_nt_kernel<bf16, EPI_F32, true, true, uint8_t, FA, FB>), dim3(tiles, g.splits),
+                       dim3(G_THREADS), 0, s, (const uint8_t*)g.A, (const uint8_t*)g.B, (bf16*)nullptr, g.M, g.N, g.K,
+                       g.lda, g.ldb, g.ldc, (const bf16*)nullptr, (const bf16*)nullptr, (int64_t)0, (bf16*)nullptr,
+                       g.part, 0, g.alpha_a, g.alpha_b);
+  else
+    hipLaunchKernelGGL((gemm_nt_kernel<bf16, EPI_F32, true, false, uint8_t, FA, FB>), dim3(tiles, g.splits),
+                       dim3(G_THREADS), 0, s, (const uint8_t*)g.A, (const uint8_t*)g.B, (bf16*)nullptr, g.M, g.N, g.K,
+                       g.lda, g.ldb, g.ldc, (const bf16*)nullptr, (const bf16*)nullptr, (int64_t)0, (bf16*)nullptr,
+                       g.part, 0, g.alpha_a, g.alpha_b);
+}
+
+int gemm_tt_f8(const GemmArgs& g, int fmt_a, int fmt_b, hipStream_t s) {
+  if (!gemm_tt_f8_supported(g.M, g.N, g.K * g.splits, g.splits, g.lda, g.ldb) || !g.alpha_a || !g.alpha_b ||
+      !g.part)
+    return -2;
+  if (fmt_a == 1 && fmt_b == 0) launch_gemm_tt_f8<1, 0>(g, s);
+  else if (fmt_a == 0 && fmt_b == 0) launch_gemm_tt_f8<0, 0>(g, s);
+  else return -1;
   return (int)hipGetLastError();
 }
 

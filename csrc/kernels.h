@@ -285,6 +285,8 @@ int gemm_set_dbg(int v);  // diagnostics: 2 = skip the epilogue
 // weight-gradient form: C[P, Q] = A^T B with A [R, P], B [R, Q] row-major (contraction over rows)
 bool gemm_tt_supported(int P, int Q, int R, int splits, int64_t lda, int64_t ldb);
 int gemm_tt(const GemmArgs& g, int dt, hipStream_t s);
+bool gemm_tt_f8_supported(int P, int Q, int R, int splits, int64_t lda, int64_t ldb);
+int gemm_tt_f8(const GemmArgs& g, int fmt_a, int fmt_b, hipStream_t s);
 int gemm_bias_grad(const float* part, int parts, int N, void* out, int odt, hipStream_t s);
 int transpose_2d(const void* in, void* out, int R, int C, int dt, hipStream_t s);
 

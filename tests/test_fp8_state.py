@@ -179,3 +179,42 @@ def test_amax_reduction_detects_slot_mismatch():
     for p in ps:
         p.join(timeout=30)
     assert all(r[1] == "ok" for r in res), res
+
+
+def test_wgrad_split_policy():
+    """fp8 weight-gradient slices: fewest workgroup rounds per token (ceil(tiles x slices / 256) / slices), each slice a
+    whole number of 128-token K-tiles and at least 1024 tokens (BERT-Large at 98304 tokens)."""
+    sp = fp8._f8_wgrad_splits
+    assert sp(98304, 4096, 1024) == 4  # 64 tiles
+    assert sp(98304, 1024, 4096) == 4
+    assert sp(98304, 3072, 1024) == 16  # 48 tiles: 3 full rounds beat 1.5 (8) and 0.75 (4)
+    assert sp(98304, 1024, 1024) == 16  # 16 tiles
+    assert sp(2048, 1024, 1024) == 2  # slices stay >= 1024 tokens
+    assert sp(384, 256, 256) == 1
+
+
+def test_operand_codes_match_the_consumed_tensor():
+    """operand_codes hands back the last fp8 GEMM's codes only for the tensor that GEMM consumed
+    (same storage and shape), once; a mismatch or a second call gets None."""
+    st = fp8.Fp8State(device="cpu")
+    a = torch.zeros(4, 8)
+    codes, inv = torch.zeros(4, 8, dtype=torch.uint8), torch.ones(1)
+    st._last = (a.data_ptr(), tuple(a.shape), codes, inv)
+    assert st.operand_codes(torch.zeros(4, 8)) is None  # another tensor
+    st._last = (a.data_ptr(), tuple(a.shape), codes, inv)
+    assert st.operand_codes(a.view(8, 4)) is None  # same storage, other shape
+    st._last = (a.data_ptr(), tuple(a.shape), codes, inv)
+    got = st.operand_codes(a)
+    assert got[0] is codes and got[1] is inv
+    assert st.operand_codes(a) is None  # taken
+    st._last = (a.data_ptr(), tuple(a.shape), codes, inv)
+    st.step()
+    assert st.operand_codes(a) is None  # a step boundary drops it
+
+
+def test_wgrad_declines_without_recipe_or_codes():
+    st = fp8.Fp8State(fp8.Fp8Recipe(fp8_wgrad=False), device="cpu")
+    c = (torch.zeros(256, 256, dtype=torch.uint8), torch.ones(1))
+    assert st.wgrad(c, c, torch.bfloat16) is None
+    st2 = fp8.Fp8State(device="cpu")
+    assert st2.wgrad(None, c, torch.bfloat16) is None

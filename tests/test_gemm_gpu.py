@@ -288,3 +288,59 @@ def test_mlp_block_matches_composition(act):
     _close(y, yr, 2e-2)
     for got, r in zip((x, w1, b1, w2), ref):
         _close(got.grad, r.grad, 3e-2)
+
+
+def _f8_codes(x, dt):
+    s = (torch.finfo(dt).max / x.abs().max().float()).reshape(1)
+    return (x.float() * s).to(dt).view(torch.uint8), (1.0 / s).float()
+
+
+@pytest.mark.parametrize("R,P,Q,splits", [(128, 256, 256, 1), (1024, 256, 512, 2), (2048, 512, 768, 4),
+                                          (8192, 1024, 1024, 8), (384, 256, 256, 3),
+                                          # partial 256-tiles: clamped staging, bounds-checked slab stores
+                                          (1024, 1600, 480, 2), (256, 16, 272, 1), (512, 4800, 1600, 2)])
+@pytest.mark.parametrize("fmt_a", [1, 0])
+def test_gemm_tt_f8_weight_grad(R, P, Q, splits, fmt_a):
+    """fp8 dW = alpha dY8^T X8 through the ds_read_b64_tr_b8 transposed-read main loop: against the
+    fp32 product of the dequantised codes (the kernel's exact inputs), asymmetric random data."""
+    C = _C()
+    torch.manual_seed(R + P + Q + fmt_a)
+    dta = torch.float8_e5m2 if fmt_a == 1 else torch.float8_e4m3fn
+    dy = torch.randn(R, P, device=DEV) * torch.linspace(0.5, 2.0, P, device=DEV)
+    x = torch.randn(R, Q, device=DEV) + torch.linspace(-1.0, 1.0, R, device=DEV)[:, None]
+    a8, sa = _f8_codes(dy, dta)
+    b8, sb = _f8_codes(x, torch.float8_e4m3fn)
+    assert C.gemm_tt_f8_supported(a8, b8, splits)
+    ref = (a8.view(dta).float() * sa).t() @ (b8.view(torch.float8_e4m3fn).float() * sb)
+    out32 = C.gemm_tt_f8(a8, b8, sa, sb, fmt_a, 0, splits, torch.float32)
+    assert out32.shape == (P, Q)
+    _close(out32, ref, 1e-4)
+    out = C.gemm_tt_f8(a8, b8, sa, sb, fmt_a, 0, splits, torch.bfloat16)
+    assert out.dtype == torch.bfloat16
+    _close(out, ref, 1e-2)
+
+
+def test_gemm_tt_f8_identity_rows():
+    """A = one-hot K-rows (dY8[r, p] = 1 iff p == r % P): dW[p, :] is the sum of X8's rows r = p mod P,
+    which pins the transposed-read byte gather (a wrong K-row / column pairing shows up as a
+    permutation, which a symmetric check could miss)."""
+    C = _C()
+    R, P, Q = 512, 256, 272
+    a = torch.zeros(R, P, device=DEV)
+    a[torch.arange(R), torch.arange(R) % P] = 1.0
+    x = torch.arange(R * Q, device=DEV, dtype=torch.float32).view(R, Q) % 13 - 6
+    a8 = a.to(torch.float8_e4m3fn).view(torch.uint8)
+    b8 = x.to(torch.float8_e4m3fn).view(torch.uint8)
+    one = torch.ones(1, device=DEV)
+    out = C.gemm_tt_f8(a8, b8, one, one, 0, 0, 1, torch.float32)
+    ref = x.view(R // P, P, Q).sum(0)
+    assert torch.equal(out, ref)
+
+
+def test_gemm_tt_f8_supported_rejects():
+    C = _C()
+    a = torch.zeros(256, 256, device=DEV, dtype=torch.uint8)
+    assert C.gemm_tt_f8_supported(a, a, 2)
+    assert not C.gemm_tt_f8_supported(a, a, 3)  # 256 rows / 3 slices is not a multiple of 128
+    assert not C.gemm_tt_f8_supported(a[:, :248].contiguous(), a, 1)  # P % 16
+    assert not C.gemm_tt_f8_supported(a.bfloat16(), a.bfloat16(), 1)
