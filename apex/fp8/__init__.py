@@ -88,6 +88,8 @@ def _C():
 
 # fp8 weight gradients: "auto" (slice policy below), "0" (bf16 weight gradients), or a slice count
 _FP8_WGRAD = os.environ.get("APEX_FP8_WGRAD", "auto")
+# batched per-step weight quantisation (Fp8State._batch_weights); "0": one weight at a time
+_FP8_WBATCH = os.environ.get("APEX_FP8_WBATCH", "1")
 
 
 def _f8_wgrad_splits(R, P, Q, cus=256):
@@ -134,6 +136,9 @@ class Fp8State:
         self.slots: dict = {}
         self._fresh: set = set()
         self._wcache: dict = {}
+        # the previous step's weights (key -> (weakref, slot, W^T used)): the first weight request of
+        # a step quantises all of them in one batched pass (_batch_weights)
+        self._wprev: dict = {}
         self._fwd = self.recipe.fmt("fwd")
         self._bwd = self.recipe.fmt("bwd")
         # (data_ptr, numel) -> (weakref to the tensor, version, codes, slot, fmt): producer-made codes
@@ -193,6 +198,7 @@ class Fp8State:
                 # not a crash). Keep fp8 weights out of reference cycles to stay exact.
                 st._dying.append(s)
         st._wcache.pop(key, None)
+        st._wprev.pop(key, None)
 
     def slot(self, key, fmt) -> int:
         s = self.slots.get(key)
@@ -245,12 +251,46 @@ class Fp8State:
         e = self._wcache.get(k)
         if e is not None and e[0]() is w and e[1] == self.gen:
             return e
+        if self._wprev:
+            self._batch_weights()
+            e = self._wcache.get(k)
+            if e is not None and e[0]() is w and e[1] == self.gen:
+                return e
         s = self.slot((k, "w"), self._fwd)
         self._fresh.discard(s)
         w8 = self._current(w.detach().contiguous(), s, self._fwd)
         e = [weakref.ref(w), self.gen, s, w8, None]
         self._wcache[k] = e
         return e
+
+    def _batch_weights(self):
+        """Quantise every weight the previous step used (and that is still alive) in one batched pass
+        (csrc/fp8.hip fp8_quantize_weights: one amax and one quantise launch for all of them,
+        each tile read once for the codes of W and, where the previous step needed them, W^T)
+        instead of three launches per weight. Same current scaling and rounding as _current +
+        weight_t. APEX_FP8_WBATCH=0: per-weight launches (A/B)."""
+        prev, self._wprev = self._wprev, {}
+        if _FP8_WBATCH == "0":
+            return
+        groups: dict = {}
+        for k, (ref, slot, want_t) in prev.items():
+            w = ref()
+            if w is None or w.dim() != 2 or not w.is_cuda or not w.is_contiguous():
+                continue
+            if w.dtype not in (torch.bfloat16, torch.float16, torch.float32):
+                continue
+            if self.slots.get((k, "w")) != slot:
+                continue
+            groups.setdefault(w.dtype, []).append((k, w, slot, want_t))
+        C = _C()
+        smax = FMT_MAX[self._fwd] * self.smax_scale
+        for items in groups.values():
+            outs = C.fp8_quantize_weights([w.detach() for _, w, _, _ in items], [s for _, _, s, _ in items],
+                                          [t for _, _, _, t in items], self._fwd, self.scale, self.scale_inv,
+                                          self.amax, smax)
+            for i, (k, w, slot, want_t) in enumerate(items):
+                self._fresh.discard(slot)
+                self._wcache[k] = [weakref.ref(w), self.gen, slot, outs[2 * i], outs[2 * i + 1] if want_t else None]
 
     def weight(self, w):
         """W [N, K] -> (e4m3 codes [N, K], scale_inv), cached for this optimizer step."""
@@ -413,6 +453,7 @@ class Fp8State:
         self.gen += 1
         self.steps += 1
         self._last = None
+        self._wprev = {k: (e[0], e[2], e[4] is not None) for k, e in self._wcache.items() if e[0]() is not None}
         self._wcache.clear()
         self._pre.clear()
         self._pre_bytes = 0

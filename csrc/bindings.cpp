@@ -1302,6 +1302,51 @@ Tensor k_fp8_quantize_t(Tensor x, int64_t fmt, Tensor scale, const c10::optional
   return y;
 }
 
+// one step's weights through the batched current-scaling quantiser: per weight the e4m3 codes
+// of W and (want_t) of W^T, scale / scale_inv / amax written at its slot -> [y0, yt0, y1, yt1, ...]
+// (yt empty when not wanted)
+std::vector<Tensor> k_fp8_quantize_weights(const std::vector<Tensor>& ws, const std::vector<int64_t>& slots,
+                                           const std::vector<bool>& want_t, int64_t fmt, Tensor scale,
+                                           Tensor scale_inv, Tensor amax, double smax) {
+  const size_t n = ws.size();
+  TORCH_CHECK(slots.size() == n && want_t.size() == n, "fp8_quantize_weights: one slot / flag per weight");
+  TORCH_CHECK(scale.is_cuda() && scale.scalar_type() == at::kFloat && scale_inv.scalar_type() == at::kFloat &&
+                  amax.scalar_type() == at::kFloat && scale.is_contiguous() && scale_inv.is_contiguous() &&
+                  amax.is_contiguous(),
+              "fp8_quantize_weights: fp32 contiguous slot buffers");
+  std::vector<Tensor> out;
+  out.reserve(2 * n);
+  if (n == 0) return out;
+  Tensor host = at::empty({(int64_t)(n * sizeof(apex::WqDesc))}, at::TensorOptions().dtype(at::kByte).pinned_memory(true));
+  auto* d = reinterpret_cast<apex::WqDesc*>(host.data_ptr<uint8_t>());
+  int64_t ab = 0, qb = 0;
+  const int dt = dt_code(ws[0].scalar_type());
+  for (size_t i = 0; i < n; ++i) {
+    const Tensor& w = ws[i];
+    TORCH_CHECK(w.is_cuda() && w.dim() == 2 && w.is_contiguous() && dt_code(w.scalar_type()) == dt &&
+                    w.device() == scale.device(),
+                "fp8_quantize_weights: contiguous 2-D device weights of one dtype");
+    TORCH_CHECK(slots[i] >= 0 && slots[i] < scale.numel() && slots[i] < scale_inv.numel() && slots[i] < amax.numel(),
+                "fp8_quantize_weights: slot out of range");
+    const int64_t R = w.size(0), C = w.size(1);
+    TORCH_CHECK(R > 0 && C > 0 && R < (1 << 30) && C < (1 << 30), "fp8_quantize_weights: weight shape");
+    Tensor y = at::empty({R, C}, w.options().dtype(at::kByte));
+    Tensor yt = want_t[i] ? at::empty({C, R}, w.options().dtype(at::kByte)) : at::empty({0}, w.options().dtype(at::kByte));
+    d[i] = apex::WqDesc{w.data_ptr(), y.data_ptr<uint8_t>(), want_t[i] ? yt.data_ptr<uint8_t>() : nullptr, (int)R, (int)C,
+                        (int)slots[i], 0, ab, qb};
+    ab += (R * C + 65535) / 65536;
+    qb += ((R + 63) / 64) * ((C + 63) / 64);
+    out.push_back(y);
+    out.push_back(yt);
+  }
+  Tensor dev = host.to(scale.device(), /*non_blocking=*/true);
+  check(apex::fp8_quantize_weights(reinterpret_cast<const apex::WqDesc*>(dev.data_ptr<uint8_t>()), (int)n, ab, qb, dt,
+                                   (int)fmt, scale.data_ptr<float>(), scale_inv.data_ptr<float>(), amax.data_ptr<float>(),
+                                   (float)smax, cur_stream()),
+        "fp8_quantize_weights");
+  return out;
+}
+
 void k_fp8_amax(Tensor x, Tensor amax) {
   TORCH_CHECK(x.is_cuda() && x.is_contiguous(), "fp8_amax: contiguous device tensor");
   f8_check_scalar(amax, "amax");
@@ -1475,6 +1520,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("epi"), py::arg("bias") = py::none(), py::arg("aux") = py::none(),
         py::arg("bias_grad_dtype") = py::none(), py::arg("out_dtype") = at::kBFloat16, py::arg("q8_out") = py::none(),
         py::arg("q8_scale") = py::none(), py::arg("q8_amax") = py::none(), py::arg("q8_fmt") = 0);
+  m.def("fp8_quantize_weights", &k_fp8_quantize_weights, py::arg("weights"), py::arg("slots"), py::arg("want_t"),
+        py::arg("fmt"), py::arg("scale"), py::arg("scale_inv"), py::arg("amax"), py::arg("smax"));
   m.def("fp8_quantize", &k_fp8_quantize, py::arg("x"), py::arg("fmt"), py::arg("scale"), py::arg("amax") = py::none(),
         py::arg("cur_amax") = py::none(), py::arg("scale_inv") = py::none(), py::arg("smax") = 0.0);
   m.def("fp8_quantize_t", &k_fp8_quantize_t, py::arg("x"), py::arg("fmt"), py::arg("scale"),

@@ -147,6 +147,112 @@ __global__ void update_scales_kernel(float* __restrict__ hist, float* __restrict
   amax_cur[sl] = 0.f;
 }
 
+// ---- batched weight quantisation (one optimizer step's weights in three launches) ----------------
+// The fp8 GEMMs quantise every weight once per step with current scaling: exact amax, then the
+// e4m3 codes of W (forward) and of W^T (input-gradient GEMM). Per weight that was an amax, a
+// quantise and a transposing quantise launch (~300 launches of ~10 us for BERT-Large's 96 GEMM
+// weights, mostly launch-bound); here every weight of the step goes through one zeroing, one amax
+// and one quantise launch, the last reading each 64 x 64 tile once for both outputs.
+// Work lists: amax blocks walk 64 K-element spans, quantise blocks 64 x 64 tiles; block -> weight
+// by binary search over the descriptors' first-block prefix.
+__global__ void wq_zero_kernel(const WqDesc* __restrict__ d, int nd, float* __restrict__ amax) {
+  for (int i = threadIdx.x; i < nd; i += blockDim.x) amax[d[i].slot] = 0.f;
+}
+
+__device__ __forceinline__ int wq_find(const WqDesc* __restrict__ d, int nd, int64_t b, bool quant) {
+  int lo = 0, hi = nd - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if ((quant ? d[mid].qblock0 : d[mid].ablock0) <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+constexpr int kWqSpan = 65536;  // elements per amax block
+
+template <typename T>
+__global__ void __launch_bounds__(256) wq_amax_kernel(const WqDesc* __restrict__ d, int nd, float* __restrict__ amax) {
+  const WqDesc w = d[wq_find(d, nd, blockIdx.x, false)];
+  const int64_t n = (int64_t)w.R * w.C;
+  const int64_t e0 = (int64_t)(blockIdx.x - w.ablock0) * kWqSpan;
+  const int64_t e1 = e0 + kWqSpan < n ? e0 + kWqSpan : n;
+  const T* x = (const T*)w.w;
+  float mx = 0.f;
+  if ((n & 7) == 0) {
+    for (int64_t i = e0 + threadIdx.x * 8; i < e1; i += 256 * 8) {
+      float v[8];
+      load_f<T, 8>(x + i, v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) mx = fmaxf(mx, fabsf(v[k]));
+    }
+  } else {
+    for (int64_t i = e0 + threadIdx.x; i < e1; i += 256) mx = fmaxf(mx, fabsf(to_f(x[i])));
+  }
+  block_amax(mx, amax + w.slot);
+}
+
+template <typename T, int FMT>
+__global__ void __launch_bounds__(256) wq_quant_kernel(const WqDesc* __restrict__ d, int nd, float* __restrict__ scale,
+                                                       float* __restrict__ scale_inv, const float* __restrict__ amax,
+                                                       float smax) {
+  __shared__ float tile[64][65];
+  const WqDesc w = d[wq_find(d, nd, blockIdx.x, true)];
+  const int tb = blockIdx.x - w.qblock0;
+  const int tiles_c = (w.C + 63) / 64;
+  const int r0 = (tb / tiles_c) * 64, c0 = (tb % tiles_c) * 64;
+  const float a = amax[w.slot];
+  const float s = (a > 0.f && isfinite(a)) ? smax / a : 1.f;
+  if (tb == 0 && threadIdx.x == 0) {
+    scale[w.slot] = s;
+    scale_inv[w.slot] = 1.f / s;
+  }
+  const T* x = (const T*)w.w;
+  // load: thread -> (row rr, 8 consecutive columns); the row-major codes go out straight away
+  for (int idx = threadIdx.x; idx < 64 * 8; idx += 256) {
+    const int rr = idx / 8, cg = (idx % 8) * 8;
+    const int r = r0 + rr, c = c0 + cg;
+    float v[8];
+    if (r < w.R && c + 8 <= w.C && (w.C & 7) == 0) {
+      load_f<T, 8>(x + (int64_t)r * w.C + c, v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] *= s;
+      uint2 q;
+      q.x = pack4<FMT>(v[0], v[1], v[2], v[3]);
+      q.y = pack4<FMT>(v[4], v[5], v[6], v[7]);
+      *reinterpret_cast<uint2*>(w.y + (int64_t)r * w.C + c) = q;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        v[k] = (r < w.R && c + k < w.C) ? to_f(x[(int64_t)r * w.C + c + k]) * s : 0.f;
+        if (r < w.R && c + k < w.C) w.y[(int64_t)r * w.C + c + k] = (uint8_t)(pack4<FMT>(v[k], 0.f, 0.f, 0.f) & 0xff);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) tile[rr][cg + k] = v[k];
+  }
+  if (!w.yt) return;  // (block-uniform)
+  __syncthreads();
+  // transposed codes: thread -> (output row c, 8 consecutive r)
+  for (int idx = threadIdx.x; idx < 64 * 8; idx += 256) {
+    const int cc = idx / 8, rg = (idx % 8) * 8;
+    const int c = c0 + cc, r = r0 + rg;
+    if (c >= w.C) continue;
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = tile[rg + k][cc];
+    if (r + 8 <= w.R && (w.R & 7) == 0) {
+      uint2 q;
+      q.x = pack4<FMT>(v[0], v[1], v[2], v[3]);
+      q.y = pack4<FMT>(v[4], v[5], v[6], v[7]);
+      *reinterpret_cast<uint2*>(w.yt + (int64_t)c * w.R + r) = q;
+    } else {
+      for (int k = 0; k < 8 && r + k < w.R; ++k)
+        w.yt[(int64_t)c * w.R + r + k] = (uint8_t)(pack4<FMT>(v[k], 0.f, 0.f, 0.f) & 0xff);
+    }
+  }
+}
+
 inline int grid_for(int64_t n8) {
   int64_t g = (n8 + 255) / 256;
   return (int)(g < 1 ? 1 : g > 1024 ? 1024 : g);  // 4 blocks / CU, grid-stride beyond
@@ -193,6 +299,22 @@ int fp8_quantize_t(const void* x, uint8_t* y, int R, int C, int dt, int fmt, flo
 int fp8_amax(const void* x, int64_t n, int dt, float* amax, hipStream_t s) {
   if (n == 0) return 0;
   FP8_DT(dt, T, hipLaunchKernelGGL((amax_kernel<T>), dim3(grid_for((n + 7) / 8)), dim3(256), 0, s, (const T*)x, n, amax));
+  return (int)hipGetLastError();
+}
+
+int fp8_quantize_weights(const WqDesc* d, int nd, int64_t ablocks, int64_t qblocks, int dt, int fmt, float* scale,
+                         float* scale_inv, float* amax, float smax, hipStream_t s) {
+  if (nd == 0) return 0;
+  if (ablocks <= 0 || qblocks <= 0 || ablocks >= (1ll << 31) || qblocks >= (1ll << 31)) return -2;
+  hipLaunchKernelGGL(wq_zero_kernel, dim3(1), dim3(256), 0, s, d, nd, amax);
+  FP8_DT(dt, T, hipLaunchKernelGGL((wq_amax_kernel<T>), dim3((int)ablocks), dim3(256), 0, s, d, nd, amax));
+  if (fmt == 0) {
+    FP8_DT(dt, T, hipLaunchKernelGGL((wq_quant_kernel<T, 0>), dim3((int)qblocks), dim3(256), 0, s, d, nd, scale, scale_inv,
+                                     amax, smax));
+  } else {
+    FP8_DT(dt, T, hipLaunchKernelGGL((wq_quant_kernel<T, 1>), dim3((int)qblocks), dim3(256), 0, s, d, nd, scale, scale_inv,
+                                     amax, smax));
+  }
   return (int)hipGetLastError();
 }
 

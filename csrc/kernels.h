@@ -279,6 +279,20 @@ int fp8_quantize(const void* x, uint8_t* y, int64_t n, int dt, int fmt, float* s
 int fp8_quantize_t(const void* x, uint8_t* y, int R, int C, int dt, int fmt, float* scale, float* scale_inv,
                    float* amax, const float* cur, float smax, hipStream_t s);
 int fp8_amax(const void* x, int64_t n, int dt, float* amax, hipStream_t s);
+// one step's weights (batched current-scaling quantisation): W [R, C] -> codes y [R, C] and, when
+// yt != null, y^T [C, R]; slot = the weight's scale / scale_inv / amax index; ablock0 / qblock0 =
+// prefix of the amax (64 K-element spans) / quantise (64 x 64 tiles) block counts
+struct WqDesc {
+  const void* w;
+  uint8_t* y;
+  uint8_t* yt;
+  int R, C;
+  int slot;
+  int pad;
+  int64_t ablock0, qblock0;
+};
+int fp8_quantize_weights(const WqDesc* d, int nd, int64_t ablocks, int64_t qblocks, int dt, int fmt, float* scale,
+                         float* scale_inv, float* amax, float smax, hipStream_t s);
 int fp8_update_scales(float* hist, float* amax_cur, float* scale, float* scale_inv, const float* fmt_max,
                       int n_slots, int hist_len, int idx, float margin_scale, hipStream_t s);
 int gemm_set_dbg(int v);  // diagnostics: 2 = skip the epilogue

@@ -555,3 +555,60 @@ def test_gemm_f8_q8_side_output_backward_epilogues(epi_name, M, N):
     ref = C.fp8_quantize(out, 1, scale, amax_ref)
     assert torch.equal(codes, ref)
     assert float(amax) == float(amax_ref)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_batched_weight_quantizer_matches_per_weight(dt):
+    """fp8_quantize_weights (one step's weights in three launches) against the per-weight current
+    scaling path (fp8_amax + fp8_quantize + fp8_quantize_t): identical codes, scale, scale_inv and
+    amax at every slot; W^T only where asked; shapes with partial 64-tiles and odd widths."""
+    C = _C()
+    torch.manual_seed(11)
+    shapes = [(1024, 1024), (3072, 1024), (100, 72), (8, 1608), (4100, 40), (33, 7)]
+    ws = [(torch.randn(*s, device=DEV) * (0.01 + i)).to(dt) for i, s in enumerate(shapes)]
+    slots = [5, 0, 3, 9, 2, 7]
+    want_t = [True, True, False, True, True, True]
+    smax = 448.0 * 0.5
+    scale, sinv, amax = (torch.full((12,), -1.0, device=DEV) for _ in range(3))
+    outs = C.fp8_quantize_weights(ws, slots, want_t, 0, scale, sinv, amax, smax)
+    for i, w in enumerate(ws):
+        a = torch.zeros(1, device=DEV)
+        C.fp8_amax(w, a)
+        s1, i1 = torch.zeros(1, device=DEV), torch.zeros(1, device=DEV)
+        y = C.fp8_quantize(w, 0, s1, None, a, i1, smax)
+        sl = slots[i]
+        assert float(amax[sl]) == float(a), i
+        assert float(scale[sl]) == float(s1) and float(sinv[sl]) == float(i1), i
+        assert torch.equal(outs[2 * i], y), i
+        if want_t[i]:
+            s2 = torch.zeros(1, device=DEV)
+            yt = C.fp8_quantize_t(w, 0, s2, None, a, torch.zeros(1, device=DEV), smax)
+            assert torch.equal(outs[2 * i + 1], yt), i
+        else:
+            assert outs[2 * i + 1].numel() == 0
+    untouched = [j for j in range(12) if j not in slots]
+    assert (scale[untouched] == -1).all() and (amax[untouched] == -1).all()
+
+
+def test_fp8_step_batches_weight_quantization(fp8_off, monkeypatch):
+    """After a step(), the first weight request quantises every weight of the previous step in one
+    batched pass; the fp8 outputs equal the per-weight path's (APEX_FP8_WBATCH=0)."""
+    from apex.ops import fused
+
+    fp8 = fp8_off
+    torch.manual_seed(2)
+    x = torch.randn(256, 256, device=DEV).bfloat16()
+    w1 = (torch.randn(512, 256, device=DEV) * 0.05).bfloat16()
+    w2 = (torch.randn(256, 512, device=DEV) * 0.05).bfloat16()
+    outs = {}
+    for mode in ("1", "0"):
+        monkeypatch.setattr(fp8, "_FP8_WBATCH", mode)
+        fp8.disable()
+        with fp8.fp8_autocast():
+            fused.fused_dense(fused.fused_dense(x, w1), w2)
+            fp8.step()
+            st = fp8.state()
+            assert len(st._wprev) == 2
+            outs[mode] = fused.fused_dense(fused.fused_dense(x, w1), w2)
+            assert not st._wprev and len(st._wcache) == 2
+    assert torch.equal(outs["1"], outs["0"])

@@ -5,7 +5,8 @@ generation, first-iteration bucket layout) into its totals. This reads the per-d
 `*_kernel_trace.csv` instead and keeps only the dispatches inside the last k training steps,
 using the optimizer's final kernel (LAMB stage 2 by default) as the step boundary.
 
-  python tools/profstep.py <kernel_trace.csv> [k=3] [top=30] [boundary=lamb_stage2]
+  python tools/profstep.py <kernel_trace.csv> [k=3] [top=30] [boundary=lamb_stage2] [skip=0]
+(skip: leave out the last `skip` steps, e.g. to read the bf16 pass of a `bench.py --fp8` trace)
 Prints ms/step per kernel name (summed over dispatches), the step wall span and the GPU-busy
 fraction (sum of kernel time / span).
 """
@@ -19,6 +20,7 @@ def main():
     k = int(sys.argv[2]) if len(sys.argv) > 2 else 3
     top = int(sys.argv[3]) if len(sys.argv) > 3 else 30
     boundary = sys.argv[4] if len(sys.argv) > 4 else "lamb_stage2"
+    skip = int(sys.argv[5]) if len(sys.argv) > 5 else 0
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     ends = [i for i, r in enumerate(rows) if boundary in r["Kernel_Name"]]
@@ -30,6 +32,8 @@ def main():
             steps[-1] = i
         else:
             steps.append(i)
+    if skip:
+        steps = steps[:-skip]
     if len(steps) < k + 1:
         raise SystemExit(f"only {len(steps)} step boundaries found")
     lo, hi = steps[-k - 1] + 1, steps[-1] + 1
