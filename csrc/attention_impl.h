@@ -546,28 +546,29 @@ attn_fwd_kernel(AttnArgs a) {
     const int64_t ooff = b * a.o_bs + h * a.o_hs + (int64_t)qrow * a.o_ss;
     T* op = (T*)a.o + ooff;
     const float qs = a.q8o ? a.q8_scale[0] : 0.f;
+    // Q8 (0: none, 1: e4m3, 2: e5m2) hoisted out of the store loop: fp8 codes of the stored
+    // (rounded) values, the attention-out GEMM's operand, from the packed words (f8_codes4)
+    auto store_o = [&](auto Q8c) {
+      constexpr int Q8 = decltype(Q8c)::value;
 #pragma unroll
-    for (int db = 0; db < D / 32; ++db) {
+      for (int db = 0; db < D / 32; ++db) {
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        typedef T t4 __attribute__((ext_vector_type(4)));
-        t4 w;
+        for (int g = 0; g < 4; ++g) {
+          typedef T t4 __attribute__((ext_vector_type(4)));
+          t4 w;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) w[e] = (T)(o[db][4 * g + e] * inv);
-        *(t4*)(op + 32 * db + 8 * g + 4 * hl) = w;
-        if (a.q8o) {  // fp8 codes of the stored (rounded) values: the attention-out GEMM's operand
-          float r[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            r[e] = (float)w[e];
-            q8mx = fmaxf(q8mx, fabsf(r[e]));
+          for (int e = 0; e < 4; ++e) w[e] = (T)(o[db][4 * g + e] * inv);
+          *(t4*)(op + 32 * db + 8 * g + 4 * hl) = w;
+          if constexpr (Q8 != 0) {
+            const uint2 ww = __builtin_bit_cast(uint2, w);
+            *(uint32_t*)(a.q8o + ooff + 32 * db + 8 * g + 4 * hl) = f8_codes4<Q8 - 1, T>(ww.x, ww.y, qs, q8mx);
           }
-          *(uint32_t*)(a.q8o + ooff + 32 * db + 8 * g + 4 * hl) =
-              a.q8_fmt == 0 ? f8_pack4<0>(r[0] * qs, r[1] * qs, r[2] * qs, r[3] * qs)
-                            : f8_pack4<1>(r[0] * qs, r[1] * qs, r[2] * qs, r[3] * qs);
         }
       }
-    }
+    };
+    if (!a.q8o) store_o(std::integral_constant<int, 0>{});
+    else if (a.q8_fmt == 0) store_o(std::integral_constant<int, 1>{});
+    else store_o(std::integral_constant<int, 2>{});
     if (hl == 0 && a.lse)
       a.lse[(int64_t)bh * a.Sq + qrow] = ltot > 0.f ? (m * sl2 + log2f(ltot)) * kLn2 : INFINITY;
   }
@@ -954,15 +955,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
           for (int i = 0; i < 4; ++i) w[i] = (T)(acc[t][i] * a.scale);
           *(t4*)(dqp + (dt0 + t) * 16 + 4 * lg) = w;
           if (a.q8dq) {  // fp8 codes of dq as stored (the QKV input-gradient GEMM's operand)
-            float r[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              r[i] = (float)w[i];
-              q8mx = fmaxf(q8mx, fabsf(r[i]));
-            }
+            const uint2 ww = __builtin_bit_cast(uint2, w);
             *(uint32_t*)(a.q8dq + qoff + (dt0 + t) * 16 + 4 * lg) =
-                a.q8_fmt == 0 ? f8_pack4<0>(r[0] * q8s, r[1] * q8s, r[2] * q8s, r[3] * q8s)
-                              : f8_pack4<1>(r[0] * q8s, r[1] * q8s, r[2] * q8s, r[3] * q8s);
+                a.q8_fmt == 0 ? f8_codes4<0, T>(ww.x, ww.y, q8s, q8mx) : f8_codes4<1, T>(ww.x, ww.y, q8s, q8mx);
           }
           if constexpr (DSUM) {
 #pragma unroll
@@ -1049,15 +1044,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
         const V8 x = join4<V8>(lo, hi);
         *(V8*)(dst + (int64_t)key * ss + d0) = x;
         if (q8dst) {  // fp8 codes of the stored values (the same element offset in the code array)
-          typedef T t8 __attribute__((ext_vector_type(8)));
-          const t8 xv = __builtin_bit_cast(t8, x);
-          float r[8];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            r[e] = (float)xv[e];
-            q8mx = fmaxf(q8mx, fabsf(r[e]));
+          const uint4 ww = __builtin_bit_cast(uint4, x);
+          uint2 c;
+          if (a.q8_fmt == 0) {
+            c.x = f8_codes4<0, T>(ww.x, ww.y, q8s, q8mx);
+            c.y = f8_codes4<0, T>(ww.z, ww.w, q8s, q8mx);
+          } else {
+            c.x = f8_codes4<1, T>(ww.x, ww.y, q8s, q8mx);
+            c.y = f8_codes4<1, T>(ww.z, ww.w, q8s, q8mx);
           }
-          f8_store8(q8dst + (int64_t)key * ss + d0, r, q8s, a.q8_fmt);
+          *(uint2*)(q8dst + (int64_t)key * ss + d0) = c;
         }
       }
     }

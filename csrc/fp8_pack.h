@@ -15,11 +15,13 @@ constexpr float kF8E5M2Max = 57344.f;
 
 template <int FMT>
 __device__ __forceinline__ uint32_t f8_pack4(float a, float b, float c, float d) {
+  // saturate with v_med3_f32: one instruction per value, and no NaN-canonicalising v_max_f32 x, x
+  // that fminf / fmaxf insert before each clamp when the input's provenance is unknown
   const float m = FMT == 0 ? kF8E4M3Max : kF8E5M2Max;
-  a = fminf(fmaxf(a, -m), m);
-  b = fminf(fmaxf(b, -m), m);
-  c = fminf(fmaxf(c, -m), m);
-  d = fminf(fmaxf(d, -m), m);
+  a = __builtin_amdgcn_fmed3f(a, -m, m);
+  b = __builtin_amdgcn_fmed3f(b, -m, m);
+  c = __builtin_amdgcn_fmed3f(c, -m, m);
+  d = __builtin_amdgcn_fmed3f(d, -m, m);
   int w = 0;
   if constexpr (FMT == 0) {
     w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, w, false);
@@ -42,6 +44,60 @@ __device__ __forceinline__ void f8_store8(uint8_t* p, const float (&v)[8], float
     w.y = f8_pack4<1>(v[4] * s, v[5] * s, v[6] * s, v[7] * s);
   }
   *reinterpret_cast<uint2*>(p) = w;
+}
+
+// ---- producer-side codes of values a 16-bit store just wrote ---------------------------------------
+// The codes must be those of the STORED (rounded) values, so they are taken from the packed 16-bit
+// words themselves: bf16 -> f32 is a shift / mask (no second rounding convert), the running max|x|
+// is one v_max3_f32 with |.| modifiers per two values, the scale one packed multiply per two.
+typedef float f8_f2 __attribute__((ext_vector_type(2)));
+
+template <typename T> __device__ __forceinline__ f8_f2 f8_unpack2(uint32_t w);
+template <> __device__ __forceinline__ f8_f2 f8_unpack2<__bf16>(uint32_t w) {
+  return f8_f2{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
+}
+template <> __device__ __forceinline__ f8_f2 f8_unpack2<_Float16>(uint32_t w) {
+  typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+  const h2 h = __builtin_bit_cast(h2, w);
+  return f8_f2{(float)h[0], (float)h[1]};
+}
+
+__device__ __forceinline__ void f8_amax2(float& mx, f8_f2 v) {
+  asm("v_max3_f32 %0, |%1|, |%2|, %0" : "+v"(mx) : "v"(v[0]), "v"(v[1]));
+}
+
+// four codes of the 16-bit values in two packed words: sat(x * s); mx = max(mx, |x|)
+template <int FMT, typename T>
+__device__ __forceinline__ uint32_t f8_codes4(uint32_t w0, uint32_t w1, float s, float& mx) {
+  const f8_f2 ab = f8_unpack2<T>(w0), cd = f8_unpack2<T>(w1);
+  f8_amax2(mx, ab);
+  f8_amax2(mx, cd);
+  const f8_f2 p = ab * f8_f2{s, s}, q = cd * f8_f2{s, s};
+  return f8_pack4<FMT>(p[0], p[1], q[0], q[1]);
+}
+
+// 8 values stored as 16-bit T (one 16-byte store) plus their codes (one 8-byte store); fmt
+// wave-uniform
+template <typename T>
+__device__ __forceinline__ void f8_store_with_codes8(T* dst, uint8_t* cdst, const float (&v)[8], float s, int fmt,
+                                                     float& mx) {
+  static_assert(sizeof(T) == 2, "16-bit stores");
+  struct alignas(16) P8 {
+    T v[8];
+  } pk;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) pk.v[i] = (T)v[i];
+  *reinterpret_cast<P8*>(dst) = pk;
+  const uint4 w = __builtin_bit_cast(uint4, pk);
+  uint2 c;
+  if (fmt == 0) {
+    c.x = f8_codes4<0, T>(w.x, w.y, s, mx);
+    c.y = f8_codes4<0, T>(w.z, w.w, s, mx);
+  } else {
+    c.x = f8_codes4<1, T>(w.x, w.y, s, mx);
+    c.y = f8_codes4<1, T>(w.z, w.w, s, mx);
+  }
+  *reinterpret_cast<uint2*>(cdst) = c;
 }
 
 // non-negative floats order like their bit patterns: max via integer atomics

@@ -276,16 +276,19 @@ __global__ void __launch_bounds__(kEwBlock) bdaln_fwd_kernel(const T* __restrict
         o[k] = (v[j][k] - mu) * rs * gv[k] + bb[k];
         gz |= gv[k] == 0.f;
       }
-      store_f<T, 8>(y + row * cols + vi * 8, o);
       if (q8.y) {
-        // fp8 codes of the output as stored (rounded to T first): the next GEMM's operand without
-        // a standalone quantise pass re-reading y from HBM
+        // with the fp8 codes of the output as stored (rounded to T): the next GEMM's operand
+        // without a standalone quantise pass re-reading y from HBM
+        if constexpr (sizeof(T) == 2) {
+          f8_store_with_codes8<T>(y + row * cols + vi * 8, q8.y + row * cols + vi * 8, o, qs, q8.fmt, mx);
+        } else {
+          store_f<T, 8>(y + row * cols + vi * 8, o);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          o[k] = to_f(from_f<T>(o[k]));
-          mx = fmaxf(mx, fabsf(o[k]));
+          for (int k = 0; k < 8; ++k) mx = fmaxf(mx, fabsf(o[k]));
+          f8_store8(q8.y + row * cols + vi * 8, o, qs, q8.fmt);
         }
-        f8_store8(q8.y + row * cols + vi * 8, o, qs, q8.fmt);
+      } else {
+        store_f<T, 8>(y + row * cols + vi * 8, o);
       }
     }
   }
@@ -434,14 +437,15 @@ __device__ __forceinline__ void bdaln_bwd_body(const T* __restrict__ dy, const T
           if (DROP) ds[k] = keep[k] ? ds[k] * scale : 0.f;
           dbi[j][k] += ds[k];
         }
-        store_f<T, 8>(dx + e, ds);
-        if constexpr (Q8) {  // fp8 codes of dx as stored: the output-gradient GEMM's operand
+        if constexpr (Q8 && sizeof(T) == 2) {  // with the fp8 codes of dx as stored (the dgrad GEMM's operand)
+          f8_store_with_codes8<T>(dx + e, q8.y + e, ds, qs, q8.fmt, mx);
+        } else {
+          store_f<T, 8>(dx + e, ds);
+          if constexpr (Q8) {
 #pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            ds[k] = to_f(from_f<T>(ds[k]));
-            mx = fmaxf(mx, fabsf(ds[k]));
+            for (int k = 0; k < 8; ++k) mx = fmaxf(mx, fabsf(ds[k]));
+            f8_store8(q8.y + e, ds, qs, q8.fmt);
           }
-          f8_store8(q8.y + e, ds, qs, q8.fmt);
         }
       }
     }
