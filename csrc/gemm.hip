@@ -283,6 +283,10 @@ __device__ __forceinline__ s16x8 frag(const char* tile, int rb, int s, int lr, i
 // software-pipelined under 64-MFMA halves) makes hipcc shuffle ~220 accumulator copies
 // (v_accvgpr_read/write) per K-tile through the loop-carried phis, so it is not used. rocprof on the 32768x1024x4096 case: MFMA busy 65 %
 // of SIMD cycles at 1.98 GHz, zero LDS bank conflicts.
+template <typename T, bool TR, int FA, int FB, int DBG>
+__device__ __forceinline__ void mainloop_bk64_loop(const T* __restrict__ A, const T* __restrict__ B, int M, int N,
+                                                   int K, int64_t lda, int64_t ldb, int m0, int n0, char* smem,
+                                                   int wid, int wr, int wc, int lane, f32x4 (&acc)[4][8]);
 template <typename T, bool TR, int FA = -1, int FB = -1, int DBG = 0>
 __device__ __forceinline__ void mainloop_bk64(const T* __restrict__ A, const T* __restrict__ B, int M, int N, int K,
                                               int64_t lda, int64_t ldb, int m0, int n0, char* smem, int wid, int wr,
@@ -292,7 +296,6 @@ __device__ __forceinline__ void mainloop_bk64(const T* __restrict__ A, const T* 
   static_assert(!F8 || sizeof(T) == 1, "fp8: uint8 codes");
   constexpr int BKE = 128 / (int)sizeof(T);
   const int nt = K / BKE;
-  const int lr = lane & 15, lk = lane >> 4;
   // prologue: A(0), B(0) -> buf0, B(1) -> buf1; retire tile 0
   stage_pieces<T, TR>(A, lda, m0, M, 0, smem, wid, lane, 0);
   stage_pieces<T, TR>(A, lda, m0, M, 0, smem, wid, lane, 2);
@@ -307,7 +310,19 @@ __device__ __forceinline__ void mainloop_bk64(const T* __restrict__ A, const T* 
   }
   bar();
   if (wr == 1) bar();  // stagger group 1 by one barrier
+  mainloop_bk64_loop<T, TR, FA, FB, DBG>(A, B, M, N, K, lda, ldb, m0, n0, smem, wid, wr, wc, lane, acc);
+}
 
+// mainloop_bk64's K loop (tile 0 staged and retired, the wave groups staggered): also the fp8 body of
+// the persistent kernel
+template <typename T, bool TR, int FA, int FB, int DBG>
+__device__ __forceinline__ void mainloop_bk64_loop(const T* __restrict__ A, const T* __restrict__ B, int M, int N,
+                                                   int K, int64_t lda, int64_t ldb, int m0, int n0, char* smem,
+                                                   int wid, int wr, int wc, int lane, f32x4 (&acc)[4][8]) {
+  constexpr bool F8 = FA >= 0;
+  constexpr int BKE = 128 / (int)sizeof(T);
+  const int nt = K / BKE;
+  const int lr = lane & 15, lk = lane >> 4;
   s16x8 fa[4][2], fb0[2][2], fb1[2][2];
   for (int t = 0; t < nt; ++t) {
     char* cur = smem + (t & 1) * G_BUF_BYTES;
@@ -638,8 +653,12 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[NJ][8], char* reg, T
                                          int64_t ldc, const T* __restrict__ bias, const T* __restrict__ aux,
                                          int64_t ldaux, T* __restrict__ aux_out, float* __restrict__ part, int m0,
                                          int n0, int tm, int wr, int wc, int lane, float alpha = 1.f,
-                                         const Q8Out& q8 = Q8Out{}, const Hook& pre = Hook{}) {
-  static_assert(!HALVES || (Q8 == 0 && !STAGED && !EDGE), "halved staging: full tiles, no fp8 codes, accumulators in registers");
+                                         const Q8Out& q8 = Q8Out{}, const Hook& pre = Hook{},
+                                         float* q8_defer = nullptr) {
+  // HALVES + Q8: the codes of the multiply / dGELU epilogues are stashed and emitted per half, and the
+  // running max|C| goes to *q8_defer (the persistent kernel issues one amax atomic per workgroup at its
+  // end: an atomic here would sit between the next tile's LDS-DMA pieces and their counted wait)
+  static_assert(!HALVES || (!STAGED && !EDGE), "halved staging: full tiles, accumulators in registers");
   const int lr = lane & 15, lk = lane >> 4;
   // acc[j][i] holds rows wr*128 + i*16 + lr, cols wc*64 + j*16 + 4*lk .. +3 of the tile. The fp32
   // accumulators are rounded to T and transposed through the wave's own 16 KB LDS region
@@ -787,7 +806,7 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[NJ][8], char* reg, T
 #pragma unroll
             for (int it = 0; it < 8; ++it) rb[it] = asm_load16(rsx_s, voff(ldaux, 8 + it), soff(ldaux, 8 + it));
           } else {
-            asm_wait<8>(rb);
+            asm_wait<Q8 != 0 ? 16 : 8>(rb);  // (half 0's stores, and with Q8 its codes, are younger)
           }
         } else if (h == 0) {
 #pragma unroll
@@ -862,7 +881,7 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[NJ][8], char* reg, T
               // fp8 codes later, from LDS: the slot's chunk (read above, this lane's alone) takes the
               // stored value back — inline, the codes' live ranges spilled ~100 VGPRs in these variants
               if constexpr (Q8 != 0) {
-                const int row = slot * 8 + lrow;
+                const int row = (HALVES ? it : slot) * 8 + lrow;
                 *reinterpret_cast<u32x4*>(reg + row * 128 + (((lane & 7) ^ (row & 7)) << 4)) = out;
               }
             }
@@ -885,6 +904,23 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[NJ][8], char* reg, T
         // slot, hoisted by the scheduler) is what pushed these epilogues past 256 VGPRs
         __builtin_amdgcn_sched_barrier(0);
       }
+      if constexpr (HALVES && Q8 != 0 && COLSUM) {  // this half's stashed outputs -> fp8 codes
+        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+#pragma unroll 4
+        for (int it = 0; it < 8; ++it) {
+          const int row = it * 8 + lrow;
+          float r[8];
+          unpack(*reinterpret_cast<const u32x4*>(reg + row * 128 + (((lane & 7) ^ (row & 7)) << 4)), r);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            q8mx = fmaxf(q8mx, fabsf(r[e]));
+            r[e] *= q8s;
+          }
+          const u32x2 w = u32x2{f8_pack4<Q8 - 1>(r[0], r[1], r[2], r[3]), f8_pack4<Q8 - 1>(r[4], r[5], r[6], r[7])};
+          __builtin_amdgcn_raw_buffer_store_b64(w, rs_q, (uint32_t)(((8 * h + it) * 8 + lrow) * ldc + lcol), 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
     if constexpr (COLSUM) {
       // lanes l, l^8, l^16, ... share the column chunk: reduce over the wave's 8 row slots
@@ -903,7 +939,7 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[NJ][8], char* reg, T
         *reinterpret_cast<f32x4*>(pp + 4) = f32x4{csum[4], csum[5], csum[6], csum[7]};
       }
     }
-    if constexpr (Q8 != 0 && COLSUM) {  // the stashed outputs -> fp8 codes
+    if constexpr (Q8 != 0 && COLSUM && !HALVES) {  // the stashed outputs -> fp8 codes
       typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 #pragma unroll 4
       for (int slot = 0; slot < 16; ++slot) {
@@ -920,7 +956,9 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[NJ][8], char* reg, T
         __builtin_amdgcn_raw_buffer_store_b64(w, rs_q, qo, 0, 0);
       }
     }
-    if constexpr (Q8 != 0) {  // one amax atomic per wave, filtered by a plain read (amax only grows)
+    if constexpr (Q8 != 0 && HALVES) {
+      *q8_defer = fmaxf(*q8_defer, q8mx);
+    } else if constexpr (Q8 != 0) {  // one amax atomic per wave, filtered by a plain read (amax only grows)
       const float m = f8_wave_max(q8mx);
       if (lane == 0 && m > 0.f && m > *(volatile float*)q8.amax) f8_atomic_max_pos(q8.amax, m);
     }
@@ -1114,40 +1152,51 @@ __device__ __forceinline__ void tile_coords(int v, int tiles_m, int tiles_n, int
 // inside the epilogue, so they have retired). Must not exceed the true count (a larger vmcnt would
 // let A(0) / B(0) through unretired): C 16, + pre-activation or gelu' 16, + the bias-grad partial row
 // 2 (lanes 0..7).
-template <int EPI> constexpr int epi_stores() {
+template <int EPI, int Q8 = 0> constexpr int epi_stores() {
   constexpr bool GELU_FWD = EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_TANH || EPI == EPI_BIAS_GELU_D ||
                             EPI == EPI_BIAS_GELU_TANH_D;
   constexpr bool COLSUM = EPI == EPI_DGELU || EPI == EPI_DGELU_TANH || EPI == EPI_MUL;
-  return 16 + (GELU_FWD ? 16 : 0) + (COLSUM ? 2 : 0);
+  return 16 + (GELU_FWD ? 16 : 0) + (COLSUM ? 2 : 0) + (Q8 != 0 ? 16 : 0);  // (+ the fp8 codes, 8 B per slot)
 }
 
-template <typename T, int EPI, int DBG = 0>
-__global__ void __launch_bounds__(G_THREADS) gemm_persist_kernel(const T* __restrict__ A, const T* __restrict__ B,
+// fp8 (TI = uint8_t codes, formats FA / FB, dequantised by alpha_a[0] * alpha_b[0]; Q8: the output's
+// own fp8 codes too): the same tile walk with mainloop_bk64's body (the fp8 instantiations keep it:
+// the balanced loop's extra live fragment spills there) and 128-element K-tiles.
+template <typename T, int EPI, typename TI = T, int FA = -1, int FB = -1, int Q8 = 0, int DBG = 0>
+__global__ void __launch_bounds__(G_THREADS) gemm_persist_kernel(const TI* __restrict__ A, const TI* __restrict__ B,
                                                                  T* __restrict__ C, int M, int N, int K, int64_t lda,
                                                                  int64_t ldb, int64_t ldc, const T* __restrict__ bias,
                                                                  const T* __restrict__ aux, int64_t ldaux,
                                                                  T* __restrict__ aux_out, float* __restrict__ part,
-                                                                 uint64_t* __restrict__ trace) {
+                                                                 uint64_t* __restrict__ trace,
+                                                                 const float* __restrict__ alpha_a = nullptr,
+                                                                 const float* __restrict__ alpha_b = nullptr,
+                                                                 Q8Out q8 = Q8Out{}) {
   __shared__ __attribute__((aligned(16))) char smem[G_LDS_BYTES];
+  __shared__ float q8red[G_THREADS / 64];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wid >> 2, wc = wid & 3;
   const int tiles_m = M / GB_M, tiles_n = N / GB_N, nwg = tiles_m * tiles_n;
   const int G = gridDim.x;
-  constexpr int BKE = 64;
+  constexpr bool F8 = FA >= 0;
+  constexpr int BKE = 128 / (int)sizeof(TI);
   const int nt = K / BKE;
   int v = blockIdx.x;
   if (v >= nwg) return;  // (the host sizes the grid to at most the tile count)
+  float alpha = 1.f;
+  if constexpr (F8) alpha = alpha_a[0] * alpha_b[0];
+  float q8run = 0.f;  // this lane's max|C| over its tiles (Q8)
   int m0, n0, tm;
   tile_coords(v, tiles_m, tiles_n, m0, n0, tm);
   // first tile's prologue (mainloop_bal's): A(0), B(0) -> buffer 0, B(1) -> buffer 1
-  stage_pieces<T, false>(A, lda, m0, M, 0, smem, wid, lane, 0);
-  stage_pieces<T, false>(A, lda, m0, M, 0, smem, wid, lane, 2);
-  stage_pieces<T, false>(B, ldb, n0, N, 0, smem + G_TILE_BYTES, wid, lane, 0);
-  stage_pieces<T, false>(B, ldb, n0, N, 0, smem + G_TILE_BYTES, wid, lane, 2);
+  stage_pieces<TI, false>(A, lda, m0, M, 0, smem, wid, lane, 0);
+  stage_pieces<TI, false>(A, lda, m0, M, 0, smem, wid, lane, 2);
+  stage_pieces<TI, false>(B, ldb, n0, N, 0, smem + G_TILE_BYTES, wid, lane, 0);
+  stage_pieces<TI, false>(B, ldb, n0, N, 0, smem + G_TILE_BYTES, wid, lane, 2);
   if (nt > 1) {
-    stage_pieces<T, false>(B, ldb, n0, N, BKE, smem + G_BUF_BYTES + G_TILE_BYTES, wid, lane, 0);
-    stage_pieces<T, false>(B, ldb, n0, N, BKE, smem + G_BUF_BYTES + G_TILE_BYTES, wid, lane, 2);
+    stage_pieces<TI, false>(B, ldb, n0, N, BKE, smem + G_BUF_BYTES + G_TILE_BYTES, wid, lane, 0);
+    stage_pieces<TI, false>(B, ldb, n0, N, BKE, smem + G_BUF_BYTES + G_TILE_BYTES, wid, lane, 2);
     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1167,15 +1216,21 @@ __global__ void __launch_bounds__(G_THREADS) gemm_persist_kernel(const T* __rest
     // waits, in vmcnt order, for every epilogue store still in flight)
     int lane_k = lane;
     asm volatile("" : "+v"(lane_k));
-    const int lrk = lane_k & 15, lkk = lane_k >> 4;
-    s16x8 fa[4][2], fb[2][2][2];
-    read_fb<false>(fb[0], smem + G_TILE_BYTES, wc * 64, lrk, lkk);  // tile 0's first B half
-    int t = 0;
-    for (; t + 1 < nt; t += 2) {
-      bal_tile<T, false, -1, -1, 0, 0>(t, nt, A, B, M, N, lda, ldb, m0, n0, smem, wid, wr, wc, lane_k, acc, fa, fb);
-      bal_tile<T, false, -1, -1, 0, 1>(t + 1, nt, A, B, M, N, lda, ldb, m0, n0, smem, wid, wr, wc, lane_k, acc, fa, fb);
+    if constexpr (F8) {
+      mainloop_bk64_loop<TI, false, FA, FB, 0>(A, B, M, N, K, lda, ldb, m0, n0, smem, wid, wr, wc, lane_k, acc);
+    } else {
+      const int lrk = lane_k & 15, lkk = lane_k >> 4;
+      s16x8 fa[4][2], fb[2][2][2];
+      read_fb<false>(fb[0], smem + G_TILE_BYTES, wc * 64, lrk, lkk);  // tile 0's first B half
+      int t = 0;
+      for (; t + 1 < nt; t += 2) {
+        bal_tile<TI, false, -1, -1, 0, 0>(t, nt, A, B, M, N, lda, ldb, m0, n0, smem, wid, wr, wc, lane_k, acc, fa, fb);
+        bal_tile<TI, false, -1, -1, 0, 1>(t + 1, nt, A, B, M, N, lda, ldb, m0, n0, smem, wid, wr, wc, lane_k, acc, fa,
+                                          fb);
+      }
+      if (t < nt)
+        bal_tile<TI, false, -1, -1, 0, 0>(t, nt, A, B, M, N, lda, ldb, m0, n0, smem, wid, wr, wc, lane_k, acc, fa, fb);
     }
-    if (t < nt) bal_tile<T, false, -1, -1, 0, 0>(t, nt, A, B, M, N, lda, ldb, m0, n0, smem, wid, wr, wc, lane_k, acc, fa, fb);
     if (wr == 0) bar();  // re-align the groups
     bar();               // every wave is past its last ds_read of this tile
     if constexpr (DBG & 2048) tr1 = __builtin_amdgcn_s_memrealtime();
@@ -1194,15 +1249,15 @@ __global__ void __launch_bounds__(G_THREADS) gemm_persist_kernel(const T* __rest
     }
     // the next tile's A(0), B(0): issued by the epilogue after its own first loads (hook)
     auto next_k0 = [&]() {
-      stage_pieces<T, false>(A, lda, m1, M, 0, smem, wid, lane_e, 0);
-      stage_pieces<T, false>(A, lda, m1, M, 0, smem, wid, lane_e, 2);
-      stage_pieces<T, false>(B, ldb, n1, N, 0, smem + G_TILE_BYTES, wid, lane_e, 0);
-      stage_pieces<T, false>(B, ldb, n1, N, 0, smem + G_TILE_BYTES, wid, lane_e, 2);
+      stage_pieces<TI, false>(A, lda, m1, M, 0, smem, wid, lane_e, 0);
+      stage_pieces<TI, false>(A, lda, m1, M, 0, smem, wid, lane_e, 2);
+      stage_pieces<TI, false>(B, ldb, n1, N, 0, smem + G_TILE_BYTES, wid, lane_e, 0);
+      stage_pieces<TI, false>(B, ldb, n1, N, 0, smem + G_TILE_BYTES, wid, lane_e, 2);
     };
     __builtin_amdgcn_sched_barrier(0);
-    epilogue<T, EPI, false, 0, 4, false, 0, true>(acc, smem + G_BUF_BYTES + wid * 8192, C, M, N, ldc, bias, aux,
-                                                   ldaux, aux_out, part, m0, n0, tm, wr, wc, lane_e, 1.f, Q8Out{},
-                                                   next_k0);
+    epilogue<T, EPI, false, 0, 4, false, Q8, true>(acc, smem + G_BUF_BYTES + wid * 8192, C, M, N, ldc, bias, aux,
+                                                    ldaux, aux_out, part, m0, n0, tm, wr, wc, lane_e, alpha, q8,
+                                                    next_k0, &q8run);
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (DBG & 2048) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1222,17 +1277,28 @@ __global__ void __launch_bounds__(G_THREADS) gemm_persist_kernel(const T* __rest
     if (!more) break;
     bar();  // every wave is done with its epilogue region: buffer 1 is free
     if (nt > 1) {
-      stage_pieces<T, false>(B, ldb, n1, N, BKE, smem + G_BUF_BYTES + G_TILE_BYTES, wid, lane_e, 0);
-      stage_pieces<T, false>(B, ldb, n1, N, BKE, smem + G_BUF_BYTES + G_TILE_BYTES, wid, lane_e, 2);
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(epi_stores<EPI>() + 4) : "memory");
+      stage_pieces<TI, false>(B, ldb, n1, N, BKE, smem + G_BUF_BYTES + G_TILE_BYTES, wid, lane_e, 0);
+      stage_pieces<TI, false>(B, ldb, n1, N, BKE, smem + G_BUF_BYTES + G_TILE_BYTES, wid, lane_e, 2);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(epi_stores<EPI, Q8>() + 4) : "memory");
     } else {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(epi_stores<EPI>()) : "memory");
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(epi_stores<EPI, Q8>()) : "memory");
     }
     bar();  // A(0), B(0) of the next tile visible to every wave
     v = vn;
     m0 = m1;
     n0 = n1;
     tm = tm1;
+  }
+  if constexpr (Q8 != 0) {  // one amax atomic per workgroup, after its last tile
+    const float m = f8_wave_max(q8run);
+    if (lane == 0) q8red[wid] = m;
+    bar();
+    if (tid == 0) {
+      float mm = 0.f;
+#pragma unroll
+      for (int w = 0; w < G_THREADS / 64; ++w) mm = fmaxf(mm, q8red[w]);
+      if (mm > 0.f) f8_atomic_max_pos(q8.amax, mm);
+    }
   }
 }
 
@@ -2198,12 +2264,46 @@ void launch_gemm(const GemmArgs& g, hipStream_t s) {
                        (const T*)g.aux, g.ldaux, (T*)g.aux_out, g.part, stagger);
 }
 
+// fp8 launches on the persistent kernel: OFF by default (APEX_GEMM_PERSIST_F8=1 turns it on). Measured
+// at the BERT fp8 shapes, M = 98304 (tools/fp8_persist_bench.py, profiles/r5_fp8_persist_ab.jsonl, same
+// box, bit-identical outputs): SLOWER on every shape — FFN2 forward 487 vs 418 us, FFN1 dgrad +
+// residual 635 vs 438, FFN2 dgrad x gelu' + codes 948 vs 760, bias 433 vs 419. The fp8 main loop runs
+// at the 256-VGPR limit and spills 3-11 registers (the one-tile kernel 3-5); in the persistent kernel
+// those scratch reloads sit in the K loop behind the previous tile's epilogue stores (loads, stores and
+// scratch retire in vmcnt order), so every reload waits for the stores.
+inline bool host_persist_f8() {
+  static int on = -1;
+  if (on == -1) {
+    const char* e = getenv("APEX_GEMM_PERSIST_F8");
+    on = (e && e[0] == '1') ? 1 : 0;
+  }
+  return on == 1 && host_persist();
+}
+
 template <typename T, int EPI, int FA, int FB>
 void launch_gemm_f8(const GemmArgs& g, hipStream_t s) {
   const int tiles = ((g.M + GB_M - 1) / GB_M) * ((g.N + GB_N - 1) / GB_N);
   // fp8 codes of C for the next GEMM (the MLP's hidden activation forward, its gradient backward)
   constexpr bool Q8_OK = EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_TANH || EPI == EPI_BIAS_GELU_D ||
                          EPI == EPI_BIAS_GELU_TANH_D || EPI == EPI_MUL || EPI == EPI_DGELU || EPI == EPI_DGELU_TANH;
+  if (g.M % GB_M == 0 && g.N % GB_N == 0 && tiles > host_cus() && host_persist_f8()) {
+    const int grid = (host_cus() / 8) * 8;
+    auto go = [&](auto q_c) {
+      hipLaunchKernelGGL((gemm_persist_kernel<T, EPI, uint8_t, FA, FB, decltype(q_c)::value>), dim3(grid),
+                         dim3(G_THREADS), 0, s, (const uint8_t*)g.A, (const uint8_t*)g.B, (T*)g.C, g.M, g.N, g.K, g.lda,
+                         g.ldb, g.ldc, (const T*)g.bias, (const T*)g.aux, g.ldaux, (T*)g.aux_out, g.part,
+                         (uint64_t*)nullptr, g.alpha_a, g.alpha_b, g.q8);
+    };
+    if constexpr (Q8_OK) {
+      if (g.q8.y) {
+        if (g.q8.fmt == 0) go(std::integral_constant<int, 1>{});
+        else go(std::integral_constant<int, 2>{});
+        return;
+      }
+    }
+    go(std::integral_constant<int, 0>{});
+    return;
+  }
   if constexpr (Q8_OK) {
     if (g.q8.y) {
       auto go = [&](auto edge_c, auto q_c) {

@@ -140,9 +140,9 @@ def _tanh_gelu(h):
 
 
 @pytest.mark.parametrize("epi", ["bias", "resid", "gelu", "dgelu", "gelu_d", "gelu_tanh_d", "mul"])
-def test_gemm_f8_epilogues(epi):
+@pytest.mark.parametrize("M,N,K", [(320, 512, 768), (4608, 4096, 256)])  # (the second: 288 tiles, persistent)
+def test_gemm_f8_epilogues(epi, M, N, K):
     C = _C()
-    M, N, K = 320, 512, 768
     a8, b8, ia, ib, af, bf = _operands(M, N, K, 0, seed=3)
     acc = af @ bf.t()
     bias = (torch.randn(N, device=DEV) * 0.1).bfloat16()
@@ -501,7 +501,7 @@ def test_blocks_fp8_producer_codes_match_standalone_path(fp8_off, monkeypatch):
 
 
 @pytest.mark.parametrize("epi_name", ["EPI_BIAS_GELU_D", "EPI_BIAS_GELU"])
-@pytest.mark.parametrize("M,N", [(512, 1024), (300, 520)])
+@pytest.mark.parametrize("M,N", [(512, 1024), (300, 520), (4608, 4096)])
 @pytest.mark.parametrize("fmt", [0, 1])
 def test_gemm_f8_q8_side_output_matches_standalone_quantize(epi_name, M, N, fmt):
     """The fp8 GEMM's bias+GELU epilogue writing the fp8 codes of its output (full and edge tiles):
@@ -530,7 +530,7 @@ def test_gemm_f8_q8_side_output_matches_standalone_quantize(epi_name, M, N, fmt)
 
 
 @pytest.mark.parametrize("epi_name", ["EPI_MUL", "EPI_DGELU"])
-@pytest.mark.parametrize("M,N", [(512, 1024), (300, 520)])
+@pytest.mark.parametrize("M,N", [(512, 1024), (300, 520), (4608, 4096)])
 def test_gemm_f8_q8_side_output_backward_epilogues(epi_name, M, N):
     """The backward (input-operand) epilogues' e5m2 side output, written from the LDS-stashed
     outputs after the slot loop: codes bit-identical to the standalone quantiser, amax equal, the
