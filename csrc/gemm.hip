@@ -84,6 +84,15 @@ __device__ __forceinline__ f32x4 mfma_f8(const s16x8& a0, const s16x8& a1, const
   return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, FMT_A, FMT_B, 0, 0x7F7F7F7F, 0, 0x7F7F7F7F);
 }
 
+// the lane id computed afresh (volatile: never CSE'd with an earlier copy or hoisted out of a loop), so
+// no VGPR holding it — or an address derived from it — stays live across a K loop: the fp8 main loop
+// runs at the 256-VGPR limit, and in the persistent kernel one more live register spills inside it
+__device__ __forceinline__ int lane_id_fresh() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+
 __device__ __forceinline__ void glds16(const void* g, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
@@ -283,7 +292,7 @@ __device__ __forceinline__ s16x8 frag(const char* tile, int rb, int s, int lr, i
 // software-pipelined under 64-MFMA halves) makes hipcc shuffle ~220 accumulator copies
 // (v_accvgpr_read/write) per K-tile through the loop-carried phis, so it is not used. rocprof on the 32768x1024x4096 case: MFMA busy 65 %
 // of SIMD cycles at 1.98 GHz, zero LDS bank conflicts.
-template <typename T, bool TR, int FA, int FB, int DBG>
+template <typename T, bool TR, int FA, int FB, int DBG, bool FRESH = false>
 __device__ __forceinline__ void mainloop_bk64_loop(const T* __restrict__ A, const T* __restrict__ B, int M, int N,
                                                    int K, int64_t lda, int64_t ldb, int m0, int n0, char* smem,
                                                    int wid, int wr, int wc, int lane, f32x4 (&acc)[4][8]);
@@ -314,17 +323,20 @@ __device__ __forceinline__ void mainloop_bk64(const T* __restrict__ A, const T* 
 }
 
 // mainloop_bk64's K loop (tile 0 staged and retired, the wave groups staggered): also the fp8 body of
-// the persistent kernel
-template <typename T, bool TR, int FA, int FB, int DBG>
+// the persistent kernel, which sets FRESH: the LDS-DMA source addresses are recomputed from a fresh
+// lane id every K-tile instead of being kept in 16 VGPRs across the loop (there they spilled, and each
+// reload waited, in vmcnt order, for every load and store in flight)
+template <typename T, bool TR, int FA, int FB, int DBG, bool FRESH>
 __device__ __forceinline__ void mainloop_bk64_loop(const T* __restrict__ A, const T* __restrict__ B, int M, int N,
                                                    int K, int64_t lda, int64_t ldb, int m0, int n0, char* smem,
-                                                   int wid, int wr, int wc, int lane, f32x4 (&acc)[4][8]) {
+                                                   int wid, int wr, int wc, int lane_in, f32x4 (&acc)[4][8]) {
   constexpr bool F8 = FA >= 0;
   constexpr int BKE = 128 / (int)sizeof(T);
   const int nt = K / BKE;
-  const int lr = lane & 15, lk = lane >> 4;
+  const int lr = lane_in & 15, lk = lane_in >> 4;
   s16x8 fa[4][2], fb0[2][2], fb1[2][2];
   for (int t = 0; t < nt; ++t) {
+    const int lane = FRESH ? lane_id_fresh() : lane_in;
     char* cur = smem + (t & 1) * G_BUF_BYTES;
     char* oth = smem + ((t + 1) & 1) * G_BUF_BYTES;
     const char* ta = cur;
@@ -1186,7 +1198,9 @@ __global__ void __launch_bounds__(G_THREADS) gemm_persist_kernel(const TI* __res
   if (v >= nwg) return;  // (the host sizes the grid to at most the tile count)
   float alpha = 1.f;
   if constexpr (F8) alpha = alpha_a[0] * alpha_b[0];
-  float q8run = 0.f;  // this lane's max|C| over its tiles (Q8)
+  if constexpr (Q8 != 0) {  // per-wave running max|C| over the tiles, in LDS (no register across the K loop)
+    if (lane == 0) q8red[wid] = 0.f;
+  }
   int m0, n0, tm;
   tile_coords(v, tiles_m, tiles_n, m0, n0, tm);
   // first tile's prologue (mainloop_bal's): A(0), B(0) -> buffer 0, B(1) -> buffer 1
@@ -1214,10 +1228,9 @@ __global__ void __launch_bounds__(G_THREADS) gemm_persist_kernel(const TI* __res
     // the K loop's per-lane addresses from an opaque lane copy: recomputed per tile rather than kept
     // live through the epilogue (where they spilled, and a scratch reload at the next tile's start
     // waits, in vmcnt order, for every epilogue store still in flight)
-    int lane_k = lane;
-    asm volatile("" : "+v"(lane_k));
+    const int lane_k = lane_id_fresh();
     if constexpr (F8) {
-      mainloop_bk64_loop<TI, false, FA, FB, 0>(A, B, M, N, K, lda, ldb, m0, n0, smem, wid, wr, wc, lane_k, acc);
+      mainloop_bk64_loop<TI, false, FA, FB, 0, true>(A, B, M, N, K, lda, ldb, m0, n0, smem, wid, wr, wc, lane_k, acc);
     } else {
       const int lrk = lane_k & 15, lkk = lane_k >> 4;
       s16x8 fa[4][2], fb[2][2][2];
@@ -1239,8 +1252,7 @@ __global__ void __launch_bounds__(G_THREADS) gemm_persist_kernel(const TI* __res
     int m1 = 0, n1 = 0, tm1 = 0;
     // an opaque copy of the lane id: everything the epilogue and the next tile's staging derive from
     // it is computed here, not hoisted above the K loop (where it stayed live and spilled ~55 VGPRs)
-    int lane_e = lane;
-    asm volatile("" : "+v"(lane_e));
+    const int lane_e = lane_id_fresh();
     if (more) {
       tile_coords(vn, tiles_m, tiles_n, m1, n1, tm1);
     } else {  // the last tile re-loads its own first K-tile (unused): the epilogue's counted waits
@@ -1255,9 +1267,14 @@ __global__ void __launch_bounds__(G_THREADS) gemm_persist_kernel(const TI* __res
       stage_pieces<TI, false>(B, ldb, n1, N, 0, smem + G_TILE_BYTES, wid, lane_e, 2);
     };
     __builtin_amdgcn_sched_barrier(0);
+    float q8w = 0.f;
     epilogue<T, EPI, false, 0, 4, false, Q8, true>(acc, smem + G_BUF_BYTES + wid * 8192, C, M, N, ldc, bias, aux,
                                                     ldaux, aux_out, part, m0, n0, tm, wr, wc, lane_e, alpha, q8,
-                                                    next_k0, &q8run);
+                                                    next_k0, &q8w);
+    if constexpr (Q8 != 0) {
+      const float m = f8_wave_max(q8w);
+      if (lane_e == 0) q8red[wid] = fmaxf(q8red[wid], m);
+    }
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (DBG & 2048) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1290,10 +1307,8 @@ __global__ void __launch_bounds__(G_THREADS) gemm_persist_kernel(const TI* __res
     tm = tm1;
   }
   if constexpr (Q8 != 0) {  // one amax atomic per workgroup, after its last tile
-    const float m = f8_wave_max(q8run);
-    if (lane == 0) q8red[wid] = m;
     bar();
-    if (tid == 0) {
+    if (wid == 0 && lane_id_fresh() == 0) {
       float mm = 0.f;
 #pragma unroll
       for (int w = 0; w < G_THREADS / 64; ++w) mm = fmaxf(mm, q8red[w]);
@@ -2265,12 +2280,13 @@ void launch_gemm(const GemmArgs& g, hipStream_t s) {
 }
 
 // fp8 launches on the persistent kernel: OFF by default (APEX_GEMM_PERSIST_F8=1 turns it on). Measured
-// at the BERT fp8 shapes, M = 98304 (tools/fp8_persist_bench.py, profiles/r5_fp8_persist_ab.jsonl, same
-// box, bit-identical outputs): SLOWER on every shape — FFN2 forward 487 vs 418 us, FFN1 dgrad +
-// residual 635 vs 438, FFN2 dgrad x gelu' + codes 948 vs 760, bias 433 vs 419. The fp8 main loop runs
-// at the 256-VGPR limit and spills 3-11 registers (the one-tile kernel 3-5); in the persistent kernel
-// those scratch reloads sit in the K loop behind the previous tile's epilogue stores (loads, stores and
-// scratch retire in vmcnt order), so every reload waits for the stores.
+// at the BERT fp8 shapes, M = 98304 (tools/fp8_persist_bench.py, same box, bit-identical outputs):
+// first SLOWER on every shape (profiles/r5_fp8_persist_ab.jsonl: FFN2 forward 487 vs 418 us, FFN1
+// dgrad + residual 635 vs 438) — the fp8 main loop runs at the 256-VGPR limit, and in the persistent
+// kernel a spilled staging address was reloaded inside the K loop behind the previous tile's epilogue
+// stores (loads, stores and scratch retire in vmcnt order). With the staging addresses recomputed from
+// a fresh lane id per K-tile (FRESH, 0 scratch): still 2-5 % slower except the out-projection forward,
+// fp8 BERT step 156.2 vs 155.2 ms (profiles/r5_fp8_persist_ab_v2.jsonl).
 inline bool host_persist_f8() {
   static int on = -1;
   if (on == -1) {
