@@ -57,6 +57,15 @@ from .. import _ext
 _MODE = os.environ.get("APEX_GEMM", "auto")
 # plain / bias-only products in auto mode: "lib" (hipBLASLt) or "own" (the persistent MFMA kernel)
 _PLAIN = os.environ.get("APEX_GEMM_PLAIN", "lib")
+# ... except vocabulary-sized ones (output width or contraction >= this, e.g. BERT's MLM decoder, 30522
+# padded to 30528): the MFMA kernel there (edge tiles, K up to the vocabulary) — the library's
+# kernels for those shapes ran 0.93 PF/s in the BERT step (profiles/r5_bert_b768_step_kernels_persist.txt:
+# 985 us forward) against 795 us on the MFMA kernel (APEX_GEMM_PLAIN=own profile). 0 disables.
+_VOCAB_MIN = int(os.environ.get("APEX_GEMM_VOCAB_MIN", "16384"))
+
+
+def _vocab_sized(a, w):
+    return _VOCAB_MIN > 0 and (w.shape[0] >= _VOCAB_MIN or a.shape[-1] >= _VOCAB_MIN)
 
 
 def _C():
@@ -73,7 +82,8 @@ def mode() -> str:
 
 def use_mfma(a, w, fused=True) -> bool:
     """MFMA kernel for this call? ``fused``: the call carries an epilogue the library lacks."""
-    if _MODE == "blas" or not a.is_cuda or (_MODE == "auto" and not fused and _PLAIN != "own"):
+    if _MODE == "blas" or not a.is_cuda or (_MODE == "auto" and not fused and _PLAIN != "own"
+                                            and not _vocab_sized(a, w)):
         return False
     return _C().gemm_supported(a, w)
 
@@ -178,7 +188,7 @@ def dgrad(dy, w, wT=None, f8=None):
         r = f8.backward_gemm(a, w, _C().EPI_NONE)
         if r is not None:
             return r[0].view(*dy.shape[:-1], w.shape[1])
-    if (_MODE == "mfma" or (_MODE == "auto" and _PLAIN == "own")) and a.is_cuda:
+    if (_MODE == "mfma" or (_MODE == "auto" and (_PLAIN == "own" or _vocab_sized(a, w)))) and a.is_cuda:
         wT = transpose(w) if wT is None else wT
         if use_mfma(a, wT, fused=False):
             C = _C()
