@@ -38,3 +38,15 @@ def test_library_split_k_fills_the_chip(monkeypatch):
         tiles = ((n + 255) // 256) * ((k + 255) // 256)
         assert M % s == 0 and s * tiles <= 256 and (s == 16 or 2 * s * tiles > 256)
     assert fused._wgrad_splits(4096, 1024, 1024) == 1
+
+
+def test_vocab_sized_weight_gradients_take_the_kernel(monkeypatch):
+    """An MLM decoder / LM head weight (vocabulary rows) goes to the transposed-read kernel in one
+    slice; APEX_WGRAD_TT_VOCAB=0 leaves it on the library."""
+    monkeypatch.setattr(fused, "_WGRAD_TT", "auto")
+    monkeypatch.setattr(fused, "_WGRAD_TT_VOCAB", True)
+    assert fused._wgrad_tt_splits(14592, 30528, 1024) == 1  # BERT-Large MLM decoder, b768
+    assert fused._wgrad_tt_splits(16384, 50304, 1600) == 1  # GPT-2 LM head
+    assert fused._wgrad_tt_splits(14590, 30528, 1024) == 0  # tokens not a multiple of 64
+    monkeypatch.setattr(fused, "_WGRAD_TT_VOCAB", False)
+    assert fused._wgrad_tt_splits(14592, 30528, 1024) == 0
