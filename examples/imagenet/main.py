@@ -37,7 +37,7 @@ from apex.fp16_utils import (FP16_Optimizer, master_params_to_model_params, mode
 from apex.models import resnet
 from apex.parallel import DistributedDataParallel as DDP
 from apex.parallel import Reducer, convert_syncbn_model
-from apex.utils.metrics import AverageMeter, reduce_tensor
+from apex.utils.metrics import AverageMeter, reduce_scalars
 from apex.utils.prefetch import DataPrefetcher
 
 ARCHS = ["resnet18", "resnet34", "resnet50", "resnet101", "resnet152"]
@@ -268,7 +268,8 @@ class Trainer:
             self._backward_step(loss)
             if i % a.print_freq == 0 or i == n - 1:
                 p1, p5 = accuracy(out.float().detach(), y, (1, 5))
-                rl, r1, r5 = (reduce_tensor(t.detach().reshape(1)) for t in (loss, p1, p5))
+                # one collective for the three metrics (reference main.py:485-489 issues one each)
+                rl, r1, r5 = reduce_scalars(loss, p1, p5)
                 if self.cuda:
                     torch.cuda.synchronize()
                 losses.update(float(rl), x.size(0))
@@ -292,7 +293,7 @@ class Trainer:
             out = self.model(x).float()
             loss = self.criterion(out, y)
             p1, p5 = accuracy(out, y, (1, 5))
-            rl, r1, r5 = (reduce_tensor(t.reshape(1)) for t in (loss, p1, p5))
+            rl, r1, r5 = reduce_scalars(loss, p1, p5)
             losses.update(float(rl), x.size(0))
             top1.update(float(r1), x.size(0))
             top5.update(float(r5), x.size(0))
