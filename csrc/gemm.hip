@@ -49,7 +49,12 @@
 namespace apex {
 namespace {
 
-constexpr int GB_M = 256, GB_N = 256, GB_K = 64, G_THREADS = 512, G_GROUP_M = 8;
+// G_GROUP_M: M-tiles per panel of the tile order (consecutive workgroups walk GROUP_M M-tiles down
+// one N column before moving right); APEX_G_GROUP_M overrides it at build time (lab sweeps)
+#ifndef APEX_G_GROUP_M
+#define APEX_G_GROUP_M 8
+#endif
+constexpr int GB_M = 256, GB_N = 256, GB_K = 64, G_THREADS = 512, G_GROUP_M = APEX_G_GROUP_M;
 constexpr int G_TILE_BYTES = GB_M * GB_K * 2;       // one operand tile: 32 KB
 constexpr int G_BUF_BYTES = 2 * G_TILE_BYTES;       // A + B: 64 KB
 constexpr int G_LDS_BYTES = 2 * G_BUF_BYTES;        // double buffered: 128 KB

@@ -91,7 +91,7 @@ template <int EPI, int DBG = 0>
 void launch_persist(const Bufs& b, hipStream_t s) {
   const int tiles = (b.M / 256) * (b.N / 256);
   const int grid = std::min(tiles, g_cus);
-  hipLaunchKernelGGL((gemm_persist_kernel<bf16, EPI, DBG>), dim3(grid), dim3(512), 0, s, b.A, b.B, b.C, b.M, b.N, b.K,
+  hipLaunchKernelGGL((gemm_persist_kernel<bf16, EPI, bf16, -1, -1, 0, DBG>), dim3(grid), dim3(512), 0, s, b.A, b.B, b.C, b.M, b.N, b.K,
                      (int64_t)b.K, (int64_t)b.K, (int64_t)b.N, b.bias, b.aux, (int64_t)b.N, b.aux_out, b.part, g_trace);
 }
 
