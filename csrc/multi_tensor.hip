@@ -236,7 +236,7 @@ __global__ void __launch_bounds__(kBlock) sgd_kernel(MTMeta m, SgdArgs a) {
       for (int u = 0; u < NG; ++u) {
         store_f_nt<P, NE>(p + j0 + u * st, pv[u]);
         if (mom) store_f_nt<float, NE>(mom + j0 + u * st, mv[u]);
-        if (cp) store_f<C, NE>(cp + j0 + u * st, pv[u]);
+        if (cp) store_f_nt<C, NE>(cp + j0 + u * st, pv[u]);
       }
     });
   }
@@ -302,7 +302,7 @@ __global__ void __launch_bounds__(kBlock) adam_kernel(MTMeta m, AdamArgs a) {
         store_f_nt<P, NE>(p + j0 + u * st, pv[u]);
         store_f_nt<float, NE>(mm + j0 + u * st, mv[u]);
         store_f_nt<float, NE>(vv + j0 + u * st, vq[u]);
-        if (cp) store_f<C, NE>(cp + j0 + u * st, pv[u]);
+        if (cp) store_f_nt<C, NE>(cp + j0 + u * st, pv[u]);
       }
     });
   }
@@ -365,7 +365,10 @@ __global__ void __launch_bounds__(kBlock) lamb_stage1_kernel(MTMeta m, LambArgs 
   const float gs = read_scale(a.grad_scale_ptr, a.grad_scale) / scal[1];
   const float rbc1 = 1.f / scal[2], rbc2 = 1.f / scal[3];
   const float b1 = a.beta1, b2 = a.beta2, b3 = a.grad_averaging ? 1.f - a.beta1 : 1.f;
-  for (int c = blockIdx.x; c < m.nchunks; c += gridDim.x) {
+  // last chunk first: the grad-norm pass just read the gradients in ascending order, so the
+  // chunks it read last may still sit in the 256 MB infinity cache
+  for (int cc = blockIdx.x; cc < m.nchunks; cc += gridDim.x) {
+    const int c = m.nchunks - 1 - cc;
     const ChunkView cv = chunk_view(m, c);
     const G* g = (const G*)m.ptr(0, cv.t) + cv.start;
     const P* p = (const P*)m.ptr(1, cv.t) + cv.start;
@@ -442,7 +445,7 @@ __global__ void __launch_bounds__(kBlock) lamb_stage2_kernel(MTMeta m, LambArgs 
 #pragma unroll
       for (int u = 0; u < NG; ++u) {
         store_f_nt<P, NE>(p + j0 + u * st, pv[u]);
-        if (cp) store_f<C, NE>(cp + j0 + u * st, pv[u]);
+        if (cp) store_f_nt<C, NE>(cp + j0 + u * st, pv[u]);
       }
     });
   }
