@@ -121,7 +121,24 @@ def _wgrad_tt_splits(M, N, K):
 # profiles/r5_gpt2_wgrad_tt_ab.jsonl; a likely cause, unverified: the isolated loop re-reads the same
 # ~260 MB of operands, mostly served from the 256 MB Infinity Cache) — so the library keeps them (forced APEX_WGRAD_TT=<slices>
 # still runs any multiple-of-8 shape on the kernel).
+# APEX_WGRAD_TT_TABLE replaces the table for A/B runs: "NxK:min_tokens:slices,..." ("none": empty).
 _WGRAD_TT_MEASURED = {}
+
+
+def _parse_tt_table(spec):
+    table = {}
+    for item in spec.split(","):
+        item = item.strip()
+        if not item or item == "none":
+            continue
+        nk, m_min, s = item.split(":")
+        n, k = nk.split("x")
+        table[(int(n), int(k))] = (int(m_min), int(s))
+    return table
+
+
+if os.environ.get("APEX_WGRAD_TT_TABLE") is not None:
+    _WGRAD_TT_MEASURED = _parse_tt_table(os.environ["APEX_WGRAD_TT_TABLE"])
 
 
 def _gt(p):

@@ -982,8 +982,8 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[NJ][8], char* reg, T
   }
 }
 
-// Launch control word (kernel argument `ctl`, no device-variable load in the kernel): bits 0..15
-// first-round stagger units, bits 16.. diagnostics mode (2 = skip the epilogue: main-loop-only
+// Launch control word (kernel argument `ctl`, no device-variable load in the kernel): bits 0..14
+// first-round stagger units, bit 15 the split-major XCD remap (kCtlSplitXcd), bits 16.. diagnostics mode (2 = skip the epilogue: main-loop-only
 // timing, tools/gemm_epi_cost.py). Both are host statics set by gemm_set_dbg().
 // First-round stagger (experiment, off by default): half of the first round's workgroups (bid & 8)
 // sleep `units` x s_sleep(127) before starting, offsetting every later tile on those CUs so their
@@ -991,6 +991,17 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[NJ][8], char* reg, T
 // bias+GELU 362 -> 312 us; the BERT step was 2.4 % SLOWER (profiles/r1_gemm_stagger.json); at
 // M = 98304 no unit count helps any fused shape (profiles/r3_gemmlab_w8_stagger.jsonl).
 int h_gemm_dbg = 0, h_gemm_stagger = 0;  // stagger: > 0 forced units, < 0 forced off, 0 launcher's
+// ctl bit 15: split-major XCD remap of split-K (transposed-read) launches, APEX_GEMM_SPLIT_XCD=0 turns
+// it off (A/B)
+constexpr int kCtlSplitXcd = 0x8000;
+inline bool host_split_xcd() {
+  static int on = -1;
+  if (on == -1) {
+    const char* e = getenv("APEX_GEMM_SPLIT_XCD");
+    on = (e && e[0] == '0') ? 0 : 1;
+  }
+  return on == 1;
+}
 
 // T: output / epilogue dtype; TI: operand dtype (T, or uint8_t fp8 with formats FA (A) / FB (B) and
 // the dequantisation alpha = alpha_a[0] * alpha_b[0] read on the device)
@@ -1014,8 +1025,20 @@ __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(const TI* __restrict
   const int tiles_m = (M + GB_M - 1) / GB_M, tiles_n = (N + GB_N - 1) / GB_N;
   const int nwg = tiles_m * tiles_n;
   const int bid = blockIdx.x;
-  const int xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
-  const int wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  int wg, split = TR ? (int)blockIdx.y : 0;
+  if (TR && (ctl & kCtlSplitXcd) && gridDim.y > 1) {
+    // split-K: the remap runs over (split, tile) jointly in dispatch order, split-major, so the
+    // workgroups an XCD holds share one K-range and meet each other's A / B panels in its L2 (tile-
+    // major, each dY panel of a weight gradient was streamed by every XCD holding one of its tiles)
+    const int L = bid + nwg * (int)blockIdx.y, nall = nwg * (int)gridDim.y;
+    const int xcd = L & 7, q = nall >> 3, rr = nall & 7;
+    const int v = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (L >> 3);
+    split = v / nwg;
+    wg = v - split * nwg;
+  } else {
+    const int xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
+    wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  }
   const int group = G_GROUP_M * tiles_n;
   const int first_m = (wg / group) * G_GROUP_M;
   const int gm = min(tiles_m - first_m, G_GROUP_M);
@@ -1035,14 +1058,14 @@ __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(const TI* __restrict
   if constexpr (DBG & 2048) tr0 = __builtin_amdgcn_s_memrealtime();
 
   {
-    const int st = ctl & 0xffff;
+    const int st = ctl & 0x7fff;
     if (st > 0 && bid < 256 && (bid & 8)) {
       for (int i = 0; i < st; ++i) __builtin_amdgcn_s_sleep(127);
     }
   }
-  if constexpr (TR) {  // split-K slice blockIdx.y: K-rows [y*K, (y+1)*K) of both operands
-    A += (int64_t)blockIdx.y * K * lda;
-    B += (int64_t)blockIdx.y * K * ldb;
+  if constexpr (TR) {  // split-K slice: K-rows [split*K, (split+1)*K) of both operands
+    A += (int64_t)split * K * lda;
+    B += (int64_t)split * K * ldb;
   }
   // mainloop_bal for the 16-bit kernels; the fp8 instantiations and the edge-tile dGELU / multiply
   // epilogues keep the previous schedule (their epilogues hold more registers: the balanced loop's
@@ -1059,7 +1082,7 @@ __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(const TI* __restrict
   if constexpr (EPI == EPI_F32) {
     // fp32 slab (split-K partials): each lane stores its 4 consecutive columns per fragment
     // (fp8 operands: dequantised here, alpha = the two per-tensor inverse scales)
-    float* out = part + (int64_t)blockIdx.y * M * ldc;
+    float* out = part + (int64_t)split * M * ldc;
     float sc = 1.f;
     if constexpr (FA >= 0) sc = alpha_a[0] * alpha_b[0];
 #pragma unroll
@@ -2272,7 +2295,8 @@ void launch_gemm(const GemmArgs& g, hipStream_t s) {
     }
   }
   const int units = h_gemm_stagger > 0 ? h_gemm_stagger : h_gemm_stagger < 0 ? 0 : host_stagger(EPI);
-  const int stagger = (units & 0xffff) | (h_gemm_dbg << 16);  // the kernel's ctl word
+  const int stagger = (units & 0x7fff) | (TR && host_split_xcd() ? kCtlSplitXcd : 0) |
+                      (h_gemm_dbg << 16);  // the kernel's ctl word
   const bool edge = g.M % GB_M != 0 || g.N % GB_N != 0;
   if (edge)  // (the transposed-read weight-gradient kernels too: partial tiles since round 5)
     hipLaunchKernelGGL((gemm_nt_kernel<T, EPI, TR, true>), dim3(tiles, TR ? g.splits : 1), dim3(G_THREADS), 0, s,
@@ -2482,12 +2506,12 @@ void launch_gemm_tt_f8(const GemmArgs& g, hipStream_t s) {
     hipLaunchKernelGGL((gemm_nt_kernel<bf16, EPI_F32, true, true, uint8_t, FA, FB>), dim3(tiles, g.splits),
                        dim3(G_THREADS), 0, s, (const uint8_t*)g.A, (const uint8_t*)g.B, (bf16*)nullptr, g.M, g.N, g.K,
                        g.lda, g.ldb, g.ldc, (const bf16*)nullptr, (const bf16*)nullptr, (int64_t)0, (bf16*)nullptr,
-                       g.part, 0, g.alpha_a, g.alpha_b);
+                       g.part, host_split_xcd() ? kCtlSplitXcd : 0, g.alpha_a, g.alpha_b);
   else
     hipLaunchKernelGGL((gemm_nt_kernel<bf16, EPI_F32, true, false, uint8_t, FA, FB>), dim3(tiles, g.splits),
                        dim3(G_THREADS), 0, s, (const uint8_t*)g.A, (const uint8_t*)g.B, (bf16*)nullptr, g.M, g.N, g.K,
                        g.lda, g.ldb, g.ldc, (const bf16*)nullptr, (const bf16*)nullptr, (int64_t)0, (bf16*)nullptr,
-                       g.part, 0, g.alpha_a, g.alpha_b);
+                       g.part, host_split_xcd() ? kCtlSplitXcd : 0, g.alpha_a, g.alpha_b);
 }
 
 int gemm_tt_f8(const GemmArgs& g, int fmt_a, int fmt_b, hipStream_t s) {
