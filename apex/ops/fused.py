@@ -121,8 +121,12 @@ def _wgrad_tt_splits(M, N, K):
 # profiles/r5_gpt2_wgrad_tt_ab.jsonl; a likely cause, unverified: the isolated loop re-reads the same
 # ~260 MB of operands, mostly served from the 256 MB Infinity Cache) — so the library keeps them (forced APEX_WGRAD_TT=<slices>
 # still runs any multiple-of-8 shape on the kernel).
+# Round 5, after the split-major XCD remap and with the library on its TunableOp selections (the
+# isolated tool's 'lib' rows were untuned before: profiles/r5_wgrad_tt_vs_tuned_lib.jsonl): the
+# attention-out weight gradients win on the kernel — BERT-Large 1024x1024 at 16 slices 198 vs 226 us,
+# GPT-2 1.5B 1600x1600 at 4 slices 117 vs 137 us — and GPT-2's FFN shapes lose (372 / 365 vs 335 / 325).
 # APEX_WGRAD_TT_TABLE replaces the table for A/B runs: "NxK:min_tokens:slices,..." ("none": empty).
-_WGRAD_TT_MEASURED = {}
+_WGRAD_TT_MEASURED = {(1024, 1024): (65536, 16), (1600, 1600): (16384, 4)}
 
 
 def _parse_tt_table(spec):

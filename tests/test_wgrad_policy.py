@@ -9,10 +9,18 @@ def test_tt_auto_takes_the_ffn_shapes_only(monkeypatch):
     assert fused._wgrad_tt_splits(M, 4096, 1024) == 4  # FFN1: 64 tiles -> one wave of 256 workgroups
     assert fused._wgrad_tt_splits(M, 1024, 4096) == 4  # FFN2
     assert fused._wgrad_tt_splits(M, 3072, 1024) == 0  # QKV (48 tiles): library
-    assert fused._wgrad_tt_splits(M, 1024, 1024) == 0  # attention out (16 tiles): library
+    assert fused._wgrad_tt_splits(M, 1024, 1024) == 16  # attention out (16 tiles): measured, 16 slices
+    assert fused._wgrad_tt_splits(32768, 1024, 1024) == 0  # ... below its measured token count: library
+    assert fused._wgrad_tt_splits(16384, 1600, 1600) == 4  # GPT-2 1.5B attention out: measured
     assert fused._wgrad_tt_splits(8192, 4096, 1024) == 0  # too few tokens
     assert fused._wgrad_tt_splits(M, 1600, 4800) == 0  # partial tiles, unmeasured: library
     assert fused._wgrad_tt_splits(M, 2560, 7680) == 0  # 300 tiles: unmeasured, library
+
+
+def test_tt_table_from_env():
+    assert fused._parse_tt_table("none") == {}
+    assert fused._parse_tt_table("1024x1024:65536:16, 1600x6400:16384:4") == {(1024, 1024): (65536, 16),
+                                                                               (1600, 6400): (16384, 4)}
 
 
 def test_tt_overrides(monkeypatch):

@@ -28,7 +28,15 @@ def main():
                     help="name:NxK,... (GPT-2 1.5B at M = 16384: qkv:4800x1600,attn_out:1600x1600,"
                          "ffn1:6400x1600,ffn2:1600x6400)")
     ap.add_argument("--splits", default="2,4,8,16")
+    ap.add_argument("--untuned", action="store_true",
+                    help="library GEMMs on hipBLASLt's default heuristics instead of the committed TunableOp "
+                         "selections the model benchmarks load (before round 5's split-XCD runs the tool had no "
+                         "TunableOp: its 'lib' rows were untuned)")
     args = ap.parse_args()
+    if not args.untuned:
+        from apex.utils.gemm_tuning import enable_tuned_gemms
+
+        enable_tuned_gemms()
     M = args.M
     shapes = {}
     for item in args.shapes.split(","):
