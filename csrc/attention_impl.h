@@ -541,34 +541,56 @@ attn_fwd_kernel(AttnArgs a) {
   // ---- epilogue
   const float ltot = l + xor32_f(l);
   float q8mx = 0.f;
+  const float inv = ltot > 0.f ? (DROPOUT ? a.drop_scale : 1.f) / ltot : 0.f;
+  // O rows packed to 16-bit: lane (r, hl) holds columns 32 db + 8 g + 4 hl .. + 3 of row qrow
+  typedef T t4 __attribute__((ext_vector_type(4)));
+  uint2 wv[D / 32][4];
+#pragma unroll
+  for (int db = 0; db < D / 32; ++db)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      t4 w;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) w[e] = (T)(o[db][4 * g + e] * inv);
+      wv[db][g] = __builtin_bit_cast(uint2, w);
+    }
+  // 16-byte row stores (cdna_hip_programming.md T21): for each column-group pair (g, g + 1) one
+  // v_permlane32_swap per dword gives the lower half-wave columns 8 g .. 8 g + 7 of its row and the
+  // upper half 8 g + 8 .. 8 g + 15 — half the store instructions of the 8-byte row-per-lane-pair
+  // stores, same bytes (the store tail of a short-lived workgroup is issue-bound). The swaps run on
+  // every lane, ahead of the row-validity branch.
+  uint4 wide[D / 32][2];
+#pragma unroll
+  for (int db = 0; db < D / 32; ++db)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const auto rx = __builtin_amdgcn_permlane32_swap(wv[db][2 * j].x, wv[db][2 * j + 1].x, false, false);
+      const auto ry = __builtin_amdgcn_permlane32_swap(wv[db][2 * j].y, wv[db][2 * j + 1].y, false, false);
+      wide[db][j] = make_uint4(rx[0], ry[0], rx[1], ry[1]);
+    }
   if (qrow < a.Sq) {
-    const float inv = ltot > 0.f ? (DROPOUT ? a.drop_scale : 1.f) / ltot : 0.f;
     const int64_t ooff = b * a.o_bs + h * a.o_hs + (int64_t)qrow * a.o_ss;
     T* op = (T*)a.o + ooff;
-    const float qs = a.q8o ? a.q8_scale[0] : 0.f;
+#pragma unroll
+    for (int db = 0; db < D / 32; ++db)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) *(uint4*)(op + 32 * db + 16 * j + 8 * hl) = wide[db][j];
     // Q8 (0: none, 1: e4m3, 2: e5m2) hoisted out of the store loop: fp8 codes of the stored
     // (rounded) values, the attention-out GEMM's operand, from the packed words (f8_codes4)
-    auto store_o = [&](auto Q8c) {
+    const float qs = a.q8o ? a.q8_scale[0] : 0.f;
+    auto store_q8 = [&](auto Q8c) {
       constexpr int Q8 = decltype(Q8c)::value;
 #pragma unroll
-      for (int db = 0; db < D / 32; ++db) {
+      for (int db = 0; db < D / 32; ++db)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          typedef T t4 __attribute__((ext_vector_type(4)));
-          t4 w;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) w[e] = (T)(o[db][4 * g + e] * inv);
-          *(t4*)(op + 32 * db + 8 * g + 4 * hl) = w;
-          if constexpr (Q8 != 0) {
-            const uint2 ww = __builtin_bit_cast(uint2, w);
-            *(uint32_t*)(a.q8o + ooff + 32 * db + 8 * g + 4 * hl) = f8_codes4<Q8 - 1, T>(ww.x, ww.y, qs, q8mx);
-          }
-        }
-      }
+        for (int g = 0; g < 4; ++g)
+          *(uint32_t*)(a.q8o + ooff + 32 * db + 8 * g + 4 * hl) =
+              f8_codes4<Q8 - 1, T>(wv[db][g].x, wv[db][g].y, qs, q8mx);
     };
-    if (!a.q8o) store_o(std::integral_constant<int, 0>{});
-    else if (a.q8_fmt == 0) store_o(std::integral_constant<int, 1>{});
-    else store_o(std::integral_constant<int, 2>{});
+    if (a.q8o) {
+      if (a.q8_fmt == 0) store_q8(std::integral_constant<int, 1>{});
+      else store_q8(std::integral_constant<int, 2>{});
+    }
     if (hl == 0 && a.lse)
       a.lse[(int64_t)bh * a.Sq + qrow] = ltot > 0.f ? (m * sl2 + log2f(ltot)) * kLn2 : INFINITY;
   }
@@ -944,22 +966,46 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
       }
       // this workgroup is the sole writer of these query rows (single key block): final dtype
       const int q = qb + 16 * qt + lq;
+      typedef T t4 __attribute__((ext_vector_type(4)));
+      uint2 wq[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        t4 w;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) w[i] = (T)(acc[t][i] * a.scale);
+        wq[t] = __builtin_bit_cast(uint2, w);
+      }
+      // 16-byte stores (as the forward's O, T21): lanes of 16-lane rows lg and lg + 1 hold 4 dims each
+      // of the same query for dim tiles t and t + 1; one v_permlane16_swap per dword gives the even
+      // rows dims 4 lg .. 4 lg + 7 of tile t and the odd rows those of tile t + 1 (every lane, ahead
+      // of the row-validity branch)
+      constexpr bool WIDE = NT % 2 == 0;
+      uint4 wd[WIDE ? NT / 2 : 1];
+      if constexpr (WIDE) {
+#pragma unroll
+        for (int t = 0; t < NT; t += 2) {
+          const auto rx = __builtin_amdgcn_permlane16_swap(wq[t].x, wq[t + 1].x, false, false);
+          const auto ry = __builtin_amdgcn_permlane16_swap(wq[t].y, wq[t + 1].y, false, false);
+          wd[t / 2] = make_uint4(rx[0], ry[0], rx[1], ry[1]);
+        }
+      }
       if (q < nq) {
         const int64_t qoff = b * a.dq_bs + h * a.dq_hs + (int64_t)q * a.dq_ss;
         T* dqp = (T*)a.dq + qoff;
+        if constexpr (WIDE) {
+#pragma unroll
+          for (int t = 0; t < NT; t += 2)
+            *(uint4*)(dqp + (dt0 + t + (lg & 1)) * 16 + 8 * (lg >> 1)) = wd[t / 2];
+        }
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
-          typedef T t4 __attribute__((ext_vector_type(4)));
-          t4 w;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) w[i] = (T)(acc[t][i] * a.scale);
-          *(t4*)(dqp + (dt0 + t) * 16 + 4 * lg) = w;
+          if constexpr (!WIDE) *(uint2*)(dqp + (dt0 + t) * 16 + 4 * lg) = wq[t];
           if (a.q8dq) {  // fp8 codes of dq as stored (the QKV input-gradient GEMM's operand)
-            const uint2 ww = __builtin_bit_cast(uint2, w);
             *(uint32_t*)(a.q8dq + qoff + (dt0 + t) * 16 + 4 * lg) =
-                a.q8_fmt == 0 ? f8_codes4<0, T>(ww.x, ww.y, q8s, q8mx) : f8_codes4<1, T>(ww.x, ww.y, q8s, q8mx);
+                a.q8_fmt == 0 ? f8_codes4<0, T>(wq[t].x, wq[t].y, q8s, q8mx) : f8_codes4<1, T>(wq[t].x, wq[t].y, q8s, q8mx);
           }
           if constexpr (DSUM) {
+            const t4 w = __builtin_bit_cast(t4, wq[t]);
 #pragma unroll
             for (int i = 0; i < 4; ++i) dqcs[t][i] += (float)w[i];
           }
@@ -1266,18 +1312,30 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
   } else {
     for (int kt = 0; kt < ntiles; ++kt) tile(kva, kt);
   }
-  // ---- epilogue: element 4g+e of block db -> dim 32db + 8g + 4hl + e of query qrow
+  // ---- epilogue: element 4g+e of block db -> dim 32db + 8g + 4hl + e of query qrow; 16-byte
+  // stores through one v_permlane32_swap per dword and column-group pair (as the forward's O)
   float* dsum = DSUM ? a.dsum + ((int64_t)b * 3 * a.H + h) * D : nullptr;
+  T* dqrow = (T*)a.dq + b * a.dq_bs + h * a.dq_hs + (int64_t)qrow * a.dq_ss;
 #pragma unroll
   for (int db = 0; db < D / 32; ++db) {
+    typedef T t4 __attribute__((ext_vector_type(4)));
+    uint2 wv[4];
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      typedef T t4 __attribute__((ext_vector_type(4)));
       t4 w;
 #pragma unroll
       for (int e = 0; e < 4; ++e) w[e] = (T)(dq[db][4 * g + e] * a.scale);
-      if (qrow < a.Sq)
-        *(t4*)((T*)a.dq + b * a.dq_bs + h * a.dq_hs + (int64_t)qrow * a.dq_ss + 32 * db + 8 * g + 4 * hl) = w;
+      wv[g] = __builtin_bit_cast(uint2, w);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const auto rx = __builtin_amdgcn_permlane32_swap(wv[2 * j].x, wv[2 * j + 1].x, false, false);
+      const auto ry = __builtin_amdgcn_permlane32_swap(wv[2 * j].y, wv[2 * j + 1].y, false, false);
+      if (qrow < a.Sq) *(uint4*)(dqrow + 32 * db + 16 * j + 8 * hl) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const t4 w = __builtin_bit_cast(t4, wv[g]);
       if constexpr (DSUM) {
         // column sums of the stored values over this wave's 32 query rows (lanes r), then one
         // atomic per dim per wave
