@@ -578,14 +578,18 @@ attn_fwd_kernel(AttnArgs a) {
     // Q8 (0: none, 1: e4m3, 2: e5m2) hoisted out of the store loop: fp8 codes of the stored
     // (rounded) values, the attention-out GEMM's operand, from the packed words (f8_codes4)
     const float qs = a.q8o ? a.q8_scale[0] : 0.f;
+    // (the codes' dwords regrouped by the same swap: 8-byte stores of 8 consecutive columns)
     auto store_q8 = [&](auto Q8c) {
       constexpr int Q8 = decltype(Q8c)::value;
 #pragma unroll
       for (int db = 0; db < D / 32; ++db)
 #pragma unroll
-        for (int g = 0; g < 4; ++g)
-          *(uint32_t*)(a.q8o + ooff + 32 * db + 8 * g + 4 * hl) =
-              f8_codes4<Q8 - 1, T>(wv[db][g].x, wv[db][g].y, qs, q8mx);
+        for (int j = 0; j < 2; ++j) {
+          const uint32_t c0 = f8_codes4<Q8 - 1, T>(wv[db][2 * j].x, wv[db][2 * j].y, qs, q8mx);
+          const uint32_t c1 = f8_codes4<Q8 - 1, T>(wv[db][2 * j + 1].x, wv[db][2 * j + 1].y, qs, q8mx);
+          const auto rc = __builtin_amdgcn_permlane32_swap(c0, c1, false, false);
+          *(uint2*)(a.q8o + ooff + 32 * db + 16 * j + 8 * hl) = make_uint2(rc[0], rc[1]);
+        }
     };
     if (a.q8o) {
       if (a.q8_fmt == 0) store_q8(std::integral_constant<int, 1>{});
@@ -997,13 +1001,25 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
           for (int t = 0; t < NT; t += 2)
             *(uint4*)(dqp + (dt0 + t + (lg & 1)) * 16 + 8 * (lg >> 1)) = wd[t / 2];
         }
+        if (a.q8dq) {  // fp8 codes of dq as stored (the QKV input-gradient GEMM's operand)
+          uint32_t cq[NT];
+#pragma unroll
+          for (int t = 0; t < NT; ++t)
+            cq[t] = a.q8_fmt == 0 ? f8_codes4<0, T>(wq[t].x, wq[t].y, q8s, q8mx) : f8_codes4<1, T>(wq[t].x, wq[t].y, q8s, q8mx);
+          if constexpr (WIDE) {  // the same regrouping: 8-byte stores (rows lg, lg + 1 share the query)
+#pragma unroll
+            for (int t = 0; t < NT; t += 2) {
+              const auto rc = __builtin_amdgcn_permlane16_swap(cq[t], cq[t + 1], false, false);
+              *(uint2*)(a.q8dq + qoff + (dt0 + t + (lg & 1)) * 16 + 8 * (lg >> 1)) = make_uint2(rc[0], rc[1]);
+            }
+          } else {
+#pragma unroll
+            for (int t = 0; t < NT; ++t) *(uint32_t*)(a.q8dq + qoff + (dt0 + t) * 16 + 4 * lg) = cq[t];
+          }
+        }
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
           if constexpr (!WIDE) *(uint2*)(dqp + (dt0 + t) * 16 + 4 * lg) = wq[t];
-          if (a.q8dq) {  // fp8 codes of dq as stored (the QKV input-gradient GEMM's operand)
-            *(uint32_t*)(a.q8dq + qoff + (dt0 + t) * 16 + 4 * lg) =
-                a.q8_fmt == 0 ? f8_codes4<0, T>(wq[t].x, wq[t].y, q8s, q8mx) : f8_codes4<1, T>(wq[t].x, wq[t].y, q8s, q8mx);
-          }
           if constexpr (DSUM) {
             const t4 w = __builtin_bit_cast(t4, wq[t]);
 #pragma unroll
