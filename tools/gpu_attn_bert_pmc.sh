@@ -1,10 +1,13 @@
 #!/bin/bash
-# BERT-shape attention (b256 s128 h16 d64, p 0.1): timing + where the waves spend their cycles
+# BERT-shape attention (SHAPE: bert = b256 s128 h16 d64, bert768 = b768; p 0.1): timing + where the
+# waves spend their cycles
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/${OUT:-bpmc}
+SHAPE=${SHAPE:-bert}
+export O
 mkdir -p $O
-timeout -k 10 200 python tools/attn_bench.py --only bert > $O/bench.jsonl 2> $O/bench.err || { tail -5 $O/bench.err; exit 2; }
+timeout -k 10 200 python tools/attn_bench.py --only $SHAPE > $O/bench.jsonl 2> $O/bench.err || { tail -5 $O/bench.err; exit 2; }
 cat $O/bench.jsonl
 i=0
 for P in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_MFMA SQ_BUSY_CYCLES" \
@@ -12,14 +15,15 @@ for P in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTI
          "FETCH_SIZE GRBM_COUNT"; do
   i=$((i+1))
   for pas in fwd bwd; do
-    timeout -s KILL 90 rocprofv3 --kernel-trace --pmc $P -d $O/${pas}_p$i -o p --output-format csv -- python tools/attn_one.py bert $pas 0.1 4 > $O/${pas}_p$i.log 2>&1 || { echo "pass $i $pas failed"; tail -5 $O/${pas}_p$i.log; exit 3; }
+    timeout -s KILL 90 rocprofv3 --kernel-trace --pmc $P -d $O/${pas}_p$i -o p --output-format csv -- python tools/attn_one.py $SHAPE $pas 0.1 4 > $O/${pas}_p$i.log 2>&1 || { echo "pass $i $pas failed"; tail -5 $O/${pas}_p$i.log; exit 3; }
   done
 done
 python - <<'PY'
-import csv, glob, json, collections
+import csv, glob, json, collections, os
 out = {}
-for f in glob.glob("gpurun_out/bpmc/*_p*/**/*counter_collection.csv", recursive=True):
-    pas = f.split("/")[2].split("_")[0]
+O = os.environ["O"]
+for f in glob.glob(O + "/*_p*/**/*counter_collection.csv", recursive=True):
+    pas = os.path.relpath(f, O).split("/")[0].split("_")[0]
     acc = collections.defaultdict(list)
     for r in csv.DictReader(open(f)):
         if "attn_" not in r["Kernel_Name"] or "delta" in r["Kernel_Name"]:
@@ -28,5 +32,6 @@ for f in glob.glob("gpurun_out/bpmc/*_p*/**/*counter_collection.csv", recursive=
     for k, v in acc.items():
         v.sort()
         out.setdefault(pas, {})[k] = v[len(v) // 2]
+json.dump(out, open(O + "/pmc_summary.json", "w"), indent=1)
 print(json.dumps(out, indent=1))
 PY
