@@ -135,9 +135,12 @@ def _parse_tt_table(spec):
         item = item.strip()
         if not item or item == "none":
             continue
-        nk, m_min, s = item.split(":")
-        n, k = nk.split("x")
-        table[(int(n), int(k))] = (int(m_min), int(s))
+        try:
+            nk, m_min, s = item.split(":")
+            n, k = nk.split("x")
+            table[(int(n), int(k))] = (int(m_min), int(s))
+        except ValueError as e:
+            raise ValueError(f"APEX_WGRAD_TT_TABLE entry {item!r}: expected NxK:min_tokens:slices") from e
     return table
 
 

@@ -21,6 +21,10 @@ def test_tt_table_from_env():
     assert fused._parse_tt_table("none") == {}
     assert fused._parse_tt_table("1024x1024:65536:16, 1600x6400:16384:4") == {(1024, 1024): (65536, 16),
                                                                                (1600, 6400): (16384, 4)}
+    import pytest
+
+    with pytest.raises(ValueError, match="APEX_WGRAD_TT_TABLE"):
+        fused._parse_tt_table("1024x1024:16")
 
 
 def test_tt_overrides(monkeypatch):
