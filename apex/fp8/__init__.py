@@ -148,7 +148,9 @@ class Fp8State:
         self._pre: dict = {}
         self._pre_bytes = 0
         self.prequant_hits = 0
-        self._last = None  # (data_ptr, shape, codes, scale_inv) of the last fp8 GEMM's activation operand
+        # (operand, its _version, codes, scale_inv) of the last fp8 GEMM's activation operand
+        self._last = None
+        self.wgrad_calls = 0  # fp8 weight-gradient GEMMs run (tests: the fp8 kernel, not the bf16 fallback)
         self._grow(128)
 
     # ------------------------------------------------------------------ slots
@@ -386,10 +388,11 @@ class Fp8State:
         ``q8`` (from ``produce``; bias+GELU epilogues): the epilogue also writes the output's fp8
         codes — ``q8_written(q8)`` tells the caller whether this call ran and wrote them."""
         if not self._fits(a, w, bias, aux, w.shape[1], w.shape[0]):
+            self._last = None  # a declined GEMM must not leave an older operand's codes claimable
             return None
         pre = self._take(a, self._fwd) if self._pre else None
         a8, ia = pre if pre is not None else self.quantize(a, (self.key_of(w), "x"), self._fwd)
-        self._last = (a.data_ptr(), tuple(a.shape), a8, ia)
+        self._last = self._remember(a, a8, ia)
         w8, iw = self.weight(w)
         kw = {}
         if q8 is not None:
@@ -406,10 +409,11 @@ class Fp8State:
     def backward_gemm(self, dy, w, epi, aux=None, bias_grad_dtype=None, q8=None):
         """dy [M, N] @ w[N, K] with epilogue ``epi`` (dy e5m2 x W^T e4m3) -> (out, extra) or None."""
         if not self._fits(dy, w, None, aux, w.shape[0], w.shape[1]):
+            self._last = None
             return None
         pre = self._take(dy, self._bwd) if self._pre else None
         d8, id_ = pre if pre is not None else self.quantize(dy, (self.key_of(w), "dy"), self._bwd)
-        self._last = (dy.data_ptr(), tuple(dy.shape), d8, id_)
+        self._last = self._remember(dy, d8, id_)
         wt8, iw = self.weight_t(w)
         kw = {}
         if q8 is not None:  # (dGELU / MUL epilogues: the hidden gradient's codes for the W1 dgrad)
@@ -425,9 +429,20 @@ class Fp8State:
         — no second quantisation of either tensor. scale_inv is a view of the slot, which only
         ``step()`` rewrites, i.e. after every backward of the step."""
         e, self._last = self._last, None
-        if e is None or e[0] != a.data_ptr() or e[1] != tuple(a.shape) or not self.wgrad_enabled():
+        if e is None or not self.wgrad_enabled():
             return None
-        return e[2], e[3]
+        t, ver, codes, sinv = e
+        # the consumed operand is held (strongly: callers pass fresh reshaped views, so object identity
+        # says nothing) until this claim or the next fp8 GEMM, so its memory cannot have been freed and
+        # reused by another tensor; same address + shape = the same bytes, and its version counter
+        # (shared by every view of the storage) rules out an in-place write since the codes were taken
+        if a.data_ptr() != t.data_ptr() or tuple(a.shape) != tuple(t.shape) or t._version != ver:
+            return None
+        return codes, sinv
+
+    @staticmethod
+    def _remember(t, codes, sinv):
+        return (t, t._version, codes, sinv)
 
     def wgrad_enabled(self):
         return self.recipe.fp8_wgrad and _FP8_WGRAD != "0" and self._fwd == E4M3
@@ -443,6 +458,7 @@ class Fp8State:
         C = _C()
         if not s or not C.gemm_tt_f8_supported(d8, x8, s):
             return None
+        self.wgrad_calls += 1
         return C.gemm_tt_f8(d8, x8, sd, sx, self._bwd, self._fwd, s, out_dtype, out=out)
 
     # ------------------------------------------------------------------ step

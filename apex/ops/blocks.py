@@ -57,19 +57,36 @@ class _GammaZeroCheck:
     holding it for every sublayer until backward costs a [tokens, hidden] activation per sublayer
     (9 GB at BERT-Large b768). So the forward allocates and saves it only when this check says a
     zero is present. The check runs as ONE batched device reduction over every gamma seen so far
-    plus ONE host read, the first time a sublayer runs after a backward pass, i.e. once per step
-    (the optimizer, our fused kernels included, writes gammas only between a backward and the next
-    forward), or when a gamma's version counter / storage changed (in-place writes through autograd-
-    visible ops). Writes through `.data` between two forwards with no backward in between are not
-    seen: that is the one case this check misses.
+    plus ONE host read (a device -> host sync), the first time a sublayer runs after an optimizer
+    step — every torch.optim.Optimizer step, the apex fused optimizers included (they write gammas
+    through raw pointers, which no version counter sees), marks the check dirty through a global
+    step post-hook — or when a gamma's version counter / storage changed (in-place writes through
+    autograd-visible ops). So with gradient accumulation or a pipeline schedule the micro-batch
+    forwards that follow a backward do not stall the host: one read per optimizer step. Until the
+    first optimizer step of the process every backward marks it dirty too (a hand-written update
+    loop through `.data`). Writes through `.data` outside an optimizer step once optimizers are in
+    use, between two forwards, are not seen: that is the one case this check misses.
     """
 
     def __init__(self):
         self._known = {}  # id(gamma) -> (weakref, version, data_ptr, has_zero)
         self._dirty = True
+        self.host_reads = 0  # device -> host reads issued (tests: one per optimizer step)
+        self._steps_seen = False
 
     def mark_dirty(self):
         self._dirty = True
+
+    def after_optimizer_step(self):
+        self._steps_seen = True
+        self._dirty = True
+
+    def after_backward(self):
+        # until an optimizer step has been seen in this process the parameters may be updated by a
+        # hand-written loop (`p.data -= lr * p.grad`, invisible to version counters): re-check after
+        # every backward then, as before; once the step hook has fired, only after steps
+        if not self._steps_seen:
+            self._dirty = True
 
     def has_zero(self, gamma):
         import weakref
@@ -88,12 +105,23 @@ class _GammaZeroCheck:
                 flags = (flat.view(len(live), -1) == 0).any(dim=1).cpu()
             else:
                 flags = torch.stack([s.any() for s in (flat == 0).split(sizes)]).cpu()
+        self.host_reads += 1
         self._known = {id(g): (weakref.ref(g), g._version, g.data_ptr(), bool(f)) for g, f in zip(live, flags)}
         self._dirty = False
         return self._known[id(gamma)][3]
 
 
 _GZ = _GammaZeroCheck()
+
+
+def _gz_after_step(opt, args, kwargs):
+    _GZ.after_optimizer_step()
+
+
+# every optimizer step (torch.optim and apex.optimizers alike) may have written a gamma
+from torch.optim.optimizer import register_optimizer_step_post_hook  # noqa: E402
+
+register_optimizer_step_post_hook(_gz_after_step)
 
 
 def _ln_plan(C, gamma, cols, needs_grad):
@@ -179,7 +207,7 @@ class _AttnSublayer(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         C = _ext.require()
-        _GZ.mark_dirty()  # an optimizer step may follow: re-check the gammas at the next forward
+        _GZ.after_backward()
         x2, wqkv, qkv, o, lse, k_lens, dmask, wo, s, gamma, mean, rstd, s_alt = ctx.saved_tensors
         B, S, E, heads, d, scale, causal, p_attn, sa, oa, p_hidden, sh, oh, has_bqkv, has_bo, bdt = ctx.cfg
         pqkv, pbqkv, pwo, pbo, pg, pb = ctx.params
@@ -264,7 +292,7 @@ class _FFNSublayer(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         C = _ext.require()
-        _GZ.mark_dirty()
+        _GZ.after_backward()
         x2, w1, hb, h, g, w2, s, gamma, mean, rstd, s_alt = ctx.saved_tensors
         p, seed, off, act, has_b2, b1dt = ctx.cfg
         f8 = ctx.f8

@@ -57,15 +57,28 @@ from .. import _ext
 _MODE = os.environ.get("APEX_GEMM", "auto")
 # plain / bias-only products in auto mode: "lib" (hipBLASLt) or "own" (the persistent MFMA kernel)
 _PLAIN = os.environ.get("APEX_GEMM_PLAIN", "lib")
-# ... except vocabulary-sized ones (output width or contraction >= this, e.g. BERT's MLM decoder, 30522
-# padded to 30528): the MFMA kernel there (edge tiles, K up to the vocabulary) — the library's
-# kernels for those shapes ran 0.93 PF/s in the BERT step (profiles/r5_bert_b768_step_kernels_persist.txt:
-# 985 us forward) against 795 us on the MFMA kernel (APEX_GEMM_PLAIN=own profile). 0 disables.
-_VOCAB_MIN = int(os.environ.get("APEX_GEMM_VOCAB_MIN", "16384"))
+# ... except the vocabulary projections measured to win on the MFMA kernel, keyed on the weight's exact
+# shape [V, H] (plain forward and input gradient of that weight): BERT-Large's MLM decoder (30522
+# padded to 30528 rows): the library's kernels ran 0.93 PF/s there in the BERT step
+# (profiles/r5_bert_b768_step_kernels_persist.txt: 985 us forward) against 788 us forward / 648 us dgrad
+# on the MFMA kernel (profiles/r5_vocab_gemm_ab.jsonl). GPT-2's LM head measured neutral there, so it
+# is not listed, and no width threshold moves unmeasured shapes (a 16384-wide FFN) off the library.
+# APEX_GEMM_VOCAB_TABLE = "VxH,..." ("none": empty).
+def _parse_shapes(spec):
+    out = set()
+    for item in spec.split(","):
+        item = item.strip()
+        if item and item != "none":
+            v, h = item.split("x")
+            out.add((int(v), int(h)))
+    return out
 
 
-def _vocab_sized(a, w):
-    return _VOCAB_MIN > 0 and (w.shape[0] >= _VOCAB_MIN or a.shape[-1] >= _VOCAB_MIN)
+_VOCAB_MEASURED = _parse_shapes(os.environ.get("APEX_GEMM_VOCAB_TABLE", "30528x1024"))
+
+
+def _vocab_sized(w):
+    return tuple(w.shape) in _VOCAB_MEASURED
 
 
 def _C():
@@ -80,10 +93,11 @@ def mode() -> str:
     return _MODE
 
 
-def use_mfma(a, w, fused=True) -> bool:
-    """MFMA kernel for this call? ``fused``: the call carries an epilogue the library lacks."""
-    if _MODE == "blas" or not a.is_cuda or (_MODE == "auto" and not fused and _PLAIN != "own"
-                                            and not _vocab_sized(a, w)):
+def use_mfma(a, w, fused=True, vocab=None) -> bool:
+    """MFMA kernel for this call? ``fused``: the call carries an epilogue the library lacks;
+    ``vocab``: the (untransposed) weight is a measured vocabulary projection (default: look at w)."""
+    vocab = _vocab_sized(w) if vocab is None else vocab
+    if _MODE == "blas" or not a.is_cuda or (_MODE == "auto" and not fused and _PLAIN != "own" and not vocab):
         return False
     return _C().gemm_supported(a, w)
 
@@ -188,9 +202,10 @@ def dgrad(dy, w, wT=None, f8=None):
         r = f8.backward_gemm(a, w, _C().EPI_NONE)
         if r is not None:
             return r[0].view(*dy.shape[:-1], w.shape[1])
-    if (_MODE == "mfma" or (_MODE == "auto" and (_PLAIN == "own" or _vocab_sized(a, w)))) and a.is_cuda:
+    vocab = _vocab_sized(w)
+    if (_MODE == "mfma" or (_MODE == "auto" and (_PLAIN == "own" or vocab))) and a.is_cuda:
         wT = transpose(w) if wT is None else wT
-        if use_mfma(a, wT, fused=False):
+        if use_mfma(a, wT, fused=False, vocab=vocab):
             C = _C()
             out, _ = C.gemm(a, wT, C.EPI_NONE)
             return out.view(*dy.shape[:-1], w.shape[1])

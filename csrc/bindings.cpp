@@ -1534,6 +1534,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bias") = py::none(), py::arg("q8_out") = py::none(), py::arg("q8_scale") = py::none(),
         py::arg("q8_amax") = py::none(), py::arg("q8_fmt") = 0);
   m.def("gemm_set_dbg", [](int64_t v) { check(apex::gemm_set_dbg((int)v), "gemm_set_dbg"); });
+  // which = 0: 16-bit persistent GEMM, 1: fp8 persistent GEMM; v = 1 / 0 forces it on / off, -1 restores
+  // the APEX_GEMM_PERSIST(_F8) choice; returns the previous forced value
+  m.def("set_gemm_persist", [](int64_t which, int64_t v) { return (int64_t)apex::gemm_set_persist((int)which, (int)v); },
+        py::arg("which"), py::arg("v"));
   m.def("flash_attn_bwd", &flash_attn_bwd, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"),
         py::arg("o"), py::arg("lse"), py::arg("dq"), py::arg("dk"), py::arg("dv"), py::arg("causal"),
         py::arg("scale"), py::arg("p_drop"), py::arg("seed"), py::arg("offset"), py::arg("k_lens"),

@@ -296,6 +296,7 @@ int fp8_quantize_weights(const WqDesc* d, int nd, int64_t ablocks, int64_t qbloc
 int fp8_update_scales(float* hist, float* amax_cur, float* scale, float* scale_inv, const float* fmt_max,
                       int n_slots, int hist_len, int idx, float margin_scale, hipStream_t s);
 int gemm_set_dbg(int v);  // diagnostics: 2 = skip the epilogue
+int gemm_set_persist(int which, int v);  // force the persistent GEMM on / off (tests); returns the previous value
 // weight-gradient form: C[P, Q] = A^T B with A [R, P], B [R, Q] row-major (contraction over rows)
 bool gemm_tt_supported(int P, int Q, int R, int splits, int64_t lda, int64_t ldb);
 int gemm_tt(const GemmArgs& g, int dt, hipStream_t s);

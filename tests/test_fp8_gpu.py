@@ -140,9 +140,19 @@ def _tanh_gelu(h):
 
 
 @pytest.mark.parametrize("epi", ["bias", "resid", "gelu", "dgelu", "gelu_d", "gelu_tanh_d", "mul"])
-@pytest.mark.parametrize("M,N,K", [(320, 512, 768), (4608, 4096, 256)])  # (the second: 288 tiles, persistent)
-def test_gemm_f8_epilogues(epi, M, N, K):
+@pytest.mark.parametrize("M,N,K,persist", [(320, 512, 768, 0), (4608, 4096, 256, 0), (4608, 4096, 256, 1)])
+def test_gemm_f8_epilogues(epi, M, N, K, persist):
+    """(4608, 4096): 288 full tiles, more than the CUs — with persist = 1 the fp8 persistent kernel
+    (off by default, forced on here through C.set_gemm_persist(1, 1)), with 0 the one-tile kernel."""
     C = _C()
+    prev = C.set_gemm_persist(1, persist)
+    try:
+        _f8_epilogue_case(C, epi, M, N, K)
+    finally:
+        C.set_gemm_persist(1, prev)
+
+
+def _f8_epilogue_case(C, epi, M, N, K):
     a8, b8, ia, ib, af, bf = _operands(M, N, K, 0, seed=3)
     acc = af @ bf.t()
     bias = (torch.randn(N, device=DEV) * 0.1).bfloat16()
@@ -272,6 +282,8 @@ def test_blocks_fp8_track_bf16(fp8_off):
         y8, g8 = run()
     st = fp8.state()
     assert st.n >= 4 * 3 - 1, st.slots  # four weights: w, x, dy slots each (the first layer's dy too)
+    if st.wgrad_enabled():  # the four weight gradients ran on the fp8 kernel, not the bf16 fallback
+        assert st.wgrad_calls == 4, st.wgrad_calls
     assert _rel(y8, y_ref) < 0.06
     for i, (a, b) in enumerate(zip(g8, g_ref)):
         assert _rel(a, b) < 0.15, (i, _rel(a, b))

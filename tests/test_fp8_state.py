@@ -195,21 +195,29 @@ def test_wgrad_split_policy():
 
 def test_operand_codes_match_the_consumed_tensor():
     """operand_codes hands back the last fp8 GEMM's codes only for the tensor that GEMM consumed
-    (same storage and shape), once; a mismatch or a second call gets None."""
+    (same bytes: address + shape of the held operand, unmodified since), once; a mismatch, an
+    in-place write in between, a declined GEMM or a second call gets None."""
     st = fp8.Fp8State(device="cpu")
     a = torch.zeros(4, 8)
     codes, inv = torch.zeros(4, 8, dtype=torch.uint8), torch.ones(1)
-    st._last = (a.data_ptr(), tuple(a.shape), codes, inv)
+    st._last = st._remember(a, codes, inv)
     assert st.operand_codes(torch.zeros(4, 8)) is None  # another tensor
-    st._last = (a.data_ptr(), tuple(a.shape), codes, inv)
+    st._last = st._remember(a, codes, inv)
     assert st.operand_codes(a.view(8, 4)) is None  # same storage, other shape
-    st._last = (a.data_ptr(), tuple(a.shape), codes, inv)
-    got = st.operand_codes(a)
+    st._last = st._remember(a, codes, inv)
+    got = st.operand_codes(a.view(4, 8))  # a fresh view of the same bytes (what the blocks pass)
     assert got[0] is codes and got[1] is inv
     assert st.operand_codes(a) is None  # taken
-    st._last = (a.data_ptr(), tuple(a.shape), codes, inv)
+    st._last = st._remember(a, codes, inv)
+    a.add_(1)  # written in place after its codes were taken: stale codes
+    assert st.operand_codes(a) is None
+    st._last = st._remember(a, codes, inv)
     st.step()
     assert st.operand_codes(a) is None  # a step boundary drops it
+    # a GEMM the fp8 path declines clears the claim (a later tensor reusing the address gets nothing)
+    st._last = st._remember(a, codes, inv)
+    assert st.forward_gemm(torch.zeros(4, 100), torch.zeros(8, 100), 0) is None
+    assert st._last is None
 
 
 def test_wgrad_declines_without_recipe_or_codes():

@@ -101,3 +101,36 @@ def test_gamma_zero_written_between_steps_is_seen():
         ps[4][7] = 1.0
     y = _run("ffn", x, ps)
     assert y.grad_fn.saved_tensors[-1] is None
+
+
+def test_gamma_check_one_host_read_per_step_with_accumulation():
+    """4 accumulated micro-batches per FusedLAMB step through both sublayer kinds: the gamma-zero
+    check reads the device once per optimizer step (the step hook marks it dirty, backward does not
+    once an optimizer step has been seen), and a zero the optimizer writes into a gamma (raw-pointer
+    kernel, no version bump) is seen at the next step's first forward, which then keeps the LN input."""
+    from apex.ops import blocks
+    from apex.optimizers import FusedLAMB
+
+    if not blocks._LN_MEM:
+        pytest.skip("APEX_LN_MEM=0")
+    dt, E = torch.bfloat16, 1024
+    pa, pf = _params("attn", E, dt, False), _params("ffn", E, dt, False)
+    opt = FusedLAMB(pa + pf, lr=1e-4)
+    x = torch.randn(2, 128, E, device=DEV).to(dt)
+    gz = blocks._GZ
+    reads = []
+    for step in range(3):
+        r0 = gz.host_reads
+        for micro in range(4):
+            y = _run("ffn", _run("attn", x, pa), pf)
+            y.float().square().mean().backward()
+        reads.append(gz.host_reads - r0)
+        opt.step()
+        opt.zero_grad()
+    assert reads[1:] == [1, 1], reads  # (step 0 may re-check before the first step hook fires)
+    # a zero written by the optimizer's kernel: seen by the next forward
+    pf[4].data[7] = 0  # .data write: no version bump, like a fused-kernel write
+    dummy = torch.nn.Parameter(torch.zeros(1, device=DEV))
+    torch.optim.SGD([dummy], lr=0.0).step()  # any optimizer's step fires the global hook
+    y = _run("ffn", x, pf)
+    assert y.grad_fn.saved_tensors[-1] is not None  # the zero-gamma fallback input is kept

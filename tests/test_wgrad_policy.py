@@ -1,5 +1,7 @@
 """Weight-gradient routing (apex.ops.fused): which shapes go to the transposed-read MFMA kernel
 (_wgrad_tt_splits) and how the library split-K slices (_wgrad_splits) are chosen. Pure host logic."""
+import torch
+
 from apex.ops import fused
 
 
@@ -62,3 +64,16 @@ def test_vocab_sized_weight_gradients_take_the_kernel(monkeypatch):
     assert fused._wgrad_tt_splits(14590, 30528, 1024) == 0  # tokens not a multiple of 64
     monkeypatch.setattr(fused, "_WGRAD_TT_VOCAB", False)
     assert fused._wgrad_tt_splits(14592, 30528, 1024) == 0
+
+
+def test_vocab_routing_is_keyed_on_measured_weight_shapes(monkeypatch):
+    """Plain forward / input-gradient products go to the MFMA kernel only for the measured
+    vocabulary projections (weight shape), never for an unmeasured wide layer (16384-wide FFN)."""
+    from apex.ops import gemm as G
+
+    assert G._vocab_sized(torch.empty(30528, 1024))  # BERT-Large MLM decoder
+    assert not G._vocab_sized(torch.empty(16384, 4096))  # FFN1 of a hidden-4096 model
+    assert not G._vocab_sized(torch.empty(4096, 16384))  # its FFN2
+    assert not G._vocab_sized(torch.empty(50304, 1600))  # GPT-2 LM head: measured neutral
+    assert G._parse_shapes("none") == set()
+    assert G._parse_shapes("50304x1600, 30528x1024") == {(50304, 1600), (30528, 1024)}

@@ -5,6 +5,7 @@
 //   build/gemmlab M N K [epi=0] [rounds=5] [reps=10]
 // Prints one JSON line per variant: us per call (min / median over rounds), PF/s, max |diff|.
 #include "../../csrc/gemm.hip"
+#include "lab_variants.h"
 
 #include <hip/hip_runtime.h>
 
