@@ -646,7 +646,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
   // on distinct bank pairs), the dQ product reads it back with ds_read_b64_tr_b16. Round 3 wrote
   // [q][key] with 16 ds_write_b16 per lane and step.
   constexpr int LDT = kBwdBQ + 4;
-  constexpr int KT_LD = kBwdBK + 8;  // K^T row stride (elements); K^T shares lds_k
+  // K^T row stride (elements); K^T shares lds_k. 144: the dQ product's 16-byte K^T row reads are
+  // conflict-free (136: 2-way; tools/lds_banks.py)
+  constexpr int KT_LD = kBwdBK + 16;
   constexpr int LDSK = D * KT_LD > kBwdBK * LDR ? D * KT_LD : kBwdBK * LDR;
   __shared__ __attribute__((aligned(16))) T lds_q[kBwdBQ * LDQ];
   __shared__ __attribute__((aligned(16))) T lds_do[kBwdBQ * LDQ];
@@ -759,17 +761,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
       vf[s] = V8{};
     }
   }
-  // whole K block to LDS transposed, K^T [D][kBwdBK + 8] (the A operand of dQ^T = K^T . dS^T,
-  // read as 16-byte rows); written once per workgroup
-  if (DQ)
-  for (int idx = threadIdx.x; idx < kBwdBK * (D / 8); idx += 256) {
-    const int row = idx / (D / 8), col = (idx % (D / 8)) * 8;
-    const int key = k0 + row;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (key < Sk) v = *(const uint4*)(kp + (int64_t)key * a.k_ss + col);
-    const T* e = (const T*)&v;
+  // whole K block to LDS transposed, K^T [D][KT_LD] (the A operand of dQ^T = K^T . dS^T, read as
+  // 16-byte rows), written once per workgroup from the K rows just loaded as B operands (kf: key
+  // mykey, dims 16s + 8hl .. +7; zero past Sk): each 2-byte store instruction writes one dim row, 32
+  // consecutive keys per half-wave — conflict-free, and no second global read of K. (Round 5 staged
+  // it from a fresh 16-byte-per-lane load of K with 8 dims x 8 keys per half-wave: 8-way conflicts,
+  // half of the kernel's conflict cycles; a conflict-free re-load needed strided global loads.)
+  if constexpr (DQ) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) lds_k[(col + j) * KT_LD + row] = e[j];
+    for (int s = 0; s < D / 16; ++s) {
+      const T* e = (const T*)&kf[s];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) lds_k[(16 * s + 8 * hl + j) * KT_LD + 32 * wid + r] = e[j];
+    }
   }
   };
   // D <= 64: the K/V loads are issued after the first query-block fetch, so both latencies

@@ -664,14 +664,19 @@ struct NoHook {
 // With HALVES the epilogue's own loads (bias, [M, N] input) are asm loads issued BEFORE `pre()` (the
 // caller's hook: the next tile's LDS-DMA pieces, exactly 8 per wave) and retired by counted waits that
 // leave those pieces (and this epilogue's stores) in flight.
+// XD (lab diagnostics, tools/gemmlab; production 0): bit 0 skips the epilogue math (the stored values
+// are the rounded accumulators, same loads and stores), bit 1 skips every global store of the epilogue
 template <typename T, int EPI, bool EDGE, int J0 = 0, int NJ = 4, bool STAGED = false, int Q8 = 0,
-          bool HALVES = false, typename Hook = NoHook>
+          bool HALVES = false, typename Hook = NoHook, int XD = 0>
 __device__ __forceinline__ void epilogue(const f32x4 (&acc)[NJ][8], char* reg, T* __restrict__ C, int M, int N,
                                          int64_t ldc, const T* __restrict__ bias, const T* __restrict__ aux,
                                          int64_t ldaux, T* __restrict__ aux_out, float* __restrict__ part, int m0,
                                          int n0, int tm, int wr, int wc, int lane, float alpha = 1.f,
                                          const Q8Out& q8 = Q8Out{}, const Hook& pre = Hook{},
-                                         float* q8_defer = nullptr) {
+                                         float* q8_defer = nullptr, const T* __restrict__ aux_next = nullptr) {
+  // aux_next (HALVES with an [M, N] input): the NEXT tile's input tile, whose 1024 128-byte lines are
+  // touched here (two dword loads per lane, retired with this tile's first input half) so that tile's
+  // epilogue loads hit the Infinity Cache instead of waiting on HBM misses
   // HALVES + Q8: the codes of the multiply / dGELU epilogues are stashed and emitted per half, and the
   // running max|C| goes to *q8_defer (the persistent kernel issues one amax atomic per workgroup at its
   // end: an atomic here would sit between the next tile's LDS-DMA pieces and their counted wait)
@@ -756,7 +761,11 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[NJ][8], char* reg, T
     // a buffer_store_dwordx4 right after issue and corrupted a dword of the stored row (seen on
     // the GPU: sporadic dwords of EPI_BIAS_GELU's pre-activation output)
     auto st = [&](const __amdgpu_buffer_rsrc_t& rs, int slot, const u32x4& x) {
-      __builtin_amdgcn_raw_buffer_store_b128(x, rs, voff(ldc, slot) + (uint32_t)soff(ldc, slot), 0, 0);
+      if constexpr (XD & 2) {  // no store: keep the value live
+        asm volatile("" ::"v"(x));
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b128(x, rs, voff(ldc, slot) + (uint32_t)soff(ldc, slot), 0, 0);
+      }
     };
     // first half of the input operand in flight (sched_barriers pin the phase order: left alone,
     // the scheduler hoists both halves' loads above the transposition and spills around them)
@@ -767,13 +776,23 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[NJ][8], char* reg, T
     if constexpr (HALVES) {
       if constexpr (AUX_IN) {
         rsx_s = sgpr_rsrc(aux + (int64_t)wrow0 * ldaux + wcol0, (uint32_t)(128 * ldaux * (int64_t)sizeof(T)));
+        uint32_t pf0 = 0u, pf1 = 0u;
+        if (aux_next) {
+          // line l = thread + 512 j of the next 256 x 256 tile: row l / 4, 64-element segment l % 4
+          const int t = (wr * 4 + wc) * 64 + lane;
+          const T* p0 = aux_next + (int64_t)(t >> 2) * ldaux + (t & 3) * 64;
+          const T* p1 = p0 + 128 * ldaux;
+          asm volatile("global_load_dword %0, %1, off" : "=v"(pf0) : "v"(p0) : "memory");
+          asm volatile("global_load_dword %0, %1, off" : "=v"(pf1) : "v"(p1) : "memory");
+        }
 #pragma unroll
         for (int it = 0; it < 8; ++it) ra[it] = asm_load16(rsx_s, voff(ldaux, it), soff(ldaux, it));
         pre();
         __builtin_amdgcn_sched_barrier(0);
         stage_acc<T, J0, NJ, 0, 4>(acc, reg, lane, alpha);
         __builtin_amdgcn_sched_barrier(0);
-        asm_wait<8>(ra);  // the 8 pieces of pre() are younger
+        asm_wait<8>(ra);  // the 8 pieces of pre() are younger (the two line touches are older: retired too)
+        asm volatile("" ::"v"(pf0), "v"(pf1));  // their registers stay reserved until the data has landed
       } else {
         if constexpr (HAS_BIAS) braw = asm_load16(sgpr_rsrc(bias + n0 + wc * 64, 128), (uint32_t)((lane & 7) * 16), 0);
         pre();
@@ -836,7 +855,10 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[NJ][8], char* reg, T
       for (int it = 0; it < 8; ++it) {
         const int slot = 8 * h + it;
         u32x4 out = rc[it];
-        if constexpr (EPI != EPI_NONE) {
+        if constexpr ((XD & 1) && EPI != EPI_NONE) {  // same bytes, no math
+          if constexpr (GELU_D) st(rs_o, slot, out);
+          if constexpr (AUX_IN) out = out ^ (h == 0 ? ra[it] : rb[it]);
+        } else if constexpr (EPI != EPI_NONE) {
           float v[8];
           unpack(rc[it], v);
           if constexpr (EPI == EPI_BIAS) {
@@ -950,7 +972,7 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[NJ][8], char* reg, T
         csum[e] = x;
       }
       // waves wc = 0..3 of one wr cover disjoint columns: one partial row per (tile, wr)
-      if (lane < 8 && ncol < N) {
+      if (!(XD & 2) && lane < 8 && ncol < N) {
         float* pp = part + (int64_t)(tm * 2 + wr) * N + ncol;
         *reinterpret_cast<f32x4*>(pp) = f32x4{csum[0], csum[1], csum[2], csum[3]};
         *reinterpret_cast<f32x4*>(pp + 4) = f32x4{csum[4], csum[5], csum[6], csum[7]};
@@ -1231,6 +1253,16 @@ __global__ void __launch_bounds__(G_THREADS) gemm_persist_kernel(const TI* __res
   }
   int m0, n0, tm;
   tile_coords(v, tiles_m, tiles_n, m0, n0, tm);
+  // epilogues with an [M, N] input: the first tile's input lines touched now (each later tile's by the
+  // epilogue before it, see epilogue() aux_next), retired by the prologue's wait below
+  constexpr bool AUX_IN = EPI == EPI_RESID || EPI == EPI_MUL || EPI == EPI_DGELU || EPI == EPI_DGELU_TANH;
+  uint32_t pf0 = 0u, pf1 = 0u;
+  if constexpr (AUX_IN && !(DBG & 16384)) {
+    const T* p0 = aux + (int64_t)(m0 + (tid >> 2)) * ldaux + n0 + (tid & 3) * 64;
+    const T* p1 = p0 + 128 * ldaux;
+    asm volatile("global_load_dword %0, %1, off" : "=v"(pf0) : "v"(p0) : "memory");
+    asm volatile("global_load_dword %0, %1, off" : "=v"(pf1) : "v"(p1) : "memory");
+  }
   // first tile's prologue (mainloop_bal's): A(0), B(0) -> buffer 0, B(1) -> buffer 1
   stage_pieces<TI, false>(A, lda, m0, M, 0, smem, wid, lane, 0);
   stage_pieces<TI, false>(A, lda, m0, M, 0, smem, wid, lane, 2);
@@ -1243,6 +1275,7 @@ __global__ void __launch_bounds__(G_THREADS) gemm_persist_kernel(const TI* __res
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
+  asm volatile("" ::"v"(pf0), "v"(pf1));  // (the line touches are older than B(1): retired above)
   bar();
   for (;;) {
     uint64_t tr0 = 0, tr1 = 0;
@@ -1296,9 +1329,10 @@ __global__ void __launch_bounds__(G_THREADS) gemm_persist_kernel(const TI* __res
     };
     __builtin_amdgcn_sched_barrier(0);
     float q8w = 0.f;
-    epilogue<T, EPI, false, 0, 4, false, Q8, true>(acc, smem + G_BUF_BYTES + wid * 8192, C, M, N, ldc, bias, aux,
+    epilogue<T, EPI, false, 0, 4, false, Q8, true, decltype(next_k0), (DBG >> 12) & 3>(acc, smem + G_BUF_BYTES + wid * 8192, C, M, N, ldc, bias, aux,
                                                     ldaux, aux_out, part, m0, n0, tm, wr, wc, lane_e, alpha, q8,
-                                                    next_k0, &q8w);
+                                                    next_k0, &q8w,
+                                                    (more && aux && !(DBG & 16384)) ? aux + (int64_t)m1 * ldaux + n1 : nullptr);
     if constexpr (Q8 != 0) {
       const float m = f8_wave_max(q8w);
       if (lane_e == 0) q8red[wid] = fmaxf(q8red[wid], m);
@@ -1324,9 +1358,9 @@ __global__ void __launch_bounds__(G_THREADS) gemm_persist_kernel(const TI* __res
     if (nt > 1) {
       stage_pieces<TI, false>(B, ldb, n1, N, BKE, smem + G_BUF_BYTES + G_TILE_BYTES, wid, lane_e, 0);
       stage_pieces<TI, false>(B, ldb, n1, N, BKE, smem + G_BUF_BYTES + G_TILE_BYTES, wid, lane_e, 2);
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(epi_stores<EPI, Q8>() + 4) : "memory");
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(((DBG >> 12) & 2 ? 0 : epi_stores<EPI, Q8>()) + 4) : "memory");
     } else {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(epi_stores<EPI, Q8>()) : "memory");
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((DBG >> 12) & 2 ? 0 : epi_stores<EPI, Q8>()) : "memory");
     }
     bar();  // A(0), B(0) of the next tile visible to every wave
     v = vn;

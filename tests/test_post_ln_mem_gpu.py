@@ -79,8 +79,11 @@ def test_sublayer_mem_mode_saves_no_input_and_matches_fp32(kind, zero):
 
 
 def test_gamma_zero_written_between_steps_is_seen():
-    """A gamma zeroed in place after a backward (as an optimizer step would) turns the fallback on at the
-    next forward; restoring it turns it off again."""
+    """A gamma zeroed in place by a raw write (no version bump) as part of an optimizer step turns the
+    fallback on at the next forward; restoring it turns it off again. The check is re-armed by the
+    global optimizer-step hook (apex.ops.blocks._GammaZeroCheck), so the write is followed by a step
+    here — earlier tests in the process have run optimizer steps, after which a backward alone no
+    longer re-arms it (one host read per step under gradient accumulation)."""
     from apex.ops import blocks
 
     if not blocks._LN_MEM:
@@ -92,7 +95,8 @@ def test_gamma_zero_written_between_steps_is_seen():
     assert y.grad_fn.saved_tensors[-1] is None
     y.sum().backward()
     with torch.no_grad():
-        ps[4].data[7] = 0  # raw write (no version bump), after a backward: the check must still see it
+        ps[4].data[7] = 0  # raw write (no version bump), as an optimizer kernel writes through its pointer
+    torch.optim.SGD([ps[4]], lr=0.0).step()  # the step post-hook re-arms the check
     y = _run("ffn", x, ps)
     assert y.grad_fn.saved_tensors[-1] is not None
     y.sum().backward()

@@ -230,6 +230,12 @@ void run_epi(Bufs& b, int rounds, int reps, hipStream_t s) {
     trace_summary(b, EPI, s, launch_persist<EPI, 2048>);
   }
   if (full && !getenv("LAB_NOPERSIST")) vs.push_back({"w8pers", launch_persist<EPI>});
+  if (full && getenv("LAB_PXD")) {  // persistent-kernel epilogue diagnostics (epilogue XD bits)
+    vs.push_back({"pers_nomath", launch_persist<EPI, 4096>});
+    vs.push_back({"pers_nostore", launch_persist<EPI, 8192>});
+    vs.push_back({"pers_nomath_nostore", launch_persist<EPI, 12288>});
+  }
+  if (full && getenv("LAB_PF")) vs.push_back({"pers_nopf", launch_persist<EPI, 16384>});  // no input-line touches
   const int64_t MN = (int64_t)b.M * b.N;
   float* dmax;
   CK(hipMalloc(&dmax, 4));
