@@ -673,10 +673,7 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[NJ][8], char* reg, T
                                          int64_t ldaux, T* __restrict__ aux_out, float* __restrict__ part, int m0,
                                          int n0, int tm, int wr, int wc, int lane, float alpha = 1.f,
                                          const Q8Out& q8 = Q8Out{}, const Hook& pre = Hook{},
-                                         float* q8_defer = nullptr, const T* __restrict__ aux_next = nullptr) {
-  // aux_next (HALVES with an [M, N] input): the NEXT tile's input tile, whose 1024 128-byte lines are
-  // touched here (two dword loads per lane, retired with this tile's first input half) so that tile's
-  // epilogue loads hit the Infinity Cache instead of waiting on HBM misses
+                                         float* q8_defer = nullptr) {
   // HALVES + Q8: the codes of the multiply / dGELU epilogues are stashed and emitted per half, and the
   // running max|C| goes to *q8_defer (the persistent kernel issues one amax atomic per workgroup at its
   // end: an atomic here would sit between the next tile's LDS-DMA pieces and their counted wait)
@@ -776,23 +773,13 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[NJ][8], char* reg, T
     if constexpr (HALVES) {
       if constexpr (AUX_IN) {
         rsx_s = sgpr_rsrc(aux + (int64_t)wrow0 * ldaux + wcol0, (uint32_t)(128 * ldaux * (int64_t)sizeof(T)));
-        uint32_t pf0 = 0u, pf1 = 0u;
-        if (aux_next) {
-          // line l = thread + 512 j of the next 256 x 256 tile: row l / 4, 64-element segment l % 4
-          const int t = (wr * 4 + wc) * 64 + lane;
-          const T* p0 = aux_next + (int64_t)(t >> 2) * ldaux + (t & 3) * 64;
-          const T* p1 = p0 + 128 * ldaux;
-          asm volatile("global_load_dword %0, %1, off" : "=v"(pf0) : "v"(p0) : "memory");
-          asm volatile("global_load_dword %0, %1, off" : "=v"(pf1) : "v"(p1) : "memory");
-        }
 #pragma unroll
         for (int it = 0; it < 8; ++it) ra[it] = asm_load16(rsx_s, voff(ldaux, it), soff(ldaux, it));
         pre();
         __builtin_amdgcn_sched_barrier(0);
         stage_acc<T, J0, NJ, 0, 4>(acc, reg, lane, alpha);
         __builtin_amdgcn_sched_barrier(0);
-        asm_wait<8>(ra);  // the 8 pieces of pre() are younger (the two line touches are older: retired too)
-        asm volatile("" ::"v"(pf0), "v"(pf1));  // their registers stay reserved until the data has landed
+        asm_wait<8>(ra);  // the 8 pieces of pre() are younger
       } else {
         if constexpr (HAS_BIAS) braw = asm_load16(sgpr_rsrc(bias + n0 + wc * 64, 128), (uint32_t)((lane & 7) * 16), 0);
         pre();
@@ -1253,16 +1240,6 @@ __global__ void __launch_bounds__(G_THREADS) gemm_persist_kernel(const TI* __res
   }
   int m0, n0, tm;
   tile_coords(v, tiles_m, tiles_n, m0, n0, tm);
-  // epilogues with an [M, N] input: the first tile's input lines touched now (each later tile's by the
-  // epilogue before it, see epilogue() aux_next), retired by the prologue's wait below
-  constexpr bool AUX_IN = EPI == EPI_RESID || EPI == EPI_MUL || EPI == EPI_DGELU || EPI == EPI_DGELU_TANH;
-  uint32_t pf0 = 0u, pf1 = 0u;
-  if constexpr (AUX_IN && !(DBG & 16384)) {
-    const T* p0 = aux + (int64_t)(m0 + (tid >> 2)) * ldaux + n0 + (tid & 3) * 64;
-    const T* p1 = p0 + 128 * ldaux;
-    asm volatile("global_load_dword %0, %1, off" : "=v"(pf0) : "v"(p0) : "memory");
-    asm volatile("global_load_dword %0, %1, off" : "=v"(pf1) : "v"(p1) : "memory");
-  }
   // first tile's prologue (mainloop_bal's): A(0), B(0) -> buffer 0, B(1) -> buffer 1
   stage_pieces<TI, false>(A, lda, m0, M, 0, smem, wid, lane, 0);
   stage_pieces<TI, false>(A, lda, m0, M, 0, smem, wid, lane, 2);
@@ -1275,7 +1252,6 @@ __global__ void __launch_bounds__(G_THREADS) gemm_persist_kernel(const TI* __res
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
-  asm volatile("" ::"v"(pf0), "v"(pf1));  // (the line touches are older than B(1): retired above)
   bar();
   for (;;) {
     uint64_t tr0 = 0, tr1 = 0;
@@ -1331,8 +1307,7 @@ __global__ void __launch_bounds__(G_THREADS) gemm_persist_kernel(const TI* __res
     float q8w = 0.f;
     epilogue<T, EPI, false, 0, 4, false, Q8, true, decltype(next_k0), (DBG >> 12) & 3>(acc, smem + G_BUF_BYTES + wid * 8192, C, M, N, ldc, bias, aux,
                                                     ldaux, aux_out, part, m0, n0, tm, wr, wc, lane_e, alpha, q8,
-                                                    next_k0, &q8w,
-                                                    (more && aux && !(DBG & 16384)) ? aux + (int64_t)m1 * ldaux + n1 : nullptr);
+                                                    next_k0, &q8w);
     if constexpr (Q8 != 0) {
       const float m = f8_wave_max(q8w);
       if (lane_e == 0) q8red[wid] = fmaxf(q8red[wid], m);

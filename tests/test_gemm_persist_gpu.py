@@ -58,8 +58,10 @@ def _cus():
 # (M, N, K): tiles = M/256 * N/256, all > 256 (the CU count) so the launcher takes the persistent
 # kernel; the first is 288 tiles (just over one round), the second 768 (three tiles per workgroup,
 # BERT's attention-out / residual width and K), the third 297 tiles with K = one K-tile (the
-# prologue's nt == 1 branch and the stores-only counted wait)
-SHAPES = [(4608, 4096, 256), (49152, 1024, 1024), (8448, 2304, 64)]
+# prologue's nt == 1 branch and the stores-only counted wait); K = 128 and 192 (two and three K-tiles)
+# cover the later tiles' K-tile 0/1 pair whose A(1) / B(1) the previous epilogue issued between its
+# halves' stores (the nt == 2 waits, and an odd tail after that pair)
+SHAPES = [(4608, 4096, 256), (49152, 1024, 1024), (8448, 2304, 64), (4608, 4096, 128), (8448, 2304, 192)]
 
 
 def _tiles(M, N):

@@ -235,7 +235,6 @@ void run_epi(Bufs& b, int rounds, int reps, hipStream_t s) {
     vs.push_back({"pers_nostore", launch_persist<EPI, 8192>});
     vs.push_back({"pers_nomath_nostore", launch_persist<EPI, 12288>});
   }
-  if (full && getenv("LAB_PF")) vs.push_back({"pers_nopf", launch_persist<EPI, 16384>});  // no input-line touches
   const int64_t MN = (int64_t)b.M * b.N;
   float* dmax;
   CK(hipMalloc(&dmax, 4));
