@@ -645,7 +645,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
   // consecutive queries each; row stride 36 elements = 18 dwords: the 16 rows of a lane group land
   // on distinct bank pairs), the dQ product reads it back with ds_read_b64_tr_b16. Round 3 wrote
   // [q][key] with 16 ds_write_b16 per lane and step.
-  constexpr int LDT = kBwdBQ + 4;
+  // D = 64: dS^T unpadded, 8-byte piece c of key row k at c ^ ((k >> 1) & 7): the ds_write_b64 stores
+  // and the dQ product's transposed reads both conflict-free (tools/lds_banks.py; 36: reads 2-way)
+#ifndef APEX_ATT_DS_SWZ
+#define APEX_ATT_DS_SWZ 1
+#endif
+  constexpr bool DSW = D == 64 && APEX_ATT_DS_SWZ;
+  constexpr int LDT = DSW ? kBwdBQ : kBwdBQ + 4;
+  auto dso = [](int row, int col) -> int {
+    if constexpr (DSW) return row * LDT + (col ^ (((row >> 1) & 7) << 2));
+    else return row * LDT + col;
+  };
   // K^T row stride (elements); K^T shares lds_k. 144: the dQ product's 16-byte K^T row reads are
   // conflict-free (136: 2-way; tools/lds_banks.py)
   constexpr int KT_LD = kBwdBK + 16;
@@ -946,7 +956,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
       t4 w;
 #pragma unroll
       for (int e = 0; e < 4; ++e) w[e] = (T)ds[4 * g4 + e];  // queries 8 g4 + 4 hl + e
-      *(t4*)(lds_ds + (32 * wid + r) * LDT + 8 * g4 + 4 * hl) = w;
+      *(t4*)(lds_ds + dso(32 * wid + r, 8 * g4 + 4 * hl)) = w;
     }
     lds_barrier();
     // dQ^T [D x 32 q] = K^T . dS^T on 16x16x32 MFMAs over the full 128-key contraction: wave
@@ -964,8 +974,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
       for (int kk = 0; kk < kBwdBK; kk += 32) {
         // B = dS [8 keys x 16 queries]: two transposed 4-key blocks of dS^T (lane 4q'+p of the
         // group addresses key row kk + 8 lg + q', queries 16 qt + 4p; lane lq receives query 16 qt + lq)
-        const T* tb = lds_ds + (kk + 8 * lg + ((lane & 15) >> 2)) * LDT + 16 * qt + 4 * (lane & 3);
-        const V8 bb = join4<V8>(lds_tr16(tb), lds_tr16(tb + 4 * LDT));
+        const int dr = kk + 8 * lg + ((lane & 15) >> 2), dc = 16 * qt + 4 * (lane & 3);
+        const V8 bb = join4<V8>(lds_tr16(lds_ds + dso(dr, dc)), lds_tr16(lds_ds + dso(dr + 4, dc)));
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
           const V8 aa = *(const V8*)(lds_k + ((dt0 + t) * 16 + lq) * KT_LD + kk + 8 * lg);
