@@ -96,7 +96,7 @@ def _wgrad_tt_splits(M, N, K):
         return 0
     if _WGRAD_TT not in ("auto", ""):
         s = int(_WGRAD_TT)
-        return s if M % (64 * s) == 0 else 0
+        return s if M % 64 == 0 and M // 64 >= s else 0
     if _WGRAD_TT_VOCAB and max(N, K) >= 16384 and M % 64 == 0:
         # vocabulary-sized weights (an MLM decoder / LM head tied to the embedding): hundreds of
         # output tiles, one slice (profiles/r5_vocab_wgrad_tt_ab.jsonl: the MLM decoder wgrad 964 -> 795 us)
@@ -104,7 +104,7 @@ def _wgrad_tt_splits(M, N, K):
     hit = _WGRAD_TT_MEASURED.get((N, K))
     if hit is not None:
         m_min, s = hit
-        return s if M >= m_min and M % (64 * s) == 0 else 0
+        return s if M >= m_min and M % 64 == 0 and M // 64 >= s else 0
     if N % 256 or K % 256:
         return 0  # partial tiles run on the kernel (forced counts above); auto keeps measured shapes only
     tiles = (N // 256) * (K // 256)

@@ -1384,7 +1384,7 @@ Tensor k_gemm_tt(Tensor a, Tensor b, int64_t splits, at::ScalarType out_dtype, c
   g.B = b.data_ptr();
   g.M = (int)P;
   g.N = (int)Q;
-  g.K = (int)(R / splits);
+  g.K = (int)R;  // all contraction rows: the kernel cuts them into `splits` slices of whole K-tiles
   g.lda = P;
   g.ldb = Q;
   g.ldc = Q;
@@ -1429,7 +1429,7 @@ Tensor k_gemm_tt_f8(Tensor a, Tensor b, Tensor alpha_a, Tensor alpha_b, int64_t 
   g.B = b.data_ptr();
   g.M = (int)P;
   g.N = (int)Q;
-  g.K = (int)(R / splits);
+  g.K = (int)R;  // all contraction rows: the kernel cuts them into `splits` slices of whole K-tiles
   g.lda = P;
   g.ldb = Q;
   g.ldc = Q;

@@ -1072,9 +1072,17 @@ __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(const TI* __restrict
       for (int i = 0; i < st; ++i) __builtin_amdgcn_s_sleep(127);
     }
   }
-  if constexpr (TR) {  // split-K slice: K-rows [split*K, (split+1)*K) of both operands
-    A += (int64_t)split * K * lda;
-    B += (int64_t)split * K * ldb;
+  if constexpr (TR) {
+    // split-K slice of the transposed-read launches: K = ALL contraction rows, cut into gridDim.y slices
+    // of whole K-tiles, [split * T / S, (split + 1) * T / S) for T K-tiles (the slices differ by at most
+    // one K-tile: any slice count fills the CUs, e.g. BERT's QKV weight gradient, 48 tiles, at 5 slices
+    // = 240 workgroups where 4 gave 192)
+    constexpr int BKT = 128 / (int)sizeof(TI);  // rows per K-tile (64 16-bit, 128 fp8)
+    const int nkt = K / BKT, ns = (int)gridDim.y;
+    const int kb = (int)((int64_t)split * nkt / ns), ke = (int)((int64_t)(split + 1) * nkt / ns);
+    A += (int64_t)kb * BKT * lda;
+    B += (int64_t)kb * BKT * ldb;
+    K = (ke - kb) * BKT;
   }
   // mainloop_bal for the 16-bit kernels; the fp8 instantiations and the edge-tile dGELU / multiply
   // epilogues keep the previous schedule (their epilogues hold more registers: the balanced loop's
@@ -1623,15 +1631,16 @@ int gemm_nt_f8(const GemmArgs& g, int fmt_a, int fmt_b, int out_dt, hipStream_t 
 
 bool gemm_tt_supported(int P, int Q, int R, int splits, int64_t lda, int64_t ldb) {
   // P, Q: any multiple of 8 (partial 256-tiles: clamped staging + bounds-checked epilogues)
-  return P > 0 && Q > 0 && splits > 0 && P % 8 == 0 && Q % 8 == 0 && R % (splits * GB_K) == 0 &&
+  return P > 0 && Q > 0 && splits > 0 && P % 8 == 0 && Q % 8 == 0 && R % GB_K == 0 && R / GB_K >= splits &&
          lda % 8 == 0 && ldb % 8 == 0;
 }
 
 int gemm_tt(const GemmArgs& g, int dt, hipStream_t s) {
-  // C[P=M, Q=N] (+)= sum_r A[r, p] B[r, q]; g.K = contraction rows per split; g.part = fp32 slabs
+  // C[P=M, Q=N] (+)= sum_r A[r, p] B[r, q]; g.K = ALL contraction rows (g.splits slices of whole K-tiles,
+  // sizes within one K-tile of each other); g.part = fp32 slabs
   // [splits, M, N] when g.epi == EPI_F32, the fp32 [M, N] accumulator (+=) when EPI_F32_ACC, else g.C
   // in the operand dtype (splits must be 1 except for EPI_F32)
-  if (!gemm_tt_supported(g.M, g.N, g.K * g.splits, g.splits, g.lda, g.ldb)) return -2;
+  if (!gemm_tt_supported(g.M, g.N, g.K, g.splits, g.lda, g.ldb)) return -2;
   if (g.epi != EPI_F32 && ((g.epi != EPI_NONE && g.epi != EPI_F32_ACC) || g.splits != 1)) return -3;
   if (dt == kBF16Code) {
     if (g.epi == EPI_F32) launch_gemm<bf16, EPI_F32, true>(g, s);
@@ -1649,8 +1658,8 @@ int gemm_tt(const GemmArgs& g, int dt, hipStream_t s) {
 
 bool gemm_tt_f8_supported(int P, int Q, int R, int splits, int64_t lda, int64_t ldb) {
   // fp8 codes: 16-byte chunks of 16 columns (partial 256-tiles clamp to the last full chunk)
-  return P > 0 && Q > 0 && splits > 0 && P % 16 == 0 && Q % 16 == 0 && R % (splits * 128) == 0 && lda % 16 == 0 &&
-         ldb % 16 == 0;
+  return P > 0 && Q > 0 && splits > 0 && P % 16 == 0 && Q % 16 == 0 && R % 128 == 0 && R / 128 >= splits &&
+         lda % 16 == 0 && ldb % 16 == 0;
 }
 
 // fp8 weight gradient: fp32 slabs [splits, P, Q] of alpha_a alpha_b sum_r A[r, p] B[r, q] over the
@@ -1672,7 +1681,7 @@ void launch_gemm_tt_f8(const GemmArgs& g, hipStream_t s) {
 }
 
 int gemm_tt_f8(const GemmArgs& g, int fmt_a, int fmt_b, hipStream_t s) {
-  if (!gemm_tt_f8_supported(g.M, g.N, g.K * g.splits, g.splits, g.lda, g.ldb) || !g.alpha_a || !g.alpha_b ||
+  if (!gemm_tt_f8_supported(g.M, g.N, g.K, g.splits, g.lda, g.ldb) || !g.alpha_a || !g.alpha_b ||
       !g.part)
     return -2;
   if (fmt_a == 1 && fmt_b == 0) launch_gemm_tt_f8<1, 0>(g, s);

@@ -182,10 +182,15 @@ def test_gemm_supported_rejects():
                                           (8192, 1024, 1024, 8), (64, 256, 256, 1), (576, 256, 512, 3),
                                           # partial 256-tiles (GPT-2's 1600 / 4800): clamped staging
                                           (1024, 1600, 480, 2), (512, 200, 264, 1), (2048, 4800, 1600, 4),
-                                          (128, 8, 1608, 1)])
+                                          (128, 8, 1608, 1),
+                                          # slice counts that do not divide the K-tiles (slices of 2-3,
+                                          # 6-7, 9-10 K-tiles; one K-tile each)
+                                          (448, 256, 256, 3), (1280, 512, 256, 3), (3072, 768, 1024, 5),
+                                          (320, 256, 256, 5)])
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 def test_gemm_tt_weight_grad(R, P, Q, splits, dt):
-    """dW = dY^T X through the transposed-read (ds_read_b64_tr_b16) main loop, split-K slabs."""
+    """dW = dY^T X through the transposed-read (ds_read_b64_tr_b16) main loop, split-K slabs (the
+    slices: whole K-tiles, [s T / S, (s + 1) T / S) of the T K-tiles)."""
     C = _C()
     torch.manual_seed(R + P + Q)
     dy = torch.randn(R, P, device=DEV).to(dt)
@@ -298,7 +303,9 @@ def _f8_codes(x, dt):
 @pytest.mark.parametrize("R,P,Q,splits", [(128, 256, 256, 1), (1024, 256, 512, 2), (2048, 512, 768, 4),
                                           (8192, 1024, 1024, 8), (384, 256, 256, 3),
                                           # partial 256-tiles: clamped staging, bounds-checked slab stores
-                                          (1024, 1600, 480, 2), (256, 16, 272, 1), (512, 4800, 1600, 2)])
+                                          (1024, 1600, 480, 2), (256, 16, 272, 1), (512, 4800, 1600, 2),
+                                          # uneven slices (1 and 2; 2 and 3 128-row K-tiles)
+                                          (384, 256, 256, 2), (640, 512, 256, 2)])
 @pytest.mark.parametrize("fmt_a", [1, 0])
 def test_gemm_tt_f8_weight_grad(R, P, Q, splits, fmt_a):
     """fp8 dW = alpha dY8^T X8 through the ds_read_b64_tr_b8 transposed-read main loop: against the
@@ -341,6 +348,6 @@ def test_gemm_tt_f8_supported_rejects():
     C = _C()
     a = torch.zeros(256, 256, device=DEV, dtype=torch.uint8)
     assert C.gemm_tt_f8_supported(a, a, 2)
-    assert not C.gemm_tt_f8_supported(a, a, 3)  # 256 rows / 3 slices is not a multiple of 128
+    assert not C.gemm_tt_f8_supported(a, a, 3)  # 256 rows = two 128-row K-tiles: at most 2 slices
     assert not C.gemm_tt_f8_supported(a[:, :248].contiguous(), a, 1)  # P % 16
     assert not C.gemm_tt_f8_supported(a.bfloat16(), a.bfloat16(), 1)

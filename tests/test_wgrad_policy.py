@@ -34,7 +34,10 @@ def test_tt_overrides(monkeypatch):
     assert fused._wgrad_tt_splits(98304, 4096, 1024) == 0
     monkeypatch.setattr(fused, "_WGRAD_TT", "8")
     assert fused._wgrad_tt_splits(98304, 3072, 1024) == 8
-    assert fused._wgrad_tt_splits(98304 + 64, 3072, 1024) == 0  # slices must divide into K-tiles
+    # slices are whole 64-row K-tiles, any count up to the K-tile count (uneven slices allowed)
+    assert fused._wgrad_tt_splits(98304 + 64, 3072, 1024) == 8
+    assert fused._wgrad_tt_splits(98304 + 32, 3072, 1024) == 0  # rows not a whole number of K-tiles
+    assert fused._wgrad_tt_splits(448, 3072, 1024) == 0  # 7 K-tiles: fewer than 8 slices
     assert fused._wgrad_tt_splits(16384, 4800, 1600) == 8  # partial tiles: the forced count applies
     monkeypatch.setattr(fused, "_WGRAD_TT", "auto")
     assert fused._wgrad_tt_splits(16384, 4800, 1600) == 0  # GPT-2 QKV: the library wins it

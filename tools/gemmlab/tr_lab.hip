@@ -63,7 +63,7 @@ template <int EPI, int DBG>
 void tr(const Prob& p, hipStream_t s) {
   const int tiles = (p.P / GB_M) * (p.Q / GB_N);
   hipLaunchKernelGGL((gemm_nt_kernel<bf16, EPI, true, false, bf16, -1, -1, DBG>), dim3(tiles, p.S), dim3(G_THREADS), 0,
-                     s, p.A, p.B, p.C, p.P, p.Q, p.R / p.S, (int64_t)p.P, (int64_t)p.Q, (int64_t)p.Q, nullptr, nullptr,
+                     s, p.A, p.B, p.C, p.P, p.Q, p.R, (int64_t)p.P, (int64_t)p.Q, (int64_t)p.Q, nullptr, nullptr,
                      (int64_t)0, nullptr, p.part, 0);
 }
 

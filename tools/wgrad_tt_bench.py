@@ -50,7 +50,7 @@ def main():
         out = torch.empty(n, k, device="cuda", dtype=torch.bfloat16)
         paths = {"lib": "0"}
         for s in (int(x) for x in args.splits.split(",")):
-            if M % (64 * s) == 0:
+            if M % 64 == 0 and M // 64 >= s:  # (slices of whole K-tiles, any count)
                 paths[f"tt_s{s}"] = str(s)
         paths["auto"] = "auto"
         res = {p: [] for p in paths}
