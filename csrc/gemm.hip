@@ -54,6 +54,17 @@ namespace {
 #ifndef APEX_G_GROUP_M
 #define APEX_G_GROUP_M 8
 #endif
+// APEX_GEMM_NT_GELU_D=1 / APEX_GEMM_NT_PLAIN=1 (A/B builds, off): the persistent bias+GELU_D epilogue
+// stores both outputs / the plain and bias-only epilogues store C non-temporally. Isolated, bias+GELU_D
+// ran 858 -> 821 us and a plain K = 1024 product 179 -> 164 us (profiles/r6_gemm_nt_stores.jsonl); in the
+// BERT step the GELU_D form was neutral (4156 vs 4155 seq/s, 3 interleaved pairs,
+// profiles/r6_gemm_nt_stores.jsonl): the next GEMM then reads its operand from HBM
+#ifndef APEX_GEMM_NT_GELU_D
+#define APEX_GEMM_NT_GELU_D 0
+#endif
+#ifndef APEX_GEMM_NT_PLAIN
+#define APEX_GEMM_NT_PLAIN 0
+#endif
 constexpr int GB_M = 256, GB_N = 256, GB_K = 64, G_THREADS = 512, G_GROUP_M = APEX_G_GROUP_M;
 constexpr int G_TILE_BYTES = GB_M * GB_K * 2;       // one operand tile: 32 KB
 constexpr int G_BUF_BYTES = 2 * G_TILE_BYTES;       // A + B: 64 KB
@@ -665,7 +676,8 @@ struct NoHook {
 // caller's hook: the next tile's LDS-DMA pieces, exactly 8 per wave) and retired by counted waits that
 // leave those pieces (and this epilogue's stores) in flight.
 // XD (lab diagnostics, tools/gemmlab; production 0): bit 0 skips the epilogue math (the stored values
-// are the rounded accumulators, same loads and stores), bit 1 skips every global store of the epilogue
+// are the rounded accumulators, same loads and stores), bit 1 skips every global store of the epilogue,
+// bit 2 stores the second output (H / gelu') non-temporally, bit 3 stores C non-temporally
 template <typename T, int EPI, bool EDGE, int J0 = 0, int NJ = 4, bool STAGED = false, int Q8 = 0,
           bool HALVES = false, typename Hook = NoHook, int XD = 0>
 __device__ __forceinline__ void epilogue(const f32x4 (&acc)[NJ][8], char* reg, T* __restrict__ C, int M, int N,
@@ -757,9 +769,19 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[NJ][8], char* reg, T
     // (ROCm 7.2) does not count the gfx950 store-data hazard — a VALU overwrote the data VGPRs of
     // a buffer_store_dwordx4 right after issue and corrupted a dword of the stored row (seen on
     // the GPU: sporadic dwords of EPI_BIAS_GELU's pre-activation output)
+    // non-temporal stores (build options above; XD bits 2 / 3 force them in the lab): nt on the second
+    // output (H / gelu') and / or on C
+    constexpr int NTX = XD | (HALVES && GELU_D && APEX_GEMM_NT_GELU_D ? 12 : 0) |
+                        (HALVES && (EPI == EPI_NONE || EPI == EPI_BIAS) && APEX_GEMM_NT_PLAIN ? 8 : 0);
     auto st = [&](const __amdgpu_buffer_rsrc_t& rs, int slot, const u32x4& x) {
       if constexpr (XD & 2) {  // no store: keep the value live
         asm volatile("" ::"v"(x));
+      } else if constexpr (NTX & 12) {  // non-temporal: aux 2 = nt
+        const bool o = &rs == &rs_o;
+        if (o ? (NTX & 4) : (NTX & 8))
+          __builtin_amdgcn_raw_buffer_store_b128(x, rs, voff(ldc, slot) + (uint32_t)soff(ldc, slot), 0, 2);
+        else
+          __builtin_amdgcn_raw_buffer_store_b128(x, rs, voff(ldc, slot) + (uint32_t)soff(ldc, slot), 0, 0);
       } else {
         __builtin_amdgcn_raw_buffer_store_b128(x, rs, voff(ldc, slot) + (uint32_t)soff(ldc, slot), 0, 0);
       }
@@ -1313,7 +1335,7 @@ __global__ void __launch_bounds__(G_THREADS) gemm_persist_kernel(const TI* __res
     };
     __builtin_amdgcn_sched_barrier(0);
     float q8w = 0.f;
-    epilogue<T, EPI, false, 0, 4, false, Q8, true, decltype(next_k0), (DBG >> 12) & 3>(acc, smem + G_BUF_BYTES + wid * 8192, C, M, N, ldc, bias, aux,
+    epilogue<T, EPI, false, 0, 4, false, Q8, true, decltype(next_k0), (DBG >> 12) & 15>(acc, smem + G_BUF_BYTES + wid * 8192, C, M, N, ldc, bias, aux,
                                                     ldaux, aux_out, part, m0, n0, tm, wr, wc, lane_e, alpha, q8,
                                                     next_k0, &q8w);
     if constexpr (Q8 != 0) {

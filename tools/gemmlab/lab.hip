@@ -235,6 +235,11 @@ void run_epi(Bufs& b, int rounds, int reps, hipStream_t s) {
     vs.push_back({"pers_nostore", launch_persist<EPI, 8192>});
     vs.push_back({"pers_nomath_nostore", launch_persist<EPI, 12288>});
   }
+  if (full && getenv("LAB_NT")) {  // non-temporal epilogue stores (XD bits 2, 3)
+    vs.push_back({"pers_nt_aux", launch_persist<EPI, 16384>});
+    vs.push_back({"pers_nt_c", launch_persist<EPI, 32768>});
+    vs.push_back({"pers_nt_both", launch_persist<EPI, 49152>});
+  }
   const int64_t MN = (int64_t)b.M * b.N;
   float* dmax;
   CK(hipMalloc(&dmax, 4));
