@@ -295,6 +295,8 @@ attn_fwd_kernel(AttnArgs a) {
   const T* kp = (const T*)a.k + b * a.k_bs + h * a.k_hs;
   const T* vp = (const T*)a.v + b * a.v_bs + h * a.v_hs;
   const T* brow = BIAS ? bias_row<T>(a, b, h, qrow) : nullptr;
+  // fp8 codes of O: scale and the amax filter value read here, their latency under the main loop
+  const float q8s = a.q8o ? a.q8_scale[0] : 0.f, q8seen = a.q8o ? f8_amax_seen(a.q8_amax) : 0.f;
 
   // Q^T fragments (B operand): lane (q=r, hl) holds Q[q][16s + 8hl .. +7]
   V8 qf[D / 16];
@@ -576,20 +578,25 @@ attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) *(uint4*)(op + 32 * db + 16 * j + 8 * hl) = wide[db][j];
     // Q8 (0: none, 1: e4m3, 2: e5m2) hoisted out of the store loop: fp8 codes of the stored
-    // (rounded) values, the attention-out GEMM's operand, from the packed words (f8_codes4)
-    const float qs = a.q8o ? a.q8_scale[0] : 0.f;
-    // (the codes' dwords regrouped by the same swap: 8-byte stores of 8 consecutive columns)
+    // (rounded) values, the attention-out GEMM's operand, from the regrouped words: wide[db][j]
+    // holds columns 32 db + 16 j + 8 hl .. + 7, so one more v_permlane32_swap per dword (the upper
+    // half-wave's j = 0 codes for the lower half's j = 1 codes) gives the lower half columns
+    // 32 db .. + 15 and the upper half 32 db + 16 .. + 31: one 16-byte code store per lane and
+    // 32 columns (it was two 8-byte stores; the store tail of these short workgroups is issue-bound)
     auto store_q8 = [&](auto Q8c) {
       constexpr int Q8 = decltype(Q8c)::value;
 #pragma unroll
-      for (int db = 0; db < D / 32; ++db)
+      for (int db = 0; db < D / 32; ++db) {
+        uint32_t c[2][2];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-          const uint32_t c0 = f8_codes4<Q8 - 1, T>(wv[db][2 * j].x, wv[db][2 * j].y, qs, q8mx);
-          const uint32_t c1 = f8_codes4<Q8 - 1, T>(wv[db][2 * j + 1].x, wv[db][2 * j + 1].y, qs, q8mx);
-          const auto rc = __builtin_amdgcn_permlane32_swap(c0, c1, false, false);
-          *(uint2*)(a.q8o + ooff + 32 * db + 16 * j + 8 * hl) = make_uint2(rc[0], rc[1]);
+          c[j][0] = f8_codes4<Q8 - 1, T>(wide[db][j].x, wide[db][j].y, q8s, q8mx);
+          c[j][1] = f8_codes4<Q8 - 1, T>(wide[db][j].z, wide[db][j].w, q8s, q8mx);
         }
+        const auto s0 = __builtin_amdgcn_permlane32_swap(c[0][0], c[1][0], false, false);
+        const auto s1 = __builtin_amdgcn_permlane32_swap(c[0][1], c[1][1], false, false);
+        *(uint4*)(a.q8o + ooff + 32 * db + 16 * hl) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+      }
     };
     if (a.q8o) {
       if (a.q8_fmt == 0) store_q8(std::integral_constant<int, 1>{});
@@ -598,7 +605,7 @@ attn_fwd_kernel(AttnArgs a) {
     if (hl == 0 && a.lse)
       a.lse[(int64_t)bh * a.Sq + qrow] = ltot > 0.f ? (m * sl2 + log2f(ltot)) * kLn2 : INFINITY;
   }
-  if (a.q8o) f8_block_amax(q8mx, a.q8_amax);  // every thread of the block reaches this
+  if (a.q8o) f8_block_amax(q8mx, a.q8_amax, q8seen);  // every thread of the block reaches this
 }
 
 // ---------------------------------------------------------------------------
@@ -796,7 +803,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
   float dqcs[D / 32][4] = {};  // DSUM: this lane's dq dims (see the dQ section) summed over queries
   // fp8 producer-side codes of dq / dk / dv (AttnArgs::q8dq..): running max|value| of this lane
   float q8mx = 0.f;
-  const float q8s = a.q8dq ? a.q8_scale[0] : 0.f;
+  const float q8s = a.q8dq ? a.q8_scale[0] : 0.f, q8seen = a.q8dq ? f8_amax_seen(a.q8_amax) : 0.f;
   auto body = [&](Pf& P, const int qb) {
     uint4 (&pf_q)[NLD] = P.q;
     uint4 (&pf_do)[NLD] = P.d;
@@ -1109,6 +1116,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
     // blocks of the same keys (64 contiguous bytes of each key row per store instruction)
     constexpr int NDB = D / 8, NTASK = NDB * (kBwdBK / 16);
     static_assert(NTASK % 16 == 0, "tasks per workgroup");
+    // fp8 codes of the stored values (the same element offset in the code array), 16 bytes per
+    // lane: the 16-lane groups g (even) and g + 1 hold adjacent 8-dim blocks of the same keys, so
+    // for iterations it and it + 1 one v_permlane16_swap per dword gives the even groups 16 dims of
+    // their iteration-it key and the odd groups 16 dims of their iteration-(it + 1) key — half the
+    // code store instructions
+    constexpr bool CPAIR = (NTASK / 16) % 2 == 0 && NDB % 2 == 0;
+    uint2 cprev = make_uint2(0u, 0u);
+    int kprev = 0, dprev = 0;
 #pragma unroll
     for (int it = 0; it < NTASK / 16; ++it) {
       const int t = it * 16 + wid * 4 + (lane >> 4);
@@ -1116,19 +1131,33 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
       const T* src = lds_k + (d0 + ((lane & 15) >> 2)) * LDE + kb + 4 * (lane & 3);
       const s16x4 lo = lds_tr16(src), hi = lds_tr16(src + 4 * LDE);
       const int key = k0 + kb + (lane & 15);
-      if (key < a.Sk) {
-        const V8 x = join4<V8>(lo, hi);
-        *(V8*)(dst + (int64_t)key * ss + d0) = x;
-        if (q8dst) {  // fp8 codes of the stored values (the same element offset in the code array)
-          const uint4 ww = __builtin_bit_cast(uint4, x);
-          uint2 c;
-          if (a.q8_fmt == 0) {
-            c.x = f8_codes4<0, T>(ww.x, ww.y, q8s, q8mx);
-            c.y = f8_codes4<0, T>(ww.z, ww.w, q8s, q8mx);
+      const V8 x = join4<V8>(lo, hi);
+      if (key < a.Sk) *(V8*)(dst + (int64_t)key * ss + d0) = x;
+      if (q8dst) {
+        const uint4 ww = __builtin_bit_cast(uint4, x);
+        uint2 c;
+        float mx = 0.f;  // only keys in range feed the amax
+        if (a.q8_fmt == 0) {
+          c.x = f8_codes4<0, T>(ww.x, ww.y, q8s, mx);
+          c.y = f8_codes4<0, T>(ww.z, ww.w, q8s, mx);
+        } else {
+          c.x = f8_codes4<1, T>(ww.x, ww.y, q8s, mx);
+          c.y = f8_codes4<1, T>(ww.z, ww.w, q8s, mx);
+        }
+        if (key < a.Sk) q8mx = fmaxf(q8mx, mx);
+        if constexpr (CPAIR) {
+          if (it & 1) {  // every lane swaps (outside the key branch)
+            const auto sx = __builtin_amdgcn_permlane16_swap(cprev.x, c.x, false, false);
+            const auto sy = __builtin_amdgcn_permlane16_swap(cprev.y, c.y, false, false);
+            const bool odd = (lane >> 4) & 1;
+            const int kk = odd ? key : kprev, dd = odd ? d0 - 8 : dprev;
+            if (kk < a.Sk) *(uint4*)(q8dst + (int64_t)kk * ss + dd) = make_uint4(sx[0], sy[0], sx[1], sy[1]);
           } else {
-            c.x = f8_codes4<1, T>(ww.x, ww.y, q8s, q8mx);
-            c.y = f8_codes4<1, T>(ww.z, ww.w, q8s, q8mx);
+            cprev = c;
+            kprev = key;
+            dprev = d0;
           }
+        } else if (key < a.Sk) {
           *(uint2*)(q8dst + (int64_t)key * ss + d0) = c;
         }
       }
@@ -1139,7 +1168,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
        a.q8dk ? a.q8dk + b * a.dk_bs + h * a.dk_hs : nullptr);
   emit(dv, rkeep, dvp, a.dv_ss, DSUM ? dsum + (int64_t)2 * a.H * D : nullptr,
        a.q8dv ? a.q8dv + b * a.dv_bs + h * a.dv_hs : nullptr);
-  if (a.q8dq) f8_block_amax(q8mx, a.q8_amax);  // every thread of the block reaches this
+  if (a.q8dq) f8_block_amax(q8mx, a.q8_amax, q8seen);  // every thread of the block reaches this
 }
 
 // dQ for key ranges longer than one backward key block: query-stationary, the forward's

@@ -126,4 +126,28 @@ __device__ __forceinline__ void f8_block_amax(float mx, float* amax) {
   }
 }
 
+// The filter value for the overload below, read at kernel START: an agent-scope atomic load (a
+// vector load that reads L2; a plain load of this wave-uniform address becomes a scalar load whose
+// cache keeps the launch's first value for every later workgroup on the CU).
+__device__ __forceinline__ float f8_amax_seen(const float* amax) {
+  return __hip_atomic_load(amax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Two-stage filter: the block max is first compared with `seen` (f8_amax_seen at kernel start, its
+// latency under the main loop); only a block that beats it re-reads amax at its end before the
+// atomic. Once amax has grown, later workgroups skip the end-of-block read round trip; the
+// workgroups that start while amax is still near 0 (it starts every step at 0) keep the exact
+// re-read — with the start value alone they all issued same-address atomics (fp8 step: LayerNorm
+// forward 136 -> 302 us, profiles/r6_bert_b768_fp8_step_kernels_stale_filter.txt).
+__device__ __forceinline__ void f8_block_amax(float mx, float* amax, float seen) {
+  __shared__ float red[4];
+  mx = f8_wave_max(mx);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    if (m > 0.f && m > seen && m > *(volatile float*)amax) f8_atomic_max_pos(amax, m);
+  }
+}
+
 }  // namespace apex

@@ -201,8 +201,10 @@ __global__ void __launch_bounds__(kEwBlock) bdaln_fwd_kernel(const T* __restrict
                                                             uint32_t thresh, float scale, Q8Out q8, int s_cond) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  // fp8 scale and amax filter value read up front (not behind the row's reductions)
+  const float qs = q8.y ? q8.scale[0] : 0.f, q8seen = q8.y ? f8_amax_seen(q8.amax) : 0.f;
   if (row >= rows) {
-    if (q8.y) f8_block_amax(0.f, q8.amax);  // the block reduction needs every wave
+    if (q8.y) f8_block_amax(0.f, q8.amax, q8seen);  // the block reduction needs every wave
     return;
   }
   const int nvec = cols >> 3;
@@ -261,8 +263,7 @@ __global__ void __launch_bounds__(kEwBlock) bdaln_fwd_kernel(const T* __restrict
     mean[row] = mu;
     rstd[row] = rs;
   }
-  float qs = 0.f, mx = 0.f;
-  if (q8.y) qs = q8.scale[0];
+  float mx = 0.f;
   bool gz = false;  // a gamma entry of exactly 0 (s_cond: the backward cannot rebuild x-hat from y)
 #pragma unroll
   for (int j = 0; j < VPT; ++j) {
@@ -292,7 +293,7 @@ __global__ void __launch_bounds__(kEwBlock) bdaln_fwd_kernel(const T* __restrict
       }
     }
   }
-  if (q8.y) f8_block_amax(mx, q8.amax);
+  if (q8.y) f8_block_amax(mx, q8.amax, q8seen);
   // s_cond (memory-efficient post-LN): s is stored only when gamma has a zero entry — every wave
   // holds the whole gamma row, so the decision is the same for every row of the launch, and the
   // backward (bdaln_bwd_kernel FROMY) makes the same test to read s instead of rebuilding x-hat.
@@ -335,6 +336,11 @@ __device__ __forceinline__ void bdaln_bwd_body(const T* __restrict__ dy, const T
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int nvec = cols >> 3;
   const float inv_n = 1.f / (float)cols;
+  float qs = 0.f, q8seen = 0.f, mx = 0.f;
+  if constexpr (Q8) {
+    qs = q8.scale[0];
+    q8seen = f8_amax_seen(q8.amax);
+  }
   float dg[VPT][8], dbt[VPT][8], dbi[VPT][8], g[VPT][8];
 #pragma unroll
   for (int j = 0; j < VPT; ++j) {
@@ -346,8 +352,6 @@ __device__ __forceinline__ void bdaln_bwd_body(const T* __restrict__ dy, const T
     if (j * 64 + lane < nvec) load_f<W, 8>(gamma + (j * 64 + lane) * 8, g[j]);
   }
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_wave * 4;
-  float qs = 0.f, mx = 0.f;
-  if constexpr (Q8) qs = q8.scale[0];
   typedef Pack<T, 8> P8;
   P8 ns[VPT], nd[VPT], ne[EXTRA ? VPT : 1];
   auto fetch = [&](int64_t row) {
@@ -450,7 +454,7 @@ __device__ __forceinline__ void bdaln_bwd_body(const T* __restrict__ dy, const T
       }
     }
   }
-  if constexpr (Q8) f8_block_amax(mx, q8.amax);
+  if constexpr (Q8) f8_block_amax(mx, q8.amax, q8seen);
   if constexpr (FROMY) __syncthreads();  // every wave is done with the staged beta / 1/gamma
   float* mine = lds + wid * 3 * cols;
 #pragma unroll

@@ -5,6 +5,8 @@ backward (codes of dQ / dK / dV), and the bias+dropout+residual+LayerNorm forwar
   off     no codes (the bf16 step's call)
   codes   codes + running amax from 0 (the fp8 step's call: a few blocks raise amax by atomics)
   noatom  codes, amax preset to 3e38 (every block's filter read sees a larger value: no atomics)
+  fresh   codes with amax zeroed before EVERY call, as in the model (each producer slot starts
+          the step at 0), minus the time of the zeroing alone
 and, for reference, the standalone quantise pass (C.fp8_quantize) over the same output.
 
     python tools/f8_producer_bench.py > profiles/r5_f8_producer_cost.jsonl
@@ -61,6 +63,8 @@ def main():
             res.setdefault("off", []).append(timeit(lambda: call(None)))
             res.setdefault("codes", []).append(timeit(lambda: call(codes), reset=lambda: amax.zero_()))
             res.setdefault("noatom", []).append(timeit(lambda: call(codes), reset=lambda: amax.fill_(3e38)))
+            zt = timeit(lambda: amax.zero_())
+            res.setdefault("fresh", []).append(timeit(lambda: (amax.zero_(), call(codes))) - zt)
             res.setdefault("standalone_quantize", []).append(
                 timeit(lambda: C.fp8_quantize(out_like, 0, scale, amax), reset=lambda: amax.zero_()))
         for k, v in res.items():
