@@ -90,6 +90,8 @@ def _C():
 _FP8_WGRAD = os.environ.get("APEX_FP8_WGRAD", "auto")
 # batched per-step weight quantisation (Fp8State._batch_weights); "0": one weight at a time
 _FP8_WBATCH = os.environ.get("APEX_FP8_WBATCH", "1")
+# codes-only producer outputs (Fp8State.codes_only_ok); "0": the 16-bit outputs are always stored
+_FP8_CODES_ONLY = os.environ.get("APEX_FP8_CODES_ONLY", "1")
 
 
 def _f8_wgrad_splits(R, P, Q, cus=256):
@@ -147,6 +149,8 @@ class Fp8State:
         # while the weakref is alive the (pointer, numel) key cannot name recycled memory.
         self._pre: dict = {}
         self._pre_bytes = 0
+        # (data_ptr, numel) -> weakref: outputs whose 16-bit values were never stored (codes only)
+        self._conly: dict = {}
         self.prequant_hits = 0
         # (operand, its _version, codes, scale_inv) of the last fp8 GEMM's activation operand
         self._last = None
@@ -323,9 +327,11 @@ class Fp8State:
         codes = torch.empty(like.shape if shape is None else shape, dtype=torch.uint8, device=like.device)
         return codes, self._view("scale", s), self._view("amax", s), fmt, s
 
-    def register(self, t, codes, slot, fmt):
+    def register(self, t, codes, slot, fmt, codes_only=False):
         """File producer-made codes of ``t`` (format ``fmt``, scaled by ``slot``) for the GEMM that
-        consumes ``t`` next."""
+        consumes ``t`` next. ``codes_only``: ``t``'s own values were never written (codes_only_ok)."""
+        if codes_only:
+            self._conly[(t.data_ptr(), t.numel())] = weakref.ref(t)
         # prune entries whose tensor died unconsumed, then cap by count and bytes (oldest first)
         for k in [k for k, e in self._pre.items() if e[0]() is None]:
             self._drop_pre(k)
@@ -359,9 +365,15 @@ class Fp8State:
         codes, _ = self.quantize(t, key, fmt)
         self.register(t, codes, s, fmt)
 
+    def _is_codes_only(self, a):
+        r = self._conly.get((a.data_ptr(), a.numel()))
+        return r is not None and r() is not None
+
     def _take(self, a, fmt):
         e = self._drop_pre((a.data_ptr(), a.numel()))
         if e is None:
+            if self._conly and self._is_codes_only(a):
+                raise RuntimeError("apex.fp8: a codes-only output reached a GEMM without its codes")
             return None
         ref, ver, codes, s, cfmt = e
         t = ref()
@@ -383,20 +395,22 @@ class Fp8State:
             return False
         return True
 
-    def forward_gemm(self, a, w, epi, bias=None, aux=None, q8=None):
+    def forward_gemm(self, a, w, epi, bias=None, aux=None, q8=None, codes_only=False):
         """a [M, K] @ w[N, K]^T with epilogue ``epi`` on the fp8 kernel -> (out, extra) or None.
         ``q8`` (from ``produce``; bias+GELU epilogues): the epilogue also writes the output's fp8
-        codes — ``q8_written(q8)`` tells the caller whether this call ran and wrote them."""
+        codes — ``q8_written(q8)`` tells the caller whether this call ran and wrote them.
+        ``codes_only`` (with ``q8``): ``out`` is allocated but its values are not stored (the caller
+        checked codes_only_ok for every consumer)."""
         if not self._fits(a, w, bias, aux, w.shape[1], w.shape[0]):
             self._last = None  # a declined GEMM must not leave an older operand's codes claimable
             return None
-        pre = self._take(a, self._fwd) if self._pre else None
+        pre = self._take(a, self._fwd) if self._pre or self._conly else None
         a8, ia = pre if pre is not None else self.quantize(a, (self.key_of(w), "x"), self._fwd)
         self._last = self._remember(a, a8, ia)
         w8, iw = self.weight(w)
         kw = {}
         if q8 is not None:
-            kw = dict(q8_out=q8[0], q8_scale=q8[1], q8_amax=q8[2], q8_fmt=q8[3])
+            kw = dict(q8_out=q8[0], q8_scale=q8[1], q8_amax=q8[2], q8_fmt=q8[3], q8_only=bool(codes_only))
             self._q8_last = q8[0]
         return _C().gemm_f8(a8, w8, ia, iw, self._fwd, epi, bias, aux, None, a.dtype, **kw)
 
@@ -406,18 +420,18 @@ class Fp8State:
         self._q8_last = None
         return ok
 
-    def backward_gemm(self, dy, w, epi, aux=None, bias_grad_dtype=None, q8=None):
+    def backward_gemm(self, dy, w, epi, aux=None, bias_grad_dtype=None, q8=None, codes_only=False):
         """dy [M, N] @ w[N, K] with epilogue ``epi`` (dy e5m2 x W^T e4m3) -> (out, extra) or None."""
         if not self._fits(dy, w, None, aux, w.shape[0], w.shape[1]):
             self._last = None
             return None
-        pre = self._take(dy, self._bwd) if self._pre else None
+        pre = self._take(dy, self._bwd) if self._pre or self._conly else None
         d8, id_ = pre if pre is not None else self.quantize(dy, (self.key_of(w), "dy"), self._bwd)
         self._last = self._remember(dy, d8, id_)
         wt8, iw = self.weight_t(w)
         kw = {}
         if q8 is not None:  # (dGELU / MUL epilogues: the hidden gradient's codes for the W1 dgrad)
-            kw = dict(q8_out=q8[0], q8_scale=q8[1], q8_amax=q8[2], q8_fmt=q8[3])
+            kw = dict(q8_out=q8[0], q8_scale=q8[1], q8_amax=q8[2], q8_fmt=q8[3], q8_only=bool(codes_only))
             self._q8_last = q8[0]
         return _C().gemm_f8(d8, wt8, id_, iw, self._bwd, epi, None, aux, bias_grad_dtype, dy.dtype, **kw)
 
@@ -447,6 +461,27 @@ class Fp8State:
     def wgrad_enabled(self):
         return self.recipe.fp8_wgrad and _FP8_WGRAD != "0" and self._fwd == E4M3
 
+    # ------------------------------------------------------------------ codes-only outputs
+    def codes_only_ok(self, a_like, w, contraction, width, aux=None):
+        """May a producer skip storing its 16-bit output? Yes when that output's consumers all read
+        fp8 codes: the next GEMM (an ``a_like``-typed operand against ``w``, given contraction /
+        output width, optional ``aux``) fits the fp8 kernel, and the weight gradient that keeps the
+        operand runs on its codes (fp8 weight gradients on). The fused MLP uses it for gelu(H) (the
+        bias+GELU+derivative forward feeds only the W2 GEMM and the W2 gradient) and for dH (the
+        multiply backward feeds only the W1 input-gradient GEMM and the W1 gradient): one [tokens,
+        4 x hidden] 16-bit store less each (csrc/gemm.hip epilogue XD bit 4). A weight gradient
+        that still declines fp8 (main_grad accumulation, a declined shape) takes the codes'
+        dequantised values (``dequantize``), never the unwritten tensor."""
+        return (_FP8_CODES_ONLY != "0" and self.wgrad_enabled() and a_like.is_cuda
+                and self._fits(a_like, w, None, aux, contraction, width))
+
+    @staticmethod
+    def dequantize(codes_sinv, fmt, dtype):
+        """(codes, scale_inv) -> the values they encode, in ``dtype`` (OCP e4m3fn / e5m2)."""
+        codes, sinv = codes_sinv
+        f8t = torch.float8_e4m3fn if fmt == E4M3 else torch.float8_e5m2
+        return (codes.view(f8t).to(torch.float32) * sinv).to(dtype)
+
     def wgrad(self, d, x, out_dtype, out=None):
         """dW [P, Q] = dy^T x from the codes ``d`` (dy [R, P], backward format) and ``x`` (x [R, Q],
         e4m3) on the fp8 transposed-read kernel (csrc/gemm.hip gemm_tt_f8) -> out_dtype (written
@@ -473,6 +508,7 @@ class Fp8State:
         self._wcache.clear()
         self._pre.clear()
         self._pre_bytes = 0
+        self._conly.clear()
         self._recycle_slots()
         if self.n == 0:
             return

@@ -153,13 +153,30 @@ def _q8_kw(q8):
     return {} if q8 is None else dict(q8_out=q8[0], q8_scale=q8[1], q8_amax=q8[2], q8_fmt=q8[3])
 
 
-def _q8_file(f8, t, q8, key, fmt):
+def _q8_file(f8, t, q8, key, fmt, codes_only=False):
     if f8 is None or not _FP8_PRODUCER:
         return
     if q8 is not None:
-        f8.register(t, q8[0], q8[4], q8[3])
+        f8.register(t, q8[0], q8[4], q8[3], codes_only=codes_only)
     else:
         f8.quantize_output(t, key, fmt)  # first use: measure with current scaling
+
+
+def _wgrad_codes_only(dy2, x2, param, f8, d8, x8, dtype):
+    """Weight gradient dy2^T x2 when one operand (``dy2`` or ``x2`` None) exists only as fp8 codes
+    (apex.fp8 codes_only_ok): the fp8 product on the codes; where that declines (main_grad
+    accumulation, a non-contiguous target, a shape the fp8 kernel rejects) the 16-bit product on the
+    codes' dequantised values — the same values the fp8 product uses, never the unwritten tensor."""
+    out = _gt(param) if param is not None else None
+    if getattr(param, "main_grad", None) is None and (out is None or out.is_contiguous()):
+        r = f8.wgrad(d8, x8, dtype, out=out)
+        if r is not None:
+            return r
+    if dy2 is None:
+        dy2 = f8.dequantize(d8, f8._bwd, dtype)
+    if x2 is None:
+        x2 = f8.dequantize(x8, f8._fwd, dtype)
+    return _wgrad(dy2, x2, param=param)
 
 class _AttnSublayer(torch.autograd.Function):
     @staticmethod
@@ -261,19 +278,28 @@ class _FFNSublayer(torch.autograd.Function):
             # the W2 GEMM (producer slot keyed by W1, role "y")
             gkey = (f8.key_of(w1), "y") if f8 is not None else None
             q8 = _q8(f8, gkey, f8._fwd, x2, shape=(x2.shape[0], w1.shape[0])) if f8 is not None else None
-            g, h = G.linear_gelu_d(x2, w1, b1, f8=f8, q8=q8) if _STORE_DERIV else \
+            # codes only: g's 16-bit values are not stored when its two consumers (the W2 GEMM below
+            # and the W2 weight gradient) read its fp8 codes
+            conly = q8 is not None and _STORE_DERIV and f8.codes_only_ok(x2, w2, w2.shape[1], w2.shape[0])
+            g, h = G.linear_gelu_d(x2, w1, b1, f8=f8, q8=q8, codes_only=conly) if _STORE_DERIV else \
                 G.linear_gelu(x2, w1, b1, f8=f8, q8=q8)
             x8 = f8.operand_codes(x2) if f8 is not None else None
             if f8 is not None:
-                _q8_file(f8, g, q8 if f8.q8_written(q8) else None, gkey, f8._fwd)
+                written = f8.q8_written(q8)
+                conly = conly and written  # (a declined fp8 GEMM stored g in full)
+                _q8_file(f8, g, q8 if written else None, gkey, f8._fwd, codes_only=conly)
             hb = None
         else:
             h = torch.mm(x2, w1.t())
             g = C.bias_act_fwd(h, b1, act)
             hb = b1
             x8 = None
+            conly = False
         t = G.linear(g, w2, f8=f8)
         ctx.f8codes = (x8, f8.operand_codes(g) if f8 is not None else None)
+        if conly and ctx.f8codes[1] is None:
+            raise RuntimeError("apex.fp8: the codes-only MLP activation was not consumed as fp8 codes")
+        ctx.g_conly = conly
         seed, off = _seed(x.device) if p > 0 else (0, 0)
         mem, store_s = _ln_plan(C, gamma, x2.shape[1], any(ctx.needs_input_grad))
         ykey = (f8.key_of(gamma), "y") if f8 is not None else None
@@ -282,7 +308,7 @@ class _FFNSublayer(torch.autograd.Function):
                                        store_s=store_s, s_cond=mem, **_q8_kw(q8))
         if f8 is not None:
             _q8_file(f8, y, q8, ykey, f8._fwd)
-        ctx.save_for_backward(x2, w1, hb, h, g, w2, y if mem else s, gamma, mean, rstd,
+        ctx.save_for_backward(x2, w1, hb, h, None if conly else g, w2, y if mem else s, gamma, mean, rstd,
                               s if mem and store_s else None)
         ctx.ln_beta = beta if mem else None
         ctx.cfg = (p, seed, off, act, b2 is not None, b1.dtype if b1 is not None else None)
@@ -310,23 +336,37 @@ class _FFNSublayer(torch.autograd.Function):
             # fp8: the epilogue also writes dh's e5m2 codes for the W1 dgrad (W1's own "dy" slot)
             hkey = (f8.key_of(w1), "dy") if f8 is not None else None
             q8h = _q8(f8, hkey, f8._bwd, dt, shape=(dt.shape[0], w1.shape[0])) if f8 is not None else None
+            # codes only: dh's consumers are the W1 input-gradient GEMM (+ residual) and the W1 gradient
+            dconly = q8h is not None and _STORE_DERIV and f8.codes_only_ok(dt, w1, w1.shape[0], w1.shape[1], aux=dres)
             if _STORE_DERIV:
                 # (dt W2) * gelu'(h) (stored) and its column sums
-                dh, db1 = G.dgrad_mul(dt, w2, h, b1dt, f8=f8, bias_grad_out=tb1, q8=q8h)
+                dh, db1 = G.dgrad_mul(dt, w2, h, b1dt, f8=f8, bias_grad_out=tb1, q8=q8h, codes_only=dconly)
             else:
                 dh, db1 = G.dgrad_dgelu(dt, w2, h, b1dt, f8=f8, bias_grad_out=tb1, q8=q8h)  # (dt W2) * gelu'(h) from h
             dt8 = f8.operand_codes(dt) if f8 is not None else None
             if q8h is not None and f8.q8_written(q8h):
-                f8.register(dh, q8h[0], q8h[4], q8h[3])
+                f8.register(dh, q8h[0], q8h[4], q8h[3], codes_only=dconly)
+            else:
+                dconly = False
             if tb1 is not None and db1 is not None and db1.data_ptr() != tb1.data_ptr():
                 db1 = tb1.copy_(db1)  # a path that could not write the slot: keep the handed-out view valid
         else:
             dh, db1 = C.bias_act_bwd(G.dgrad(dt, w2, f8=f8), h, hb, act)
             dt8 = f8.operand_codes(dt) if f8 is not None else None
+            dconly = False
         x8, g8 = ctx.f8codes
-        dw2 = _wgrad(dt, g, param=pw2, f8=(f8, dt8, g8))
+        if ctx.g_conly:
+            dw2 = _wgrad_codes_only(dt, None, pw2, f8, dt8, g8, dt.dtype)
+        else:
+            dw2 = _wgrad(dt, g, param=pw2, f8=(f8, dt8, g8))
         dx = G.dgrad_resid(dh, w1, dres, f8=f8)  # residual grad accumulated in the GEMM epilogue
-        dw1 = _wgrad(dh, x2, param=pw1, f8=(f8, f8.operand_codes(dh) if f8 is not None else None, x8))
+        dh8 = f8.operand_codes(dh) if f8 is not None else None
+        if dconly:
+            if dh8 is None:
+                raise RuntimeError("apex.fp8: the codes-only MLP hidden gradient was not consumed as fp8 codes")
+            dw1 = _wgrad_codes_only(None, x2, pw1, f8, dh8, x8, dt.dtype)
+        else:
+            dw1 = _wgrad(dh, x2, param=pw1, f8=(f8, dh8, x8))
         return (dx.view_as(dy), dw1, db1 if b1dt is not None else None, dw2, db2 if has_b2 else None, dgamma,
                 dbeta, None, None, None)
 

@@ -155,15 +155,16 @@ def linear_gelu(x, w, b, act=ACT_GELU, f8=None, q8=None):
     return y.view(shp), h.view(shp)
 
 
-def linear_gelu_d(x, w, b, act=ACT_GELU, f8=None, q8=None):
+def linear_gelu_d(x, w, b, act=ACT_GELU, f8=None, q8=None, codes_only=False):
     """(gelu(h), gelu'(h)) with h = x w^T + b: the forward of an MLP whose backward multiplies by
     the stored derivative (dgrad_mul) instead of re-evaluating erf/exp from h. The derivative
-    is taken at the rounded h, as the unfused composition's backward would."""
+    is taken at the rounded h, as the unfused composition's backward would. ``codes_only`` (fp8,
+    with ``q8``): gelu(h) is left unwritten on the fp8 kernel — only its codes are stored."""
     a = _2d(x)
     C = _C()
     shp = (*x.shape[:-1], w.shape[0])
-    r = f8.forward_gemm(a, w, C.EPI_BIAS_GELU_TANH_D if act == ACT_GELU_TANH else C.EPI_BIAS_GELU_D, b, q8=q8) \
-        if f8 is not None and b is not None else None
+    r = f8.forward_gemm(a, w, C.EPI_BIAS_GELU_TANH_D if act == ACT_GELU_TANH else C.EPI_BIAS_GELU_D, b, q8=q8,
+                        codes_only=codes_only) if f8 is not None and b is not None else None
     if r is not None:
         return r[0].view(shp), r[1].view(shp)
     if use_mfma(a, w) and b is not None and b.dtype == x.dtype:
@@ -176,13 +177,14 @@ def linear_gelu_d(x, w, b, act=ACT_GELU, f8=None, q8=None):
     return y.view(shp), gd.view(shp)
 
 
-def dgrad_mul(dy, w, gd, bias_dtype, wT=None, f8=None, bias_grad_out=None, q8=None):
+def dgrad_mul(dy, w, gd, bias_dtype, wT=None, f8=None, bias_grad_out=None, q8=None, codes_only=False):
     """(dh, db): dh = (dy @ w) * gd (gd = the stored activation derivative), db = column sums of dh
-    (written into ``bias_grad_out`` on the MFMA path when given)."""
+    (written into ``bias_grad_out`` on the MFMA path when given). ``codes_only`` (fp8, with ``q8``):
+    dh is left unwritten on the fp8 kernel — only its codes (and db) are stored."""
     a = _2d(dy)
     g2 = _2d(gd)
     C = _C()
-    r = f8.backward_gemm(a, w, C.EPI_MUL, g2, bias_dtype, q8=q8) if f8 is not None else None
+    r = f8.backward_gemm(a, w, C.EPI_MUL, g2, bias_dtype, q8=q8, codes_only=codes_only) if f8 is not None else None
     if r is not None:
         return r
     if _MODE != "blas" and a.is_cuda and g2.is_contiguous() and g2.dtype == a.dtype:

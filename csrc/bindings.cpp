@@ -1190,7 +1190,7 @@ std::vector<Tensor> k_gemm_f8(Tensor a, Tensor b, Tensor alpha_a, Tensor alpha_b
                               const c10::optional<Tensor>& bias, const c10::optional<Tensor>& aux,
                               c10::optional<at::ScalarType> bias_grad_dtype, at::ScalarType out_dtype,
                               const c10::optional<Tensor>& q8_out, const c10::optional<Tensor>& q8_scale,
-                              const c10::optional<Tensor>& q8_amax, int64_t q8_fmt) {
+                              const c10::optional<Tensor>& q8_amax, int64_t q8_fmt, bool q8_only) {
   TORCH_CHECK(k_gemm_f8_supported(a, b), "gemm_f8: unsupported operands (uint8 codes, K % 128 == 0, N % 8 == 0, "
               "16-byte aligned, unit inner stride)");
   TORCH_CHECK(out_dtype == at::kBFloat16 || out_dtype == at::kHalf, "gemm_f8: bf16 / fp16 output");
@@ -1240,6 +1240,10 @@ std::vector<Tensor> k_gemm_f8(Tensor a, Tensor b, Tensor alpha_a, Tensor alpha_b
   }
   g.q8 = q8_args(q8_out, q8_scale, q8_amax, q8_fmt, c, "gemm_f8");
   TORCH_CHECK(!g.q8.y || gelu_fwd || mul, "gemm_f8: q8_out needs a GELU / dGELU / MUL epilogue");
+  // q8_only: the returned C is allocated but (on the kernels that honour it: bias+GELU+derivative and
+  // multiply, full 256x256 tiles) never written — the caller promises that only the codes are read
+  TORCH_CHECK(!q8_only || g.q8.y, "gemm_f8: q8_only needs q8_out");
+  g.q8.only = q8_only ? 1 : 0;
   check(apex::gemm_nt_f8(g, (int)fmt_a, 0, dt_code(out_dtype), cur_stream()), "gemm_f8");
   if (mul && bias_grad_dtype.has_value()) {
     extra = at::empty({N}, a.options().dtype(*bias_grad_dtype));
@@ -1519,7 +1523,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_f8", &k_gemm_f8, py::arg("a"), py::arg("b"), py::arg("alpha_a"), py::arg("alpha_b"), py::arg("fmt_a"),
         py::arg("epi"), py::arg("bias") = py::none(), py::arg("aux") = py::none(),
         py::arg("bias_grad_dtype") = py::none(), py::arg("out_dtype") = at::kBFloat16, py::arg("q8_out") = py::none(),
-        py::arg("q8_scale") = py::none(), py::arg("q8_amax") = py::none(), py::arg("q8_fmt") = 0);
+        py::arg("q8_scale") = py::none(), py::arg("q8_amax") = py::none(), py::arg("q8_fmt") = 0,
+        py::arg("q8_only") = false);
   m.def("fp8_quantize_weights", &k_fp8_quantize_weights, py::arg("weights"), py::arg("slots"), py::arg("want_t"),
         py::arg("fmt"), py::arg("scale"), py::arg("scale_inv"), py::arg("amax"), py::arg("smax"));
   m.def("fp8_quantize", &k_fp8_quantize, py::arg("x"), py::arg("fmt"), py::arg("scale"), py::arg("amax") = py::none(),

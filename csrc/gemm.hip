@@ -677,7 +677,10 @@ struct NoHook {
 // leave those pieces (and this epilogue's stores) in flight.
 // XD (lab diagnostics, tools/gemmlab; production 0): bit 0 skips the epilogue math (the stored values
 // are the rounded accumulators, same loads and stores), bit 1 skips every global store of the epilogue,
-// bit 2 stores the second output (H / gelu') non-temporally, bit 3 stores C non-temporally
+// bit 2 stores the second output (H / gelu') non-temporally, bit 3 stores C non-temporally.
+// Bit 4 (production, fp8 codes-only outputs, Q8Out::only): C itself is not stored — its fp8 codes
+// (and the GELU_D derivative / the MUL bias-grad partials) are: the fp8 step's consumers of the MLP
+// hidden activation and its gradient read only the codes (apex.fp8 codes_only_ok)
 template <typename T, int EPI, bool EDGE, int J0 = 0, int NJ = 4, bool STAGED = false, int Q8 = 0,
           bool HALVES = false, typename Hook = NoHook, int XD = 0>
 __device__ __forceinline__ void epilogue(const f32x4 (&acc)[NJ][8], char* reg, T* __restrict__ C, int M, int N,
@@ -947,7 +950,7 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[NJ][8], char* reg, T
             }
           }
         }
-        st(rs_c, slot, out);
+        if constexpr (!(XD & 16)) st(rs_c, slot, out);
         // one slot at a time: unpacking every slot's operands up front (16 bf16 -> 16 fp32 per
         // slot, hoisted by the scheduler) is what pushed these epilogues past 256 VGPRs
         __builtin_amdgcn_sched_barrier(0);
@@ -1037,7 +1040,7 @@ inline bool host_split_xcd() {
 // T: output / epilogue dtype; TI: operand dtype (T, or uint8_t fp8 with formats FA (A) / FB (B) and
 // the dequantisation alpha = alpha_a[0] * alpha_b[0] read on the device)
 template <typename T, int EPI, bool TR, bool EDGE, typename TI = T, int FA = -1, int FB = -1, int DBG = 0,
-          int Q8 = 0>
+          int Q8 = 0, bool NOC = false>
 __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(const TI* __restrict__ A, const TI* __restrict__ B,
                                                             T* __restrict__ C, int M, int N, int K, int64_t lda,
                                                             int64_t ldb, int64_t ldc, const T* __restrict__ bias,
@@ -1174,8 +1177,9 @@ __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(const TI* __restrict
   }
   float alpha = 1.f;
   if constexpr (FA >= 0) alpha = alpha_a[0] * alpha_b[0];
-  epilogue<T, EPI, EDGE, 0, 4, false, Q8>(acc, smem + wid * 16384, C, M, N, ldc, bias, aux, ldaux, aux_out, part, m0,
-                                         n0, tm, wr, wc, lane, alpha, q8);
+  epilogue<T, EPI, EDGE, 0, 4, false, Q8, false, NoHook, NOC ? 16 : 0>(acc, smem + wid * 16384, C, M, N, ldc, bias,
+                                                                        aux, ldaux, aux_out, part, m0, n0, tm, wr, wc,
+                                                                        lane, alpha, q8);
   if constexpr ((DBG & 2048) && FA < 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     bar();
@@ -1527,22 +1531,32 @@ void launch_gemm_f8(const GemmArgs& g, hipStream_t s) {
     go(std::integral_constant<int, 0>{});
     return;
   }
+  // codes-only C (Q8Out::only): the bias+GELU+derivative forward and the multiply backward on full
+  // tiles; elsewhere the flag is ignored (C written as well: a superset, never wrong)
+  constexpr bool NOC_OK = EPI == EPI_BIAS_GELU_D || EPI == EPI_BIAS_GELU_TANH_D || EPI == EPI_MUL;
   if constexpr (Q8_OK) {
     if (g.q8.y) {
-      auto go = [&](auto edge_c, auto q_c) {
+      auto go = [&](auto edge_c, auto q_c, auto noc_c) {
         hipLaunchKernelGGL((gemm_nt_kernel<T, EPI, false, decltype(edge_c)::value, uint8_t, FA, FB, 0,
-                                           decltype(q_c)::value>),
+                                           decltype(q_c)::value, decltype(noc_c)::value>),
                            dim3(tiles), dim3(G_THREADS), 0, s, (const uint8_t*)g.A, (const uint8_t*)g.B, (T*)g.C, g.M,
                            g.N, g.K, g.lda, g.ldb, g.ldc, (const T*)g.bias, (const T*)g.aux, g.ldaux, (T*)g.aux_out,
                            g.part, 0, g.alpha_a, g.alpha_b, g.q8);
       };
       const bool edge = g.M % GB_M != 0 || g.N % GB_N != 0;
+      if constexpr (NOC_OK) {
+        if (g.q8.only && !edge) {
+          if (g.q8.fmt == 0) go(std::false_type{}, std::integral_constant<int, 1>{}, std::true_type{});
+          else go(std::false_type{}, std::integral_constant<int, 2>{}, std::true_type{});
+          return;
+        }
+      }
       if (g.q8.fmt == 0) {
-        if (edge) go(std::true_type{}, std::integral_constant<int, 1>{});
-        else go(std::false_type{}, std::integral_constant<int, 1>{});
+        if (edge) go(std::true_type{}, std::integral_constant<int, 1>{}, std::false_type{});
+        else go(std::false_type{}, std::integral_constant<int, 1>{}, std::false_type{});
       } else {
-        if (edge) go(std::true_type{}, std::integral_constant<int, 2>{});
-        else go(std::false_type{}, std::integral_constant<int, 2>{});
+        if (edge) go(std::true_type{}, std::integral_constant<int, 2>{}, std::false_type{});
+        else go(std::false_type{}, std::integral_constant<int, 2>{}, std::false_type{});
       }
       return;
     }

@@ -162,6 +162,7 @@ struct Q8Out {
   const float* scale = nullptr;
   float* amax = nullptr;
   int fmt = 0;
+  int only = 0;  // GEMM producers: the codes are the output's only consumer-visible form (C not stored)
 };
 int bdaln_supported(int cols);
 int bdaln_wide_supported(int cols);  // 2056..4096 columns (bdaln fwd/bwd only, not the embedding block)

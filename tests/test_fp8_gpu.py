@@ -626,3 +626,95 @@ def test_fp8_step_batches_weight_quantization(fp8_off, monkeypatch):
             outs[mode] = fused.fused_dense(fused.fused_dense(x, w1), w2)
             assert not st._wprev and len(st._wcache) == 2
     assert torch.equal(outs["1"], outs["0"])
+
+
+@pytest.mark.parametrize("epi_name", ["EPI_BIAS_GELU_D", "EPI_MUL"])
+@pytest.mark.parametrize("M,N", [(512, 1024), (300, 520)])
+def test_gemm_f8_codes_only_output(epi_name, M, N):
+    """q8_only (codes-only output, csrc/gemm.hip epilogue XD bit 4): the fp8 codes, the amax, the
+    second output (gelu') and the bias-gradient sums equal those of the call that also stores C;
+    on full tiles C is left unwritten (it keeps the allocator's bytes), edge tiles ignore the flag."""
+    C = _C()
+    torch.manual_seed(14)
+    K = 256
+    one = torch.ones(1, device=DEV)
+    mul = epi_name == "EPI_MUL"
+    fmt_a = 1 if mul else 0
+    a8 = C.fp8_quantize(torch.randn(M, K, device=DEV).bfloat16(), fmt_a, one)
+    w8 = C.fp8_quantize((torch.randn(N, K, device=DEV) * 0.1).bfloat16(), 0, one)
+    epi = getattr(C, epi_name)
+    bias = None if mul else (torch.randn(N, device=DEV) * 0.1).bfloat16()
+    aux = torch.randn(M, N, device=DEV).bfloat16() if mul else None
+    bdt = torch.float32 if mul else None
+    scale = torch.tensor([5.0], device=DEV)
+    outs = []
+    for only in (False, True):
+        amax = torch.zeros(1, device=DEV)
+        codes = torch.full((M, N), 7, device=DEV, dtype=torch.uint8)
+        c, extra = C.gemm_f8(a8, w8, one, one, fmt_a, epi, bias, aux, bdt, torch.bfloat16, q8_out=codes,
+                             q8_scale=scale, q8_amax=amax, q8_fmt=1 if mul else 0, q8_only=only)
+        torch.cuda.synchronize()
+        outs.append((c, extra, codes, float(amax)))
+    (c0, e0, k0, a0), (c1, e1, k1, a1) = outs
+    assert torch.equal(k0, k1) and a0 == a1
+    torch.testing.assert_close(e1, e0, rtol=0, atol=0)
+    if M % 256 or N % 256:
+        assert torch.equal(c1, c0)  # edge launch: the flag is ignored, C stored
+    with pytest.raises(RuntimeError):
+        C.gemm_f8(a8, w8, one, one, fmt_a, epi, bias, aux, bdt, torch.bfloat16, q8_only=True)
+
+
+def test_ffn_codes_only_matches_stored_outputs(fp8_off, monkeypatch):
+    """The fused FFN sublayer with codes-only gelu(H) and dH (apex.fp8 codes_only_ok; full 256x256
+    tiles: 512 tokens, F = 1024) against the same steps with both stored: bit-identical outputs and
+    gradients (every consumer reads the codes either way), gelu(H) not saved for backward; and with
+    the fp8 weight gradient forced to decline, the dequantised-codes fallback stays close."""
+    import apex.fp8 as fp8mod
+    from apex.ops import blocks
+
+    fp8 = fp8_off
+    torch.manual_seed(1)
+    B, S, E, F = 4, 128, 256, 1024
+    dt = torch.bfloat16
+    x = torch.randn(B, S, E, device=DEV, dtype=dt)
+    mk = lambda *s, sc=0.05: (torch.randn(*s, device=DEV) * sc).to(dt).requires_grad_(True)
+    params = [mk(F, E), mk(F), mk(E, F), mk(E), (torch.rand(E, device=DEV) + 0.5).to(dt).requires_grad_(True), mk(E)]
+
+    def run(codes_only, decline_wgrad=False):
+        monkeypatch.setattr(fp8mod, "_FP8_CODES_ONLY", "1" if codes_only else "0")
+        fp8.disable()
+        outs, saved_g = [], []
+        for step in range(3):
+            with fp8.fp8_autocast():
+                st = fp8.state()
+                if decline_wgrad:
+                    monkeypatch.setattr(st, "wgrad", lambda *a, **k: None)
+                xi = x.clone().requires_grad_(True)
+                y = blocks.ffn_sublayer(xi, *params)
+                node = y.grad_fn if hasattr(y.grad_fn, "saved_tensors") else y.grad_fn.next_functions[0][0]
+                saved_g.append(node.saved_tensors[4] is None)  # (x2, w1, hb, h, g, ...)
+                dy = torch.randn(y.shape, device=DEV, generator=torch.Generator(device=DEV).manual_seed(step)).to(dt)
+                grads = torch.autograd.grad(y, [xi] + params, dy)
+            outs.append((y.detach(), grads))
+            fp8.step()
+        fp8.disable()
+        return outs, saved_g
+
+    ref, g_ref = run(False)
+    got, g_got = run(True)
+    assert not any(g_ref)
+    assert all(g_got[1:])  # step 0: the slot's first use stores g (standalone current scaling)
+    for (ya, ga), (yb, gb) in zip(got, ref):
+        torch.testing.assert_close(ya, yb, rtol=0, atol=0)
+        for a, b in zip(ga, gb):
+            torch.testing.assert_close(a, b, rtol=0, atol=0)
+    # fallback: every weight gradient declines fp8 -> 16-bit products, on the codes' dequantised values
+    # for g / dH; against the same declined run with g / dH stored (the difference: e4m3 / e5m2
+    # rounding of those two operands — e5m2's 2 mantissa bits alone give ~5 % in the W1 gradient;
+    # the unwritten tensor's bytes would give O(1) or NaN)
+    fb, _ = run(True, decline_wgrad=True)
+    fr, _ = run(False, decline_wgrad=True)
+    for (ya, ga), (yb, gb) in zip(fb, fr):
+        for a, b in zip(ga, gb):
+            rel = float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12))
+            assert rel < 0.15, rel
