@@ -149,8 +149,20 @@ def _q8(f8, key, fmt, like, shape=None):
     return f8.produce(key, fmt, like, shape=shape)
 
 
-def _q8_kw(q8):
-    return {} if q8 is None else dict(q8_out=q8[0], q8_scale=q8[1], q8_amax=q8[2], q8_fmt=q8[3])
+def _q8_kw(q8, only=False):
+    if q8 is None:
+        return {}
+    kw = dict(q8_out=q8[0], q8_scale=q8[1], q8_amax=q8[2], q8_fmt=q8[3])
+    if only:
+        kw["q8_only"] = True
+    return kw
+
+
+def _wgrad_f8(dy2, x2, param, f8, d8, x8, dy_only, x_only):
+    """_wgrad, or _wgrad_codes_only when either operand exists as fp8 codes only."""
+    if dy_only or x_only:
+        return _wgrad_codes_only(None if dy_only else dy2, None if x_only else x2, param, f8, d8, x8, dy2.dtype)
+    return _wgrad(dy2, x2, param=param, f8=(f8, d8, x8))
 
 
 def _q8_file(f8, t, q8, key, fmt, codes_only=False):
@@ -231,16 +243,20 @@ class _AttnSublayer(torch.autograd.Function):
         f8 = ctx.f8
         dkey = (f8.key_of(wo), "dy") if f8 is not None else None
         q8 = _q8(f8, dkey, f8._bwd, s) if f8 is not None else None
+        # codes only: dt's consumers are the out-projection input-gradient GEMM and its weight gradient
+        tconly = q8 is not None and f8.codes_only_ok(_2d(dy), wo, wo.shape[0], wo.shape[1])
         dres, dt, dgamma, dbeta, dbo = C.bdaln_bwd(_2d(dy), s, gamma, mean, rstd, float(p_hidden), sh, oh, has_bo,
                                                    dgamma_out=_gt(pg), dbeta_out=_gt(pb),
                                                    dbias_out=_gt(pbo) if has_bo else None, beta=ctx.ln_beta,
-                                                   s_alt=s_alt, **_q8_kw(q8))
+                                                   s_alt=s_alt, **_q8_kw(q8, tconly))
         if q8 is not None:
-            f8.register(dt, q8[0], q8[4], q8[3])
+            f8.register(dt, q8[0], q8[4], q8[3], codes_only=tconly)
         dctx = G.dgrad(dt, wo, f8=f8).view(B, S, heads, d)
         x8, o8 = ctx.f8codes
-        dwo = _wgrad(dt, o.view(B * S, E), param=pwo,
-                     f8=(f8, f8.operand_codes(dt) if f8 is not None else None, o8))
+        dt8 = f8.operand_codes(dt) if f8 is not None else None
+        if tconly and dt8 is None:
+            raise RuntimeError("apex.fp8: the codes-only output gradient was not consumed as fp8 codes")
+        dwo = _wgrad_f8(dt, o.view(B * S, E), pwo, f8, dt8, o8, tconly, False)
         q, k, v = qkv.view(B, S, 3, heads, d).unbind(2)
         dqkv = torch.empty_like(qkv)
         dq, dk, dv = dqkv.view(B, S, 3, heads, d).unbind(2)
@@ -325,12 +341,16 @@ class _FFNSublayer(torch.autograd.Function):
         pw1, pb1, pw2, pb2, pg, pb = ctx.params
         dkey = (f8.key_of(w2), "dy") if f8 is not None else None
         q8 = _q8(f8, dkey, f8._bwd, s) if f8 is not None else None
+        # codes only: dt's consumers are the W2 input-gradient GEMM (its epilogue reads gelu'(h) / h)
+        # and the W2 weight gradient
+        tconly = q8 is not None and f8.codes_only_ok(_2d(dy), w2, w2.shape[0], w2.shape[1],
+                                                     aux=h if hb is None and act == ACT_GELU and b1dt is not None else None)
         dres, dt, dgamma, dbeta, db2 = C.bdaln_bwd(_2d(dy), s, gamma, mean, rstd, float(p), seed, off, has_b2,
                                                    dgamma_out=_gt(pg), dbeta_out=_gt(pb),
                                                    dbias_out=_gt(pb2) if has_b2 else None, beta=ctx.ln_beta,
-                                                   s_alt=s_alt, **_q8_kw(q8))
+                                                   s_alt=s_alt, **_q8_kw(q8, tconly))
         if q8 is not None:
-            f8.register(dt, q8[0], q8[4], q8[3])
+            f8.register(dt, q8[0], q8[4], q8[3], codes_only=tconly)
         if hb is None and act == ACT_GELU and b1dt is not None:
             tb1 = _gt(pb1)
             # fp8: the epilogue also writes dh's e5m2 codes for the W1 dgrad (W1's own "dy" slot)
@@ -355,10 +375,9 @@ class _FFNSublayer(torch.autograd.Function):
             dt8 = f8.operand_codes(dt) if f8 is not None else None
             dconly = False
         x8, g8 = ctx.f8codes
-        if ctx.g_conly:
-            dw2 = _wgrad_codes_only(dt, None, pw2, f8, dt8, g8, dt.dtype)
-        else:
-            dw2 = _wgrad(dt, g, param=pw2, f8=(f8, dt8, g8))
+        if tconly and dt8 is None:
+            raise RuntimeError("apex.fp8: the codes-only output gradient was not consumed as fp8 codes")
+        dw2 = _wgrad_f8(dt, g, pw2, f8, dt8, g8, tconly, ctx.g_conly)
         dx = G.dgrad_resid(dh, w1, dres, f8=f8)  # residual grad accumulated in the GEMM epilogue
         dh8 = f8.operand_codes(dh) if f8 is not None else None
         if dconly:

@@ -643,7 +643,7 @@ std::vector<Tensor> k_bdaln_bwd(Tensor dy, Tensor s, Tensor gamma, Tensor mean, 
                                 const c10::optional<Tensor>& ds_extra, const c10::optional<Tensor>& beta,
                                 const c10::optional<Tensor>& q8_out, const c10::optional<Tensor>& q8_scale,
                                 const c10::optional<Tensor>& q8_amax, int64_t q8_fmt,
-                                const c10::optional<Tensor>& s_alt) {
+                                const c10::optional<Tensor>& s_alt, bool q8_only) {
   // beta given: `s` is the LN output y of a store_s = false (or s_cond) forward (x-hat = (y - beta) /
   // gamma); s_alt: the s_cond forward's conditionally stored LN input, read instead when gamma has a 0
   Tensor dyc = dy.contiguous();
@@ -664,6 +664,10 @@ std::vector<Tensor> k_bdaln_bwd(Tensor dy, Tensor s, Tensor gamma, Tensor mean, 
   Tensor dbias = has_bias ? out_or_empty(dbias_out, gamma.sizes(), gamma.options(), "bdaln_bwd dbias") : Tensor();
   Tensor ws = at::empty({apex::bdaln_ws_floats(rows, (int)cols)}, s.options().dtype(at::kFloat));
   auto dp = drop_params(p);
+  apex::Q8Out q8 = q8_args(q8_out, q8_scale, q8_amax, q8_fmt, dx, "bdaln_bwd");
+  // q8_only: dx is allocated but not written (its consumers read the codes alone)
+  TORCH_CHECK(!q8_only || q8.y, "bdaln_bwd: q8_only needs q8_out");
+  q8.only = q8_only ? 1 : 0;
   check(apex::bdaln_bwd(dyc.data_ptr(), s.data_ptr(), gamma.data_ptr(), from_y ? beta->data_ptr() : nullptr,
                         mean.data_ptr<float>(),
                         rstd.data_ptr<float>(), dse.defined() ? dse.data_ptr() : nullptr, dres.data_ptr(),
@@ -671,7 +675,7 @@ std::vector<Tensor> k_bdaln_bwd(Tensor dy, Tensor s, Tensor gamma, Tensor mean, 
                         dbeta.data_ptr(), has_bias ? dbias.data_ptr() : nullptr, ws.data_ptr<float>(), rows,
                         (int)cols, (uint64_t)seed, (uint64_t)offset, dp.first, dp.second,
                         dt_code(s.scalar_type()), dt_code(gamma.scalar_type()), cur_stream(),
-                        q8_args(q8_out, q8_scale, q8_amax, q8_fmt, dx, "bdaln_bwd"),
+                        q8,
                         (from_y && s_alt.has_value() && s_alt->defined() && s_alt->numel() == s.numel())
                             ? s_alt->data_ptr() : nullptr),
         "bdaln_bwd");
@@ -1599,7 +1603,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("p"), py::arg("seed"), py::arg("offset"), py::arg("has_bias"), py::arg("dgamma_out") = py::none(),
         py::arg("dbeta_out") = py::none(), py::arg("dbias_out") = py::none(), py::arg("ds_extra") = py::none(),
         py::arg("beta") = py::none(), py::arg("q8_out") = py::none(), py::arg("q8_scale") = py::none(),
-        py::arg("q8_amax") = py::none(), py::arg("q8_fmt") = 0, py::arg("s_alt") = py::none());
+        py::arg("q8_amax") = py::none(), py::arg("q8_fmt") = 0, py::arg("s_alt") = py::none(),
+        py::arg("q8_only") = false);
   m.def("input_normalize", &k_input_normalize);
   m.def("gemm_supported", &k_gemm_supported);
   m.def("gemm", &k_gemm, py::arg("a"), py::arg("b"), py::arg("epi") = 0, py::arg("bias") = py::none(),

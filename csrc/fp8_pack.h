@@ -77,17 +77,17 @@ __device__ __forceinline__ uint32_t f8_codes4(uint32_t w0, uint32_t w1, float s,
 }
 
 // 8 values stored as 16-bit T (one 16-byte store) plus their codes (one 8-byte store); fmt
-// wave-uniform
+// wave-uniform. store_v = false (wave-uniform; codes-only outputs, Q8Out::only): the codes alone
 template <typename T>
 __device__ __forceinline__ void f8_store_with_codes8(T* dst, uint8_t* cdst, const float (&v)[8], float s, int fmt,
-                                                     float& mx) {
+                                                     float& mx, bool store_v = true) {
   static_assert(sizeof(T) == 2, "16-bit stores");
   struct alignas(16) P8 {
     T v[8];
   } pk;
 #pragma unroll
   for (int i = 0; i < 8; ++i) pk.v[i] = (T)v[i];
-  *reinterpret_cast<P8*>(dst) = pk;
+  if (store_v) *reinterpret_cast<P8*>(dst) = pk;
   const uint4 w = __builtin_bit_cast(uint4, pk);
   uint2 c;
   if (fmt == 0) {

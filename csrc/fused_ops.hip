@@ -442,9 +442,10 @@ __device__ __forceinline__ void bdaln_bwd_body(const T* __restrict__ dy, const T
           dbi[j][k] += ds[k];
         }
         if constexpr (Q8 && sizeof(T) == 2) {  // with the fp8 codes of dx as stored (the dgrad GEMM's operand)
-          f8_store_with_codes8<T>(dx + e, q8.y + e, ds, qs, q8.fmt, mx);
+          // (q8.only: dx's consumers read the codes alone — apex.fp8 codes_only_ok — dx is not stored)
+          f8_store_with_codes8<T>(dx + e, q8.y + e, ds, qs, q8.fmt, mx, !q8.only);
         } else {
-          store_f<T, 8>(dx + e, ds);
+          if (!(Q8 && q8.only)) store_f<T, 8>(dx + e, ds);
           if constexpr (Q8) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) mx = fmaxf(mx, fabsf(ds[k]));

@@ -411,6 +411,15 @@ def test_bdaln_q8_side_output_matches_standalone_quantize(fmt, p):
         dref = C.fp8_quantize(dx, 1 - fmt, scale, damax_ref)
         assert torch.equal(dcodes, dref), from_y
         assert float(damax) == float(damax_ref)
+        # codes only (q8_only: dx not stored): the same codes, amax, dres and parameter gradients
+        ocodes = torch.empty_like(codes)
+        oamax = torch.zeros(1, device=DEV)
+        only = C.bdaln_bwd(dy, sin, g, mean, rstd, p, 11, 3, True, beta=be if from_y else None, q8_out=ocodes,
+                           q8_scale=scale, q8_amax=oamax, q8_fmt=1 - fmt, q8_only=True)
+        assert torch.equal(ocodes, dcodes) and float(oamax) == float(damax)
+        assert torch.equal(only[0], plain[0])
+        for a_, b_ in zip(only[2:], plain[2:]):
+            torch.testing.assert_close(a_, b_, rtol=0, atol=0)
 
 
 @pytest.mark.parametrize("p,S,D", [(0.0, 128, 64), (0.1, 128, 64), (0.1, 96, 64), (0.0, 77, 32), (0.1, 128, 128)])
