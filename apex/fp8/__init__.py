@@ -33,11 +33,11 @@ Producer-side quantisation
   buffer; ``register()`` files the codes under the bf16 tensor; the consuming ``forward_gemm`` /
   ``backward_gemm`` takes them instead of running a standalone quantise pass over that tensor.
   Codes only (``codes_only_ok``, APEX_FP8_CODES_ONLY=0 turns it off): where every consumer of a
-  producer's output reads codes — the MLP's gelu(H) and dH (fp8 GEMM epilogues) and the sublayers'
-  output gradient dt (LayerNorm backward) — the 16-bit output is not stored at all. A weight
-  gradient that still has to run in 16 bits takes the codes' dequantised values. Measured on the
-  BERT-Large step: 152.6 -> 147.0 ms (1.236x -> 1.282x bf16), peak memory 108.8 -> 90.8 GB
-  (profiles/r6_bench_fp8_codes_only_ab.jsonl).
+  producer's output reads codes — the MLP's gelu(H) and dH (fp8 GEMM epilogues), the sublayers'
+  output gradient dt (LayerNorm backward) and the attention input gradient dQKV (flash backward) —
+  the 16-bit output is not stored at all. A weight gradient that still has to run in 16 bits takes
+  the codes' dequantised values. Measured on the BERT-Large step: 152.5 -> 144.2 ms (1.22x ->
+  1.29x bf16), peak memory 108.8 -> 90.8 GB (profiles/r6_bench_fp8_codes_only_ab.jsonl).
 
 Use
   amp:       ``amp.initialize(model, opt, opt_level="O2", fp8=True)`` (or an ``Fp8Recipe``) — the

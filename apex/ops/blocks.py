@@ -268,16 +268,23 @@ class _AttnSublayer(torch.autograd.Function):
         qkey = (f8.key_of(wqkv), "dy") if f8 is not None else None
         q8d = _q8(f8, qkey, f8._bwd, dqkv) if f8 is not None else None
         kw = {}
+        # codes only: dqkv's consumers are the QKV input-gradient GEMM (+ residual) and the QKV weight
+        # gradient (the bias gradient comes from the kernel's own column sums)
+        qconly = q8d is not None and f8.codes_only_ok(_2d(dy), wqkv, wqkv.shape[0], wqkv.shape[1], aux=_2d(dres))
         if q8d is not None:
             cq, ck, cv = q8d[0].view(B, S, 3, heads, d).unbind(2)
-            kw = dict(q8_dq=cq, q8_dk=ck, q8_dv=cv, q8_scale=q8d[1], q8_amax=q8d[2], q8_fmt=q8d[3])
+            kw = dict(q8_dq=cq, q8_dk=ck, q8_dv=cv, q8_scale=q8d[1], q8_amax=q8d[2], q8_fmt=q8d[3], q8_only=qconly)
         written = C.flash_attn_bwd(dctx, q, k, v, o, lse, dq, dk, dv, bool(causal), scale, float(p_attn), sa, oa,
                                    k_lens, dmask, dsum, **kw)
+        qconly = qconly and written  # (the two-kernel backward writes no codes and stores dqkv)
         if q8d is not None and written:
-            f8.register(dqkv, q8d[0], q8d[4], q8d[3])
+            f8.register(dqkv, q8d[0], q8d[4], q8d[3], codes_only=qconly)
         dbqkv = C.partial_colsum(dsum, bdt, _gt(pbqkv)) if has_bqkv else None
         dx = G.dgrad_resid(dqkv, wqkv, dres, f8=f8)  # residual grad accumulated in the GEMM epilogue
-        dwqkv = _wgrad(dqkv, x2, param=pqkv, f8=(f8, f8.operand_codes(dqkv) if f8 is not None else None, x8))
+        dq8 = f8.operand_codes(dqkv) if f8 is not None else None
+        if qconly and dq8 is None:
+            raise RuntimeError("apex.fp8: the codes-only attention input gradient was not consumed as fp8 codes")
+        dwqkv = _wgrad_f8(dqkv, x2, pqkv, f8, dq8, x8, qconly, False)
         return (dx.view(B, S, E), dwqkv, dbqkv, dwo, dbo if has_bo else None, dgamma, dbeta,
                 None, None, None, None, None, None)
 

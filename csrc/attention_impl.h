@@ -1018,9 +1018,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
         const int64_t qoff = b * a.dq_bs + h * a.dq_hs + (int64_t)q * a.dq_ss;
         T* dqp = (T*)a.dq + qoff;
         if constexpr (WIDE) {
+          if (!a.q8only) {
 #pragma unroll
-          for (int t = 0; t < NT; t += 2)
-            *(uint4*)(dqp + (dt0 + t + (lg & 1)) * 16 + 8 * (lg >> 1)) = wd[t / 2];
+            for (int t = 0; t < NT; t += 2)
+              *(uint4*)(dqp + (dt0 + t + (lg & 1)) * 16 + 8 * (lg >> 1)) = wd[t / 2];
+          }
         }
         if (a.q8dq) {  // fp8 codes of dq as stored (the QKV input-gradient GEMM's operand)
           uint32_t cq[NT];
@@ -1040,7 +1042,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
         }
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
-          if constexpr (!WIDE) *(uint2*)(dqp + (dt0 + t) * 16 + 4 * lg) = wq[t];
+          if constexpr (!WIDE) {
+            if (!a.q8only) *(uint2*)(dqp + (dt0 + t) * 16 + 4 * lg) = wq[t];
+          }
           if constexpr (DSUM) {
             const t4 w = __builtin_bit_cast(t4, wq[t]);
 #pragma unroll
@@ -1132,7 +1136,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 6
       const s16x4 lo = lds_tr16(src), hi = lds_tr16(src + 4 * LDE);
       const int key = k0 + kb + (lane & 15);
       const V8 x = join4<V8>(lo, hi);
-      if (key < a.Sk) *(V8*)(dst + (int64_t)key * ss + d0) = x;
+      if (key < a.Sk && !a.q8only) *(V8*)(dst + (int64_t)key * ss + d0) = x;
       if (q8dst) {
         const uint4 ww = __builtin_bit_cast(uint4, x);
         uint2 c;

@@ -423,7 +423,7 @@ bool flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor 
                     const c10::optional<Tensor>& bias, const c10::optional<Tensor>& q8_dq,
                     const c10::optional<Tensor>& q8_dk, const c10::optional<Tensor>& q8_dv,
                     const c10::optional<Tensor>& q8_scale, const c10::optional<Tensor>& q8_amax, int64_t q8_fmt,
-                    const c10::optional<Tensor>& dbias) {
+                    const c10::optional<Tensor>& dbias, bool q8_only) {
   apex::AttnArgs a = attn_common(q, k, v, causal, scale, p_drop, seed, offset, k_lens);
   a.dbg = (int)dbg;
   attn_set_bias(a, bias, q);
@@ -474,6 +474,7 @@ bool flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor 
     a.q8dv = attn_q8(q8_dv, dv, "flash_attn_bwd dv");
     TORCH_CHECK(a.q8dk && a.q8dv, "flash_attn_bwd: q8_dq, q8_dk and q8_dv go together");
     attn_q8_scale(a, q8_scale, q8_amax, q8_fmt, dq);
+    a.q8only = q8_only ? 1 : 0;  // dq / dk / dv allocated, not written: the caller reads their codes alone
     q8 = true;
   }
   check(apex::attn_bwd(a, dout.data_ptr(), delta_ws.defined() ? delta_ws.data_ptr<float>() : nullptr,
@@ -1553,7 +1554,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dmask"), py::arg("dsum") = py::none(), py::arg("dbg") = 0, py::arg("bias") = py::none(),
         py::arg("q8_dq") = py::none(), py::arg("q8_dk") = py::none(), py::arg("q8_dv") = py::none(),
         py::arg("q8_scale") = py::none(), py::arg("q8_amax") = py::none(), py::arg("q8_fmt") = 0,
-        py::arg("dbias") = py::none());
+        py::arg("dbias") = py::none(), py::arg("q8_only") = false);
   m.def("partial_colsum", &k_partial_colsum, py::arg("part"), py::arg("out_dtype"), py::arg("out") = py::none());
   m.def("flash_dropout_mask", &flash_dropout_mask);
   m.def("lse_merge", &k_lse_merge, py::arg("acc_o"), py::arg("acc_lse"), py::arg("o"), py::arg("lse"),

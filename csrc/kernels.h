@@ -119,6 +119,9 @@ struct AttnArgs {
   const float* q8_scale;
   float* q8_amax;
   int q8_fmt;  // 0 = e4m3, 1 = e5m2
+  // backward with q8dq..: dq / dk / dv are NOT stored, only their codes (their consumers, the QKV
+  // input-gradient GEMM and weight gradient, read codes alone: apex.fp8 codes_only_ok)
+  int q8only;
 };
 inline uint32_t attn_drop_thresh(double p) {  // 8-bit keep threshold in [1, 255], 0 = off
   if (p <= 0.0) return 0u;

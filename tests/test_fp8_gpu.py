@@ -461,6 +461,16 @@ def test_flash_attention_fp8_codes_match_standalone_quantize(p, S, D):
     damax_ref = torch.zeros(1, device=DEV)
     assert torch.equal(dcodes, C.fp8_quantize(dqkv, 1, scale, damax_ref))
     assert float(damax) == float(damax_ref)
+    # codes only (q8_only: dq / dk / dv not stored): the same codes and amax, the buffers untouched
+    ocodes = torch.empty_like(dcodes)
+    oamax = torch.zeros(1, device=DEV)
+    dqkv_o = torch.full_like(qkv, 3.0)
+    assert C.flash_attn_bwd(do, q, k, v, o, lse, *dqkv_o.view(B, S, 3, H, D).unbind(2), False, D ** -0.5, p, 3, 4,
+                            None, dmask, q8_dq=ocodes.view(B, S, 3, H, D)[:, :, 0], q8_dk=ocodes.view(B, S, 3, H, D)[:, :, 1],
+                            q8_dv=ocodes.view(B, S, 3, H, D)[:, :, 2], q8_scale=scale, q8_amax=oamax, q8_fmt=1,
+                            q8_only=True)
+    assert torch.equal(ocodes, dcodes) and float(oamax) == float(damax)
+    assert bool((dqkv_o == 3.0).all())
     # a long key range runs the two-kernel backward: no codes, reported as such
     q2, k2, v2 = (torch.randn(2, 256, H, D, device=DEV, dtype=dt) for _ in range(3))
     o2, lse2, dm2 = C.flash_attn_fwd(q2, k2, v2, False, D ** -0.5, 0.0, 0, 0, None)
