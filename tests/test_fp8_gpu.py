@@ -737,3 +737,49 @@ def test_ffn_codes_only_matches_stored_outputs(fp8_off, monkeypatch):
         for a, b in zip(ga, gb):
             rel = float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12))
             assert rel < 0.15, rel
+
+
+def test_codes_only_with_accumulation_and_no_grad(fp8_off, monkeypatch):
+    """Codes-only outputs across two accumulated micro-batches per optimizer step and a no-grad
+    forward in between (inference under fp8): the same gradients as with every output stored."""
+    import apex.fp8 as fp8mod
+    from apex.ops import blocks
+
+    fp8 = fp8_off
+    torch.manual_seed(2)
+    B, S, E, H, F = 4, 128, 256, 4, 1024
+    dt = torch.bfloat16
+    xs = [torch.randn(B, S, E, device=DEV, dtype=dt) for _ in range(2)]
+    mk = lambda *s, sc=0.05: (torch.randn(*s, device=DEV) * sc).to(dt).requires_grad_(True)
+    params = [mk(3 * E, E), mk(3 * E), mk(E, E), mk(E), mk(F, E), mk(F), mk(E, F), mk(E)]
+    params += [(torch.rand(E, device=DEV) + 0.5).to(dt).requires_grad_(True), mk(E),
+               (torch.rand(E, device=DEV) + 0.5).to(dt).requires_grad_(True), mk(E)]
+
+    def run(codes_only):
+        monkeypatch.setattr(fp8mod, "_FP8_CODES_ONLY", "1" if codes_only else "0")
+        fp8.disable()
+        out = []
+        for step in range(3):
+            acc = [torch.zeros_like(p, dtype=torch.float32) for p in params]
+            with fp8.fp8_autocast():
+                wqkv, bqkv, wo, bo, w1, b1, w2, b2, g1, be1, g2, be2 = params
+                for mb, x in enumerate(xs):
+                    h = blocks.attention_sublayer(x, wqkv, bqkv, wo, bo, g1, be1, H)
+                    y = blocks.ffn_sublayer(h, w1, b1, w2, b2, g2, be2)
+                    with torch.no_grad():
+                        y_eval = blocks.ffn_sublayer(h.detach(), w1, b1, w2, b2, g2, be2)
+                    dy = torch.randn(y.shape, device=DEV,
+                                     generator=torch.Generator(device=DEV).manual_seed(10 * step + mb)).to(dt)
+                    for a, g in zip(acc, torch.autograd.grad(y, params, dy)):
+                        a += g.float()
+                out.append(([a.clone() for a in acc], y_eval.float().clone()))
+            fp8.step()
+        fp8.disable()
+        return out
+
+    ref = run(False)
+    got = run(True)
+    for (ga, ya), (gb, yb) in zip(got, ref):
+        torch.testing.assert_close(ya, yb, rtol=0, atol=0)
+        for a, b in zip(ga, gb):
+            torch.testing.assert_close(a, b, rtol=0, atol=0)
