@@ -50,7 +50,9 @@ def parse():
     ap.add_argument("--fp32-microbatch", type=int, default=256)
     ap.add_argument("--layers", type=int, default=24, help="(debug only; the metric needs 24)")
     ap.add_argument("--fp8", action="store_true",
-                    help="extra pass: the same step with amp fp8=True (NOT the headline: reported under extra.fp8)")
+                    help="extra pass: the same step with amp fp8=True (NOT the headline: reported under extra.fp8); "
+                         "on by default for a 1-GPU run")
+    ap.add_argument("--no-fp8", action="store_true", help="skip the default 1-GPU fp8 pass")
     ap.add_argument("--fp8-steps", type=int, default=10)
     ap.add_argument("--fp16", action="store_true",
                     help="extra pass: the same step as amp O2 fp16 with DYNAMIC loss scaling (the reference's O2; "
@@ -231,7 +233,9 @@ def main():
         gc.collect()
         if not rehearsal:
             torch.cuda.empty_cache()
-    if args.fp8 and not args.fp32_only:
+    # the fp8 pass runs by default on one GPU (so the round-end record carries its speedup, not only
+    # builder runs); multi-GPU runs keep it opt-in
+    if (args.fp8 or (world == 1 and not args.no_fp8 and not rehearsal)) and not args.fp32_only:
         # per-tensor scaled fp8 forward / input-gradient GEMMs (apex.fp8): an extension beyond the
         # metric's amp O2 bf16 configuration, so it never replaces the headline value
         from apex import fp8 as _fp8
