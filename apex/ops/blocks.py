@@ -190,6 +190,7 @@ def _wgrad_codes_only(dy2, x2, param, f8, d8, x8, dtype):
         x2 = f8.dequantize(x8, f8._fwd, dtype)
     return _wgrad(dy2, x2, param=param)
 
+
 class _AttnSublayer(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, wqkv, bqkv, wo, bo, gamma, beta, heads, p_attn, p_hidden, eps, causal, k_lens):
